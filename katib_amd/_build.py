@@ -1,0 +1,104 @@
+"""In-tree builders for the native pieces.
+
+* ``_native``  - C++17 runtime (store, parser, supervisor, samplers), g++ + pybind11.
+* ``_hipkern`` - HIP/CDNA4 kernels for gfx950, built with hipcc through
+  ``torch.utils.cpp_extension`` conventions but as an explicit in-tree ``.so`` so
+  the artefact travels with the repo snapshot to the GPU box.
+
+Both builds are incremental: a target is rebuilt only when a source is newer.
+"""
+
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+NATIVE_SRC = os.path.join(PKG_DIR, "csrc", "native")
+HIP_SRC = os.path.join(PKG_DIR, "csrc", "hip")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _newer(target: str, sources) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def native_target() -> str:
+    return os.path.join(PKG_DIR, "_native" + EXT_SUFFIX)
+
+
+def build_native(force: bool = False, verbose: bool = False) -> str:
+    import pybind11
+
+    srcs = sorted(glob.glob(os.path.join(NATIVE_SRC, "*.cpp")))
+    deps = srcs + sorted(glob.glob(os.path.join(NATIVE_SRC, "*.hpp")))
+    out = native_target()
+    if not force and not _newer(out, deps):
+        return out
+    inc = [pybind11.get_include(), sysconfig.get_paths()["include"], NATIVE_SRC]
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-result"]
+    cmd += [f"-I{i}" for i in inc] + srcs + ["-o", out + ".tmp", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def hip_target() -> str:
+    return os.path.join(PKG_DIR, "_hipkern" + EXT_SUFFIX)
+
+
+def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950") -> str:
+    """Compile every ``csrc/hip/*.hip`` kernel file + the torch binding into one .so."""
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    srcs = sorted(glob.glob(os.path.join(HIP_SRC, "*.hip"))) + sorted(glob.glob(os.path.join(HIP_SRC, "*.cpp")))
+    deps = srcs + sorted(glob.glob(os.path.join(HIP_SRC, "*.h")))
+    out = hip_target()
+    if not srcs:
+        return ""
+    if not force and not _newer(out, deps):
+        return out
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    hipcc = os.path.join(rocm, "bin", "hipcc")
+    torch_inc = ce.include_paths()  # torch + torch/csrc/api
+    py_inc = sysconfig.get_paths()["include"]
+    torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    build_dir = os.path.join(PKG_DIR, "csrc", "hip", "build")
+    os.makedirs(build_dir, exist_ok=True)
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={arch}", "-D__HIP_PLATFORM_AMD__=1",
+              "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_hipkern", "-DTORCH_API_INCLUDE_EXTENSION_H",
+              "-D_GLIBCXX_USE_CXX11_ABI=" + str(int(torch._C._GLIBCXX_USE_CXX11_ABI)),
+              "-fno-gpu-rdc", "-Wno-unused-result", "-Wno-deprecated-declarations"]
+    inc = [f"-I{p}" for p in torch_inc + [py_inc, HIP_SRC]]
+    objs = []
+    for s in srcs:
+        o = os.path.join(build_dir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + sorted(glob.glob(os.path.join(HIP_SRC, "*.h")))):
+            lang = ["-x", "hip"] if s.endswith(".hip") else []
+            cmd = [hipcc] + common + inc + lang + ["-c", s, "-o", o]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.check_call(cmd)
+    link = [hipcc, "-shared", "-fPIC", f"--offload-arch={arch}"] + objs + [
+        f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+        f"-Wl,-rpath,{torch_lib}", "-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(link), file=sys.stderr)
+    subprocess.check_call(link)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+if __name__ == "__main__":
+    print(build_native(verbose=True))
+    print(build_hip(verbose=True))

@@ -1,0 +1,251 @@
+"""Trial "jobs" on a single MI355X node.
+
+A trial's ``runSpec`` (the rendered trial template) is turned into a
+:class:`LaunchPlan` - one or more local processes - instead of a Kubernetes
+object. Supported kinds:
+
+* ``batch/v1 Job`` - the primary container's ``command``/``args``/``env``/
+  ``workingDir``; ``resources.limits`` ``amd.com/gpu`` (or ``nvidia.com/gpu``)
+  selects the GPU count; ``activeDeadlineSeconds`` and an explicit
+  ``backoffLimit`` are honoured.
+* Kubeflow training jobs (``PyTorchJob``, ``TFJob``, ``XGBoostJob``, ``MXJob``,
+  ``MPIJob``): one process per replica, wired with ``MASTER_ADDR=127.0.0.1``,
+  ``MASTER_PORT``, ``WORLD_SIZE``, ``RANK``, ``LOCAL_RANK`` (torch.distributed over
+  RCCL) or ``TF_CONFIG``; metrics come from the primary replica selected by
+  ``primaryPodLabels`` (master/chief/launcher), mirroring the reference's
+  primary-pod semantics (``inject_webhook.go:143-148``).
+* ``LocalProcess`` (native kind, ``apiVersion: katib-amd.io/v1``): ``command`` for
+  a subprocess or ``entrypoint: module:function`` to run in a warm GPU worker.
+* ``Function``: SDK ``tune()`` objective source executed in a warm worker.
+
+The job status handed to the GJSON success/failure conditions is synthesised in
+the shape of the corresponding Kubernetes status (``status.conditions[]``).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import socket
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+from ..api import constants as C
+
+GPU_RESOURCE_KEYS = ("amd.com/gpu", "nvidia.com/gpu", "gpu")
+
+_REPLICA_KEYS = {
+    "PyTorchJob": ("pytorchReplicaSpecs", ["Master", "Worker"]),
+    "TFJob": ("tfReplicaSpecs", ["Chief", "Master", "Worker", "PS", "Evaluator"]),
+    "XGBoostJob": ("xgbReplicaSpecs", ["Master", "Worker"]),
+    "MXJob": ("mxReplicaSpecs", ["Scheduler", "Server", "Worker", "Tuner", "TunerServer", "TunerTracker"]),
+    "MPIJob": ("mpiReplicaSpecs", ["Launcher", "Worker"]),
+}
+_PRIMARY_ROLE = {"PyTorchJob": "Master", "TFJob": "Chief", "XGBoostJob": "Master", "MXJob": "Scheduler",
+                 "MPIJob": "Launcher"}
+
+
+@dataclass
+class ReplicaPlan:
+    role: str
+    index: int
+    argv: List[str]
+    env: Dict[str, str]
+    cwd: Optional[str]
+    gpus: int
+    primary: bool
+    entrypoint: Optional[str] = None  # "module:function" for warm-worker execution
+    function: Optional[Dict] = None  # {"source":..., "entry":..., "params": {...}}
+
+
+@dataclass
+class LaunchPlan:
+    kind: str
+    replicas: List[ReplicaPlan] = field(default_factory=list)
+    deadline: float = 0.0
+    backoff_limit: int = 0
+
+    @property
+    def primary(self) -> ReplicaPlan:
+        for r in self.replicas:
+            if r.primary:
+                return r
+        return self.replicas[0]
+
+    @property
+    def total_gpus(self) -> int:
+        return sum(r.gpus for r in self.replicas)
+
+
+class JobSpecError(ValueError):
+    pass
+
+
+def _gpus(container: Dict) -> int:
+    res = container.get("resources") or {}
+    for section in ("limits", "requests"):
+        sec = res.get(section) or {}
+        for k in GPU_RESOURCE_KEYS:
+            if k in sec:
+                try:
+                    return int(sec[k])
+                except (TypeError, ValueError):
+                    return 1
+    return 0
+
+
+def _env(container: Dict) -> Dict[str, str]:
+    out = {}
+    for e in container.get("env") or []:
+        if "value" in e and e.get("name"):
+            out[e["name"]] = str(e["value"])
+    return out
+
+
+def _container(pod_spec: Dict, primary_name: str) -> Dict:
+    cs = pod_spec.get("containers") or []
+    if not cs:
+        raise JobSpecError("pod template has no containers")
+    for c in cs:
+        if c.get("name") == primary_name:
+            return c
+    return cs[0]
+
+
+def _argv(c: Dict) -> List[str]:
+    cmd = list(c.get("command") or []) + list(c.get("args") or [])
+    if not cmd:
+        raise JobSpecError("container %r has no command: image ENTRYPOINT lookup is not available on a "
+                           "node-local scheduler; set command/args explicitly" % c.get("name"))
+    return [str(a) for a in cmd]
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Optional[Dict[str, str]] = None) -> LaunchPlan:
+    kind = run_spec.get("kind", "")
+    spec = run_spec.get("spec") or {}
+    if kind == C.JOB_KIND_JOB:
+        pod = (spec.get("template") or {}).get("spec") or {}
+        c = _container(pod, primary_container)
+        plan = LaunchPlan(kind=kind, deadline=float(spec.get("activeDeadlineSeconds") or 0),
+                          backoff_limit=int(spec["backoffLimit"]) if "backoffLimit" in spec else 0)
+        plan.replicas.append(ReplicaPlan("primary", 0, _argv(c), _env(c), c.get("workingDir"), _gpus(c), True))
+        return plan
+    if kind == C.JOB_KIND_LOCAL:
+        plan = LaunchPlan(kind=kind, deadline=float(spec.get("activeDeadlineSeconds") or 0),
+                          backoff_limit=int(spec.get("backoffLimit") or 0))
+        env = {e["name"]: str(e["value"]) for e in spec.get("env") or [] if "value" in e}
+        args = [str(a) for a in spec.get("args") or []]
+        gpus = int(spec.get("gpus") or 0)
+        if spec.get("entrypoint"):
+            plan.replicas.append(ReplicaPlan("primary", 0, args, env, spec.get("workingDir"), gpus, True,
+                                             entrypoint=spec["entrypoint"]))
+        else:
+            cmd = [str(a) for a in spec.get("command") or []] + args
+            if not cmd:
+                raise JobSpecError("LocalProcess needs spec.command or spec.entrypoint")
+            plan.replicas.append(ReplicaPlan("primary", 0, cmd, env, spec.get("workingDir"), gpus, True))
+        return plan
+    if kind == "Function":
+        plan = LaunchPlan(kind=kind, deadline=float(spec.get("activeDeadlineSeconds") or 0))
+        env = {e["name"]: str(e["value"]) for e in spec.get("env") or [] if "value" in e}
+        plan.replicas.append(ReplicaPlan("primary", 0, [], env, spec.get("workingDir"), int(spec.get("gpus") or 0),
+                                         True, function={"source": spec.get("source", ""),
+                                                         "entry": spec.get("entry", ""),
+                                                         "params": spec.get("params", {}),
+                                                         "packages": spec.get("packages", [])}))
+        return plan
+    if kind in _REPLICA_KEYS:
+        key, roles = _REPLICA_KEYS[kind]
+        rspecs = spec.get(key) or {}
+        if not rspecs:
+            raise JobSpecError("%s has no %s" % (kind, key))
+        plan = LaunchPlan(kind=kind, deadline=float((spec.get("runPolicy") or {}).get("activeDeadlineSeconds")
+                                                    or spec.get("activeDeadlineSeconds") or 0))
+        primary_role = _PRIMARY_ROLE[kind]
+        if kind == "TFJob" and "Chief" not in rspecs and "Master" in rspecs:
+            primary_role = "Master"
+        ordered = [r for r in roles if r in rspecs] + [r for r in rspecs if r not in roles]
+        if primary_role not in rspecs:
+            primary_role = ordered[0]
+        world = sum(int(rspecs[r].get("replicas", 1)) for r in ordered
+                    if not (kind == "MPIJob" and r == "Launcher"))
+        port = free_port()
+        rank = 0
+        cluster = {}
+        for role in ordered:
+            n = int(rspecs[role].get("replicas", 1))
+            cluster[role.lower()] = ["127.0.0.1:%d" % (port + 1 + len(cluster) * 64 + i) for i in range(n)]
+        for role in ordered:
+            rs = rspecs[role]
+            pod = ((rs.get("template") or {}).get("spec")) or {}
+            c = _container(pod, primary_container)
+            n = int(rs.get("replicas", 1))
+            for i in range(n):
+                env = _env(c)
+                if kind in ("PyTorchJob", "XGBoostJob"):
+                    env.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
+                                "RANK": str(rank), "LOCAL_RANK": str(rank), "PET_NNODES": str(world)})
+                elif kind == "TFJob":
+                    env["TF_CONFIG"] = json.dumps({"cluster": cluster, "task": {"type": role.lower(), "index": i}})
+                elif kind == "MXJob":
+                    env.update({"DMLC_ROLE": role.lower(), "DMLC_PS_ROOT_URI": "127.0.0.1",
+                                "DMLC_PS_ROOT_PORT": str(port)})
+                is_primary = role == primary_role and i == 0
+                if kind == "MPIJob" and role == "Worker":
+                    continue  # mpirun in the launcher spawns the workers itself
+                plan.replicas.append(ReplicaPlan(role.lower(), i, _argv(c), env, c.get("workingDir"), _gpus(c),
+                                                 is_primary))
+                rank += 1
+        return plan
+    raise JobSpecError("unsupported trial kind %r (supported: Job, %s, LocalProcess, Function)"
+                       % (kind, ", ".join(_REPLICA_KEYS)))
+
+
+def job_status(kind: str, phase: str, reason: str = "", message: str = "") -> Dict:
+    """phase: Created | Running | Succeeded | Failed."""
+    conds = []
+    if kind in _REPLICA_KEYS:
+        conds.append({"type": "Created", "status": "True"})
+        if phase in ("Running", "Succeeded", "Failed"):
+            conds.append({"type": "Running", "status": "True" if phase == "Running" else "False"})
+        if phase == "Succeeded":
+            conds.append({"type": "Succeeded", "status": "True", "reason": reason, "message": message})
+        if phase == "Failed":
+            conds.append({"type": "Failed", "status": "True", "reason": reason, "message": message})
+        return {"status": {"conditions": conds}}
+    st = {"active": 1 if phase == "Running" else 0, "succeeded": 1 if phase == "Succeeded" else 0,
+          "failed": 1 if phase == "Failed" else 0}
+    if phase == "Succeeded":
+        conds.append({"type": "Complete", "status": "True", "reason": reason, "message": message})
+    elif phase == "Failed":
+        conds.append({"type": "Failed", "status": "True", "reason": reason, "message": message})
+    st["conditions"] = conds
+    return {"status": st}
+
+
+def map_paths(values: List[str], mapping: Dict[str, str]) -> List[str]:
+    out = []
+    for v in values:
+        for src, dst in mapping.items():
+            if src and src in v:
+                v = v.replace(src, dst)
+        out.append(v)
+    return out
+
+
+def path_mapping(trial_dir: str, paths: List[str]) -> Dict[str, str]:
+    """Absolute collector paths (``/var/log/katib/...``) are remapped under the
+    trial directory so concurrent trials never share a metrics file."""
+    mapping = {}
+    for p in paths:
+        if p and os.path.isabs(p):
+            d = p.rstrip("/")
+            mapping[d] = os.path.join(trial_dir, "fs") + d
+    # longest first so nested paths map correctly
+    return dict(sorted(mapping.items(), key=lambda kv: -len(kv[0])))
