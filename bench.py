@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DARTS CIFAR-10 search wall-clock (BASELINE.md B5 / BASELINE.json config 4).
+
+Runs the flagship workload - one full DARTS search step (second-order architect:
+5 forward + 5 backward passes, Adam on alphas, clipped SGD on weights) - on N
+GPUs of one node, one process per GPU (torchrun env; RCCL all-reduce of the
+flat gradient buffers). Times exactly ``--steps`` steps after ``--warmup``
+untimed steps, bracketed by barrier + synchronize, MAX over ranks, then projects
+the reference's end-to-end search: ``epochs x (steps/epoch x step time +
+validation pass)`` with the B5 config (C=4, L=2, N=3, stem x1, 6 primitives +
+none, batch 128 per GPU, 25k/25k split, 2 epochs) unless ``--config default``
+(darts-gpu.yaml: C=16, L=3, N=4, stem x3).
+
+Lower is better; vs_baseline = value / 282 s (B5, 1x NVIDIA GPU, end to end).
+Data: synthetic CIFAR-10-shaped tensors resident in HBM, random-init weights.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+B5_SECONDS = 282.0
+PRIMS = ["separable_convolution_3x3", "dilated_convolution_3x3", "dilated_convolution_5x5", "avg_pooling_3x3",
+         "max_pooling_3x3", "skip_connection"]
+CONFIGS = {
+    "b5": dict(init_channels=4, num_layers=2, num_nodes=3, stem_multiplier=1, epochs=2),
+    "default": dict(init_channels=16, num_layers=3, num_nodes=4, stem_multiplier=3, epochs=3),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="b5", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=128, help="per-GPU batch")
+    ap.add_argument("--capture", type=int, default=1)
+    ap.add_argument("--ops", default=os.environ.get("KATIB_AMD_DARTS_OPS", "hip"))
+    ap.add_argument("--valid-batches", type=int, default=10)
+    args = ap.parse_args()
+
+    import torch
+
+    from katib_amd.models.darts import DartsLayout
+    from katib_amd.models.darts_search import DartsSearch
+    from katib_amd.ops import darts as dops
+    from katib_amd.parallel.comm import Comm
+    from katib_amd.workloads.data import cifar10
+
+    comm = Comm.from_env()
+    dev = comm.device
+    if dev.type == "cuda" and args.ops == "hip":
+        try:
+            dops.set_backend("hip")
+            from katib_amd.ops import hip_darts  # noqa: F401  (fails loudly if the extension is missing)
+        except Exception as e:
+            if comm.rank == 0:
+                print("hip ops unavailable (%s); using torch ops" % e, file=sys.stderr)
+            dops.set_backend("torch")
+            args.ops = "torch"
+    cfg = CONFIGS[args.config]
+    layout = DartsLayout(PRIMS, init_channels=cfg["init_channels"], num_layers=cfg["num_layers"],
+                         num_nodes=cfg["num_nodes"], stem_multiplier=cfg["stem_multiplier"])
+    search = DartsSearch(layout, dev, comm, capture=bool(args.capture) and dev.type == "cuda")
+    n_train = 50000
+    ds = cifar10(dev, n=n_train)
+    train, valid = ds.subset(0, n_train // 2), ds.subset(n_train // 2, n_train)
+    bs = args.batch
+    tb = train.batches(bs, seed=0, shard=comm.rank, num_shards=comm.world_size, drop_last=True)
+    vb = valid.batches(bs, seed=1, shard=comm.rank, num_shards=comm.world_size, drop_last=True)
+    batches = []
+    for i, (t, v) in enumerate(zip(tb, vb)):
+        batches.append((t, v))
+        if len(batches) >= 16:
+            break
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        (tx, ty), (vx, vy) = batches[i % len(batches)]
+        search.step(tx, ty, vx, vy)
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        (tx, ty), (vx, vy) = batches[i % len(batches)]
+        search.step(tx, ty, vx, vy)
+    sync()
+    comm.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    ms_step = comm.allreduce_max(dt * 1000.0 / args.steps)
+    loss = float(search.loss_out)
+
+    # validation pass cost (no_grad forward, BN in eval mode) -- part of every search epoch
+    vbatches = [v for _, v in batches][: args.valid_batches]
+    for vx, vy in vbatches[:2]:
+        search.evaluate(vx, vy)
+    sync()
+    t1 = time.perf_counter()
+    for vx, vy in vbatches:
+        search.evaluate(vx, vy)
+    sync()
+    ms_valid = comm.allreduce_max((time.perf_counter() - t1) * 1000.0 / max(len(vbatches), 1))
+
+    steps_per_epoch = math.ceil((n_train // 2) / (bs * comm.world_size))
+    epoch_s = steps_per_epoch * ms_step / 1000.0 + steps_per_epoch * ms_valid / 1000.0
+    wall = cfg["epochs"] * epoch_s
+    if comm.rank == 0:
+        out = {
+            "metric": "darts_cifar10_search_wall_clock_s",
+            "value": round(wall, 3),
+            "unit": "s",
+            "n_gpus": comm.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": round(wall / B5_SECONDS, 5) if args.config == "b5" else None,
+            "dtype": "fp32",
+            "data": "synthetic (CIFAR-10-shaped, device-resident); random-init weights",
+            "config": {"model": "darts-cnn-cifar10 supernet (%s: C=%d, L=%d, N=%d, stem x%d, 6 primitives + none)"
+                                % (args.config, cfg["init_channels"], cfg["num_layers"], cfg["num_nodes"],
+                                   cfg["stem_multiplier"]),
+                       "global_batch": bs * comm.world_size, "seq_len": None,
+                       "parallelism": "dp%d" % comm.world_size, "epochs": cfg["epochs"],
+                       "steps_per_epoch": steps_per_epoch, "ops": args.ops, "hip_graph": bool(search.capture),
+                       "second_order": True},
+            "ms_valid_batch": round(ms_valid, 4),
+            "train_images_per_s": round(bs * comm.world_size * 1000.0 / ms_step, 1),
+            "final_loss": round(loss, 4),
+            "baseline_b5_s": B5_SECONDS,
+        }
+        print(json.dumps(out), flush=True)
+    comm.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,248 @@
+// torch bindings for the DARTS HIP kernels (module katib_amd._hipkern).
+// Every entry point validates shapes/dtypes/devices against what the kernel's grid
+// and LDS layout assume before launching on the current HIP stream (graph-capture safe:
+// no allocation, no synchronisation here).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "darts_ops.h"
+
+using namespace katib_hip;
+using at::Tensor;
+using OptT = c10::optional<Tensor>;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_f32(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+template <typename T>
+T* ptr_or_null(const OptT& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
+}
+
+// bn tuple: (sums: Optional[f64 tensor], rmean, rvar, inv_count, eval, eps)
+BNRef make_bn(const py::tuple& b, int C) {
+  BNRef r{};
+  OptT sums = b[0].cast<OptT>(), rm = b[1].cast<OptT>(), rv = b[2].cast<OptT>();
+  if (sums.has_value() && sums->defined()) {
+    TORCH_CHECK(sums->scalar_type() == at::kDouble && sums->numel() >= 2 * C, "bn sums must be f64 [2C]");
+  }
+  r.sums = ptr_or_null<double>(sums);
+  r.rmean = ptr_or_null<float>(rm);
+  r.rvar = ptr_or_null<float>(rv);
+  r.inv_count = b[3].cast<float>();
+  r.eval = b[4].cast<bool>() ? 1 : 0;
+  r.eps = b[5].cast<float>();
+  r.C = C;
+  TORCH_CHECK(r.eval ? (r.rmean && r.rvar) : (r.sums != nullptr), "bn reference lacks its statistics");
+  return r;
+}
+
+// grad source tuple: (g, z, S1 (f64 view [C]), S2 (f64 view [C]), bn tuple, w: Optional, widx)
+GradSrc make_gs(const py::tuple& t, int C) {
+  GradSrc g{};
+  Tensor gt = t[0].cast<Tensor>(), zt = t[1].cast<Tensor>();
+  check_f32(gt, "g");
+  check_f32(zt, "z");
+  g.g = gt.data_ptr<float>();
+  g.z = zt.data_ptr<float>();
+  OptT s1 = t[2].cast<OptT>(), s2 = t[3].cast<OptT>();
+  g.S1 = ptr_or_null<double>(s1);
+  g.S2 = ptr_or_null<double>(s2);
+  g.bn = make_bn(t[4].cast<py::tuple>(), C);
+  g.eval = g.bn.eval;
+  TORCH_CHECK(g.eval || (g.S1 && g.S2), "training-mode BN backward needs S1/S2 reductions");
+  OptT w = t[5].cast<OptT>();
+  g.w = ptr_or_null<float>(w);
+  g.widx = t[6].cast<int>();
+  return g;
+}
+
+int pick_chunk(int C, int per_channel_floats, int fixed_floats) {
+  // keep dynamic LDS <= 64 KB so several blocks stay resident per CU
+  const int budget = 16384 - fixed_floats;
+  int ch = C;
+  while (ch > 1 && ch * per_channel_floats > budget) ch = (ch + 1) / 2;
+  return std::max(ch, 1);
+}
+
+void dwpw_fwd(Tensor x, Tensor dw, Tensor pw, int64_t K, int64_t dil, int64_t S, int64_t pad,
+              c10::optional<py::tuple> inbn, Tensor d, Tensor z, OptT stats, bool use_mfma) {
+  check_f32(x, "x"); check_f32(dw, "dw"); check_f32(pw, "pw"); check_f32(d, "d"); check_f32(z, "z");
+  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Ho = z.size(2), Wo = z.size(3);
+  TORCH_CHECK(dw.numel() == C * K * K && pw.numel() == C * C, "weight shapes");
+  TORCH_CHECK(z.size(0) == N && z.size(1) == C && d.sizes() == z.sizes(), "output shapes");
+  TORCH_CHECK(64 % Wo == 0 && Ho % (64 / Wo) == 0, "tile constraint: 64 % Wo == 0 and Ho % (64/Wo) == 0");
+  TORCH_CHECK(C <= kMaxC, "C too large");
+  TORCH_CHECK(Ho == (H + 2 * pad - dil * (K - 1) - 1) / S + 1, "output height mismatch");
+  DwPwFwdArgs a{};
+  a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.pw = pw.data_ptr<float>();
+  a.d = d.data_ptr<float>(); a.z = z.data_ptr<float>(); a.stats = ptr_or_null<double>(stats);
+  if (a.stats) TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= 2 * C, "stats f64 [2C]");
+  a.N = N; a.C = C; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.pad = pad;
+  const int TR = 64 / Wo;
+  const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
+  a.chunk = pick_chunk(C, IR * IW, C * 64 + 2 * C);
+  a.use_mfma = (use_mfma && C % 16 == 0) ? 1 : 0;
+  bool prebn = inbn.has_value();
+  if (prebn) a.inbn = make_bn(*inbn, C);
+  launch_dwpw_fwd(a, K, dil, S, prebn, cur_stream());
+}
+
+void pw_fwd(Tensor x, Tensor pw, Tensor z, OptT stats, int64_t co_off, int64_t S, int64_t off) {
+  check_f32(x, "x"); check_f32(pw, "pw"); check_f32(z, "z");
+  const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int Cout = pw.size(0), Ho = z.size(2), Wo = z.size(3);
+  TORCH_CHECK(pw.size(1) == Cin && co_off + Cout <= z.size(1) && z.size(0) == N, "pw shapes");
+  TORCH_CHECK((Ho * Wo) % 64 == 0, "Ho*Wo must be a multiple of 64");
+  TORCH_CHECK(Cin <= kMaxC && Cout <= kMaxC, "channels");
+  PwFwdArgs a{};
+  a.x = x.data_ptr<float>(); a.pw = pw.data_ptr<float>(); a.z = z.data_ptr<float>();
+  a.stats = ptr_or_null<double>(stats);
+  a.N = N; a.Cin = Cin; a.Cout = Cout; a.CoutTotal = z.size(1); a.co_off = co_off;
+  a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off;
+  launch_pw_fwd(a, cur_stream());
+}
+
+void pool_fwd(Tensor x, Tensor zavg, Tensor zmax, OptT sa, OptT sm, int64_t S) {
+  check_f32(x, "x"); check_f32(zavg, "zavg"); check_f32(zmax, "zmax");
+  PoolFwdArgs a{};
+  a.x = x.data_ptr<float>(); a.zavg = zavg.data_ptr<float>(); a.zmax = zmax.data_ptr<float>();
+  a.stats_avg = ptr_or_null<double>(sa); a.stats_max = ptr_or_null<double>(sm);
+  a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = zavg.size(2); a.Wo = zavg.size(3);
+  TORCH_CHECK(a.Ho == (a.H - 1) / S + 1 && zmax.sizes() == zavg.sizes(), "pool shapes");
+  launch_pool_fwd(a, S, cur_stream());
+}
+
+void combine_fwd(std::vector<Tensor> zs, std::vector<py::tuple> bns, std::vector<int64_t> widx, OptT w,
+                 int64_t id_idx, OptT xid, OptT gamma, OptT beta, Tensor out, double momentum, bool update_running,
+                 bool accumulate, std::vector<py::tuple> upd) {
+  check_f32(out, "out");
+  TORCH_CHECK(zs.size() == bns.size() && zs.size() == widx.size() && (int)zs.size() <= kMaxOps, "ops");
+  CombineFwdArgs a{};
+  a.N = out.size(0); a.C = out.size(1); a.HW = out.size(2) * out.size(3);
+  TORCH_CHECK(a.C <= kMaxC, "C too large");
+  a.nops = zs.size();
+  for (size_t k = 0; k < zs.size(); ++k) {
+    check_f32(zs[k], "z");
+    TORCH_CHECK(zs[k].sizes() == out.sizes(), "combine input shape");
+    a.z[k] = zs[k].data_ptr<float>();
+    a.bn[k] = make_bn(bns[k], a.C);
+    a.widx[k] = widx[k];
+  }
+  TORCH_CHECK((int)upd.size() <= kMaxOps, "too many update-only BN layers");
+  a.nupd = upd.size();
+  for (size_t k = 0; k < upd.size(); ++k) a.upd[k] = make_bn(upd[k], a.C);
+  a.w = ptr_or_null<float>(w); a.id_idx = id_idx; a.xid = ptr_or_null<float>(xid);
+  if (a.xid) TORCH_CHECK(xid->sizes() == out.sizes(), "identity shape");
+  a.gamma = ptr_or_null<float>(gamma); a.beta = ptr_or_null<float>(beta);
+  a.out = out.data_ptr<float>(); a.momentum = momentum; a.update_running = update_running;
+  a.accumulate = accumulate;
+  launch_combine_fwd(a, cur_stream());
+}
+
+void combine_bwd_reduce(Tensor dout, std::vector<Tensor> zs, std::vector<py::tuple> bns, OptT xid, Tensor red,
+                        std::vector<int64_t> widx, int64_t id_idx, OptT gw) {
+  check_f32(dout, "dout");
+  TORCH_CHECK(red.scalar_type() == at::kDouble, "red must be f64");
+  CombineBwdArgs a{};
+  a.N = dout.size(0); a.C = dout.size(1); a.HW = dout.size(2) * dout.size(3);
+  a.nops = zs.size();
+  TORCH_CHECK(a.nops <= kMaxOps && red.numel() >= (a.nops + 1) * a.C + 1, "red size");
+  for (int k = 0; k < a.nops; ++k) {
+    TORCH_CHECK(zs[k].sizes() == dout.sizes(), "z shape");
+    a.z[k] = zs[k].data_ptr<float>();
+    a.bn[k] = make_bn(bns[k], a.C);
+  }
+  a.dout = dout.data_ptr<float>(); a.xid = ptr_or_null<float>(xid); a.red = red.data_ptr<double>();
+  a.gw = ptr_or_null<double>(gw); a.id_idx = id_idx;
+  if (a.gw) {
+    TORCH_CHECK(gw->scalar_type() == at::kDouble, "gw must be f64");
+    TORCH_CHECK((int)widx.size() == a.nops, "widx per op");
+    for (int k = 0; k < a.nops; ++k) {
+      TORCH_CHECK(widx[k] >= 0 && widx[k] < gw->numel(), "widx out of range");
+      a.widx[k] = widx[k];
+    }
+    TORCH_CHECK(id_idx < gw->numel(), "id_idx out of range");
+  }
+  launch_combine_bwd_reduce(a, cur_stream());
+}
+
+void pw_bwd(py::tuple gs, Tensor pw, OptT ain, Tensor x, OptT dd, OptT gx, OptT gW, int64_t co_off,
+            int64_t S, int64_t off, int64_t mode, bool need_dx) {
+  check_f32(pw, "pw"); check_f32(x, "x");
+  PwBwdArgs a{};
+  const int Cout = pw.size(0), Cin = pw.size(1);
+  Tensor g = gs[0].cast<Tensor>();
+  a.N = g.size(0); a.CoutTotal = g.size(1); a.Ho = g.size(2); a.Wo = g.size(3);
+  a.gs = make_gs(gs, a.CoutTotal);
+  a.Cin = Cin; a.Cout = Cout; a.co_off = co_off; a.S = S; a.off = off; a.mode = mode;
+  a.need_dx = need_dx;
+  a.H = x.size(2); a.W = x.size(3);
+  TORCH_CHECK(Cin * Cout <= 4096, "pw_bwd supports Cin*Cout <= 4096");
+  TORCH_CHECK((a.Ho * a.Wo) % 64 == 0, "Ho*Wo % 64");
+  a.pw = pw.data_ptr<float>(); a.x = x.data_ptr<float>();
+  a.ain = ptr_or_null<float>(ain); a.dd = ptr_or_null<float>(dd); a.gx = ptr_or_null<float>(gx);
+  a.gW = ptr_or_null<float>(gW);
+  if (mode == 0) {
+    TORCH_CHECK(a.ain && (!need_dx || a.dd), "mode 0 needs ain (and dd)");
+  } else {
+    TORCH_CHECK(!need_dx || a.gx, "mode 1 needs gx");
+  }
+  if (a.gW) TORCH_CHECK(gW->numel() == Cin * Cout, "gW size");
+  launch_pw_bwd(a, cur_stream());
+}
+
+void dw_bwd(Tensor x, c10::optional<py::tuple> inbn, Tensor dw, Tensor dd, Tensor gout, OptT gW, OptT red,
+            int64_t K, int64_t dil, int64_t S, int64_t pad) {
+  check_f32(x, "x"); check_f32(dw, "dw"); check_f32(dd, "dd"); check_f32(gout, "gout");
+  DwBwdArgs a{};
+  a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = dd.size(2); a.Wo = dd.size(3);
+  TORCH_CHECK(64 % a.Wo == 0 && a.Ho % (64 / a.Wo) == 0, "tile constraint");
+  TORCH_CHECK(a.H == a.Ho * S && a.W == a.Wo * S, "dw_bwd needs H == Ho*S");
+  TORCH_CHECK(gout.sizes() == x.sizes(), "gout shape");
+  a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.dd = dd.data_ptr<float>();
+  a.gout = gout.data_ptr<float>(); a.gW = ptr_or_null<float>(gW); a.red = ptr_or_null<double>(red);
+  a.pad = pad;
+  const int TR = 64 / a.Wo, r = (K - 1) / 2 * dil, h = (r + S - 1) / S, OR = TR + 2 * h;
+  const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (a.Wo - 1) * S + (K - 1) * dil + 1;
+  a.chunk = pick_chunk(a.C, OR * a.Wo + IR * IW + 2, 2 * a.C);
+  bool prebn = inbn.has_value();
+  if (prebn) a.inbn = make_bn(*inbn, a.C);
+  launch_dw_bwd(a, K, dil, S, prebn, cur_stream());
+}
+
+void pool_bwd(c10::optional<py::tuple> ga, c10::optional<py::tuple> gm, Tensor x, OptT dout_id, OptT w,
+              int64_t id_idx, Tensor gx, int64_t S) {
+  check_f32(x, "x"); check_f32(gx, "gx");
+  PoolBwdArgs a{};
+  a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3);
+  a.Ho = (a.H - 1) / S + 1; a.Wo = (a.W - 1) / S + 1;
+  if (ga.has_value()) a.ga = make_gs(*ga, a.C);
+  if (gm.has_value()) a.gm = make_gs(*gm, a.C);
+  a.x = x.data_ptr<float>(); a.dout_id = ptr_or_null<float>(dout_id); a.w = ptr_or_null<float>(w);
+  a.id_idx = id_idx; a.gx = gx.data_ptr<float>();
+  launch_pool_bwd(a, S, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, fused optimizers)";
+  m.def("dwpw_fwd", &dwpw_fwd);
+  m.def("pw_fwd", &pw_fwd);
+  m.def("pool_fwd", &pool_fwd);
+  m.def("combine_fwd", &combine_fwd);
+  m.def("combine_bwd_reduce", &combine_bwd_reduce);
+  m.def("pw_bwd", &pw_bwd);
+  m.def("dw_bwd", &dw_bwd);
+  m.def("pool_bwd", &pool_bwd);
+}

@@ -1,0 +1,711 @@
+// DARTS supernet edge kernels for CDNA4 (gfx950), fp32 NCHW.
+//
+// One MixedOp edge (reference operations.py:164-180) costs ~100+ tiny kernels
+// through PyTorch/MIOpen at C=4..64 channels (per-sample im2col loops, 50-80 us
+// BN reductions over 4 channels). Here an edge is ~7 forward / ~12 backward
+// launches:
+//
+//   dwpw_fwd    ReLU (or BN-apply+ReLU of the previous stage) -> depthwise KxK
+//               (stride, dilation) -> pointwise 1x1, input tile + halo staged in
+//               LDS, depthwise result kept in LDS, pointwise on MFMA
+//               (v_mfma_f32_16x16x4_f32) when C % 16 == 0, per-channel BN
+//               statistics (sum, sum of squares) reduced in-wave and added with
+//               one fp64 atomic per channel per wave.
+//   pool_fwd    avg (count_include_pad=False) + max 3x3 in one pass + stats.
+//   pw_fwd      ReLU -> 1x1 conv (StdConv / FactorizedReduce halves) + stats.
+//   combine_fwd out = sum_k w_k * BN_k(z_k) + w_id * x, running-stat update.
+//   *_bwd       BN backward evaluated on the fly from the reductions of
+//               combine_bwd_reduce, pointwise-transpose, transposed depthwise,
+//               weight gradients accumulated into the flat gradient buffer with
+//               float atomics (one per weight per block).
+//
+// All shapes are checked on the host (darts_bind.cpp) before launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+
+#include "darts_ops.h"
+
+namespace katib_hip {
+
+__device__ __forceinline__ void bn_coeffs(const BNRef& b, int c, float& mean, float& invstd) {
+  if (b.eval) {
+    mean = b.rmean[c];
+    invstd = rsqrtf(b.rvar[c] + b.eps);
+  } else {
+    double m = b.sums[c] * (double)b.inv_count;
+    double v = b.sums[b.C + c] * (double)b.inv_count - m * m;
+    if (v < 0) v = 0;
+    mean = (float)m;
+    invstd = rsqrtf((float)v + b.eps);
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// dwpw_fwd: z = pw . dw(act(in)), d = dw(act(in)); act = relu(x) or relu(BN(x))
+// grid: N * (Ho / TR) blocks, 256 threads. P = TR * Wo == 64 (host-enforced)
+// ------------------------------------------------------------------------------------------------
+template <int K, int DIL, int S, bool PREBN>
+__global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdArgs a) {
+  constexpr int P = 64;
+  const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int TR = P / Wo;
+  const int tiles = Ho / TR;
+  const int n = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int oy0 = tile * TR;
+  const int pad = a.pad;
+  const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
+  const int IW = (Wo - 1) * S + (K - 1) * DIL + 1;
+  const int iy0 = oy0 * S - pad, ix0 = -pad;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sD = smem;                       // [C][P]
+  float* sIn = smem + C * P;              // [CH][IR][IW]
+  float* sMean = sIn + a.chunk * IR * IW;  // [C]
+  float* sInv = sMean + C;                 // [C]
+  const int tid = threadIdx.x;
+  if (PREBN) {
+    for (int c = tid; c < C; c += 256) bn_coeffs(a.inbn, c, sMean[c], sInv[c]);
+    __syncthreads();
+  }
+  const float* xin = a.x + (size_t)n * C * H * W;
+  for (int c0 = 0; c0 < C; c0 += a.chunk) {
+    const int cn = min(a.chunk, C - c0);
+    const int tot = cn * IR * IW;
+    for (int i = tid; i < tot; i += 256) {
+      int cc = i / (IR * IW), r = (i / IW) % IR, q = i % IW;
+      int iy = iy0 + r, ix = ix0 + q, c = c0 + cc;
+      float v = 0.f;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        v = xin[((size_t)c * H + iy) * W + ix];
+        if (PREBN) v = (v - sMean[c]) * sInv[c];
+        v = fmaxf(v, 0.f);
+      }
+      sIn[i] = v;
+    }
+    __syncthreads();
+    for (int i = tid; i < cn * P; i += 256) {
+      int cc = i / P, p = i % P;
+      int c = c0 + cc;
+      int ty = p / Wo, tx = p % Wo;
+      const float* wk = a.dw + c * K * K;
+      const float* src = sIn + (cc * IR + ty * S) * IW + tx * S;
+      float acc = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) acc += wk[ky * K + kx] * src[ky * DIL * IW + kx * DIL];
+      sD[c * P + p] = acc;
+      a.d[(((size_t)n * C + c) * Ho + oy0 + ty) * Wo + tx] = acc;
+    }
+    __syncthreads();
+  }
+  // pointwise: z[co][p] = sum_ci pw[co][ci] * sD[ci][p]
+  const int wave = tid >> 6, lane = tid & 63;
+  if (a.use_mfma) {
+    // v_mfma_f32_16x16x4_f32: each wave owns 16 output channels per pass, 4 pixel blocks of 16
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    for (int cob = wave * 16; cob < C; cob += 64) {
+      f4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+      for (int k0 = 0; k0 < C; k0 += 4) {
+        float av = a.pw[(cob + (lane & 15)) * C + k0 + (lane >> 4)];
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          float bv = sD[(k0 + (lane >> 4)) * P + pb * 16 + (lane & 15)];
+          acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[pb], 0, 0, 0);
+        }
+      }
+      // C/D map: col (pixel) = lane & 15, row (co) = (lane >> 4) * 4 + r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int co = cob + (lane >> 4) * 4 + r;
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          int p = pb * 16 + (lane & 15);
+          float v = acc[pb][r];
+          a.z[(((size_t)n * C + co) * Ho + oy0 + p / Wo) * Wo + p % Wo] = v;
+          s += v;
+          s2 += v * v;
+        }
+        if (a.stats) {
+          // reduce over the 16 lanes that share this co (lanes with equal lane>>4)
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+          }
+          if ((lane & 15) == 0) {
+            atomicAdd(a.stats + co, (double)s);
+            atomicAdd(a.stats + C + co, (double)s2);
+          }
+        }
+      }
+    }
+  } else {
+    for (int co = wave; co < C; co += 4) {
+      const int cou = __builtin_amdgcn_readfirstlane(co);
+      const float* wrow = a.pw + cou * C;
+      float v = 0.f;
+      for (int ci = 0; ci < C; ++ci) v += wrow[ci] * sD[ci * P + lane];
+      a.z[(((size_t)n * C + cou) * Ho + oy0 + lane / Wo) * Wo + lane % Wo] = v;
+      if (a.stats) {
+        float s = wave_sum(v), s2 = wave_sum(v * v);
+        if (lane == 0) {
+          atomicAdd(a.stats + cou, (double)s);
+          atomicAdd(a.stats + C + cou, (double)s2);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// pw_fwd: z[:, co_off + co] = pw . relu(x) at (oy*S + off, ox*S + off); StdConv / FR half
+// grid: N*Ho*Wo/64 blocks of 64-pixel tiles; Cin, Cout <= 256
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdArgs a) {
+  constexpr int P = 64;
+  const int Cin = a.Cin, Cout = a.Cout, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int HWo = Ho * Wo;
+  const int pix0 = blockIdx.x * P;  // flat over N*Ho*Wo (HWo % 64 == 0)
+  const int n = pix0 / HWo;
+  const int prem = pix0 % HWo;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sX = smem;  // [Cin][P]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (int i = tid; i < Cin * P; i += 256) {
+    int ci = i / P, p = i % P;
+    int pp = prem + p, oy = pp / Wo, ox = pp % Wo;
+    int iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+    float v = 0.f;
+    if (iy < H && ix < W) v = fmaxf(a.x[(((size_t)n * Cin + ci) * H + iy) * W + ix], 0.f);
+    sX[i] = v;
+  }
+  __syncthreads();
+  for (int co = wave; co < Cout; co += 4) {
+    const int cou = __builtin_amdgcn_readfirstlane(co);
+    const float* wrow = a.pw + cou * Cin;
+    float v = 0.f;
+    for (int ci = 0; ci < Cin; ++ci) v += wrow[ci] * sX[ci * P + lane];
+    int pp = prem + lane;
+    a.z[((size_t)n * a.CoutTotal + a.co_off + cou) * HWo + pp] = v;
+    if (a.stats) {
+      float s = wave_sum(v), s2 = wave_sum(v * v);
+      if (lane == 0) {
+        atomicAdd(a.stats + a.co_off + cou, (double)s);
+        atomicAdd(a.stats + a.CoutTotal + a.co_off + cou, (double)s2);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// pool_fwd: avg (count_include_pad=False) and max 3x3/pad 1, stride S. One block per (n, c) plane.
+// ------------------------------------------------------------------------------------------------
+template <int S>
+__global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdArgs a) {
+  const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int nc = blockIdx.x, c = nc % C;
+  const float* xp = a.x + (size_t)nc * H * W;
+  float sa = 0, sa2 = 0, sm = 0, sm2 = 0;
+  for (int o = threadIdx.x; o < Ho * Wo; o += 256) {
+    int oy = o / Wo, ox = o % Wo;
+    float sum = 0.f, mx = -INFINITY;
+    int cnt = 0;
+    for (int ky = 0; ky < 3; ++ky) {
+      int iy = oy * S - 1 + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        int ix = ox * S - 1 + kx;
+        if (ix < 0 || ix >= W) continue;
+        float v = xp[iy * W + ix];
+        sum += v;
+        cnt++;
+        mx = (v > mx || v != v) ? v : mx;
+      }
+    }
+    float av = sum / (float)cnt;
+    a.zavg[(size_t)nc * Ho * Wo + o] = av;
+    a.zmax[(size_t)nc * Ho * Wo + o] = mx;
+    sa += av;
+    sa2 += av * av;
+    sm += mx;
+    sm2 += mx * mx;
+  }
+  if (!a.stats_avg) return;
+  __shared__ float red[4][4];
+  sa = wave_sum(sa);
+  sa2 = wave_sum(sa2);
+  sm = wave_sum(sm);
+  sm2 = wave_sum(sm2);
+  int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    red[wave][0] = sa;
+    red[wave][1] = sa2;
+    red[wave][2] = sm;
+    red[wave][3] = sm2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    double* dst = threadIdx.x < 2 ? a.stats_avg : a.stats_max;
+    atomicAdd(dst + (threadIdx.x & 1) * C + c, (double)t);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// combine_fwd: out = sum_k w[k] * BN_k(z_k) + wid * x  (elementwise), running stats in block 0
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdArgs a) {
+  const int C = a.C, HW = a.HW;
+  const size_t total = (size_t)a.N * C * HW;
+  __shared__ float sMean[kMaxOps][kMaxC], sInv[kMaxOps][kMaxC], sW[kMaxOps + 1];
+  for (int i = threadIdx.x; i < a.nops * C; i += 256) {
+    int k = i / C, c = i % C;
+    bn_coeffs(a.bn[k], c, sMean[k][c], sInv[k][c]);
+  }
+  if (threadIdx.x < a.nops) sW[threadIdx.x] = a.w ? a.w[a.widx[threadIdx.x]] : 1.f;
+  if (threadIdx.x == 0) sW[kMaxOps] = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+  __syncthreads();
+  if (blockIdx.x == 0 && a.update_running) {
+    for (int i = threadIdx.x; i < (a.nops + a.nupd) * C; i += 256) {
+      int k = i / C, c = i % C;
+      const BNRef& b = k < a.nops ? a.bn[k] : a.upd[k - a.nops];
+      if (!b.rmean || b.eval) continue;
+      double m = b.sums[c] * (double)b.inv_count;
+      double v = b.sums[C + c] * (double)b.inv_count - m * m;
+      if (v < 0) v = 0;
+      double cnt = 1.0 / (double)b.inv_count;
+      double vu = cnt > 1 ? v * cnt / (cnt - 1) : v;
+      b.rmean[c] = (1.f - a.momentum) * b.rmean[c] + a.momentum * (float)m;
+      b.rvar[c] = (1.f - a.momentum) * b.rvar[c] + a.momentum * (float)vu;
+    }
+  }
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    int c = (int)((i / HW) % C);
+    float acc = 0.f;
+    for (int k = 0; k < a.nops; ++k) acc += sW[k] * (a.z[k][i] - sMean[k][c]) * sInv[k][c];
+    if (a.xid) acc += sW[kMaxOps] * a.xid[i];
+    if (a.gamma) acc = acc * a.gamma[c] + a.beta[c];
+    a.out[i] = a.accumulate ? a.out[i] + acc : acc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// combine_bwd_reduce: S1[c] = sum dout, S2[k][c] = sum dout * zhat_k, Sid = sum dout * x
+// One block per (n, c) plane.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdArgs a) {
+  const int C = a.C, HW = a.HW;
+  const int nc = blockIdx.x, c = nc % C;
+  __shared__ float sMean[kMaxOps], sInv[kMaxOps];
+  __shared__ float red[4][kMaxOps + 2];
+  if (threadIdx.x < a.nops) bn_coeffs(a.bn[threadIdx.x], c, sMean[threadIdx.x], sInv[threadIdx.x]);
+  __syncthreads();
+  float s1 = 0.f, sid = 0.f;
+  float s2[kMaxOps];
+#pragma unroll
+  for (int k = 0; k < kMaxOps; ++k) s2[k] = 0.f;
+  const size_t base = (size_t)nc * HW;
+  for (int i = threadIdx.x; i < HW; i += 256) {
+    float g = a.dout[base + i];
+    s1 += g;
+#pragma unroll
+    for (int k = 0; k < kMaxOps; ++k)
+      if (k < a.nops) s2[k] += g * (a.z[k][base + i] - sMean[k]) * sInv[k];
+    if (a.xid) sid += g * a.xid[base + i];
+  }
+  int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  s1 = wave_sum(s1);
+  sid = wave_sum(sid);
+#pragma unroll
+  for (int k = 0; k < kMaxOps; ++k) s2[k] = wave_sum(s2[k]);
+  if (lane == 0) {
+    red[wave][0] = s1;
+    red[wave][1] = sid;
+#pragma unroll
+    for (int k = 0; k < kMaxOps; ++k) red[wave][2 + k] = s2[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < a.nops + 2) {
+    int j = threadIdx.x;
+    float t = red[0][j] + red[1][j] + red[2][j] + red[3][j];
+    if (j == 0) {
+      atomicAdd(a.red + c, (double)t);
+    } else if (j == 1) {
+      if (a.xid) {
+        atomicAdd(a.red + (size_t)(1 + a.nops) * C, (double)t);
+        if (a.gw && a.id_idx >= 0) atomicAdd(a.gw + a.id_idx, (double)t);
+      }
+    } else {
+      atomicAdd(a.red + (size_t)(j - 1) * C + c, (double)t);
+      if (a.gw) atomicAdd(a.gw + a.widx[j - 2], (double)t);
+    }
+  }
+}
+
+// on-the-fly BN backward: dz = wk * invstd * (g - S1/cnt - zhat * S2/cnt)
+__device__ __forceinline__ float bn_bwd_val(const GradSrc& gs, size_t i, int c, float mean, float inv, float wk) {
+  float zh = (gs.z[i] - mean) * inv;
+  float g = gs.g[i];
+  if (gs.eval) return wk * inv * g;
+  float m1 = (float)(gs.S1[c] * (double)gs.bn.inv_count);
+  float m2 = (float)(gs.S2[c] * (double)gs.bn.inv_count);
+  return wk * inv * (g - m1 - zh * m2);
+}
+
+// ------------------------------------------------------------------------------------------------
+// pw_bwd: dz (on the fly) -> dd = pw^T dz ; dW_pw += dz (x) a_in.
+// mode 0 (dw-pw stage): a_in = stored depthwise output d; writes dd [N,Cin,Ho,Wo].
+// mode 1 (StdConv / FR half): a_in = relu(x) at strided positions; gx += dd * (x > 0).
+// grid: persistent over 64-pixel tiles; weight grads accumulated in registers across tiles.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
+  constexpr int P = 64;
+  const int Cin = a.Cin, Cout = a.Cout, Ho = a.Ho, Wo = a.Wo, HWo = Ho * Wo;
+  const int ntiles = a.N * HWo / P;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sDz = smem;             // [Cout][P]
+  float* sA = sDz + Cout * P;    // [Cin][P]
+  float* sMean = sA + Cin * P;   // [Cout]
+  float* sInv = sMean + Cout;
+  float* sW = sInv + Cout;       // [1]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (int c = tid; c < Cout; c += 256) bn_coeffs(a.gs.bn, c, sMean[c], sInv[c]);
+  if (tid == 0) sW[0] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
+  __syncthreads();
+  const float wk = sW[0];
+  // per-thread weight-grad accumulators: pairs (co, ci) = tid + 256*j
+  constexpr int MAXJ = 16;  // Cout*Cin <= 4096
+  float gacc[MAXJ];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) gacc[j] = 0.f;
+  const int npairs = Cout * Cin;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int pix0 = t * P, n = pix0 / HWo, prem = pix0 % HWo;
+    for (int i = tid; i < Cout * P; i += 256) {
+      int co = i / P, p = i % P;
+      size_t gi = ((size_t)n * a.CoutTotal + a.co_off + co) * HWo + prem + p;
+      sDz[i] = bn_bwd_val(a.gs, gi, a.co_off + co, sMean[co], sInv[co], wk);
+    }
+    for (int i = tid; i < Cin * P; i += 256) {
+      int ci = i / P, p = i % P;
+      int pp = prem + p;
+      float v;
+      if (a.mode == 0) {
+        v = a.ain[((size_t)n * Cin + ci) * HWo + pp];
+      } else {
+        int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+        v = (iy < a.H && ix < a.W) ? fmaxf(a.x[(((size_t)n * Cin + ci) * a.H + iy) * a.W + ix], 0.f) : 0.f;
+      }
+      sA[i] = v;
+    }
+    __syncthreads();
+    if (a.gW) {
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) {
+        int pr = tid + 256 * j;
+        if (pr < npairs) {
+          int co = pr / Cin, ci = pr % Cin;
+          float s = 0.f;
+          for (int p = 0; p < P; ++p) s += sDz[co * P + p] * sA[ci * P + p];
+          gacc[j] += s;
+        }
+      }
+    }
+    // dd[ci][p] = sum_co pw[co][ci] dz[co][p]
+    if (a.need_dx) {
+      for (int ci = wave; ci < Cin; ci += 4) {
+        const int ciu = __builtin_amdgcn_readfirstlane(ci);
+        float v = 0.f;
+        for (int co = 0; co < Cout; ++co) v += a.pw[co * Cin + ciu] * sDz[co * P + lane];
+        int pp = prem + lane;
+        if (a.mode == 0) {
+          a.dd[((size_t)n * Cin + ciu) * HWo + pp] = v;
+        } else {
+          int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+          if (iy < a.H && ix < a.W) {
+            size_t xi = (((size_t)n * Cin + ciu) * a.H + iy) * a.W + ix;
+            if (a.x[xi] > 0.f) a.gx[xi] += v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (a.gW) {
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      int pr = tid + 256 * j;
+      if (pr < npairs) atomicAdd(a.gW + pr, gacc[j]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dw_bwd: transposed depthwise. For own output rows [oy0, oy0+TR): dW_dw += dd * act(in);
+// for own input rows [oy0*S, (oy0+TR)*S): ga = sum_taps dw * dd, masked by act'(in).
+// PREBN: input = z_prev (pre-BN), act = relu(BN(.)) -> writes g_prev and reductions for BN bwd.
+// else  : input = x, act = relu -> gx += ga * (x > 0).
+// ------------------------------------------------------------------------------------------------
+template <int K, int DIL, int S, bool PREBN>
+__global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
+  constexpr int P = 64;
+  const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int TR = P / Wo;
+  const int tiles = Ho / TR;
+  const int n = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int oy0 = tile * TR;
+  const int pad = a.pad;
+  const int r = (K - 1) / 2 * DIL;         // == pad for these ops
+  const int h = (r + S - 1) / S;           // halo output rows
+  const int OR = TR + 2 * h;               // staged dd rows
+  const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
+  const int IW = (Wo - 1) * S + (K - 1) * DIL + 1;
+  const int iy0 = oy0 * S - pad;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sDD = smem;                        // [CH][OR][Wo]
+  float* sIn = sDD + a.chunk * OR * Wo;     // [CH][IR][IW]
+  float* sMean = sIn + a.chunk * IR * IW;   // [C]
+  float* sInv = sMean + C;
+  float* sRed = sInv + C;                   // [2][CH] per-block BN-bwd partials (PREBN)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (PREBN) {
+    for (int c = tid; c < C; c += 256) bn_coeffs(a.inbn, c, sMean[c], sInv[c]);
+    __syncthreads();
+  }
+  const float* xin = a.x + (size_t)n * C * H * W;
+  const float* ddn = a.dd + (size_t)n * C * Ho * Wo;
+  const int own_in = TR * S;  // own input rows start at oy0*S
+  for (int c0 = 0; c0 < C; c0 += a.chunk) {
+    const int cn = min(a.chunk, C - c0);
+    for (int i = tid; i < cn * OR * Wo; i += 256) {
+      int cc = i / (OR * Wo), rr = (i / Wo) % OR, q = i % Wo;
+      int oy = oy0 - h + rr;
+      sDD[i] = (oy >= 0 && oy < Ho) ? ddn[((size_t)(c0 + cc) * Ho + oy) * Wo + q] : 0.f;
+    }
+    for (int i = tid; i < cn * IR * IW; i += 256) {
+      int cc = i / (IR * IW), rr = (i / IW) % IR, q = i % IW;
+      int iy = iy0 + rr, ix = -pad + q, c = c0 + cc;
+      float v = 0.f;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        v = xin[((size_t)c * H + iy) * W + ix];
+        if (PREBN) v = (v - sMean[c]) * sInv[c];
+        v = fmaxf(v, 0.f);
+      }
+      sIn[i] = v;
+    }
+    if (PREBN)
+      for (int i = tid; i < 2 * a.chunk; i += 256) sRed[i] = 0.f;
+    __syncthreads();
+    // weight grads: one (channel, tap) per thread-group, reduce over own output pixels
+    if (a.gW) {
+      for (int job = wave; job < cn * K * K; job += 4) {
+        int cc = job / (K * K), tap = job % (K * K), ky = tap / K, kx = tap % K;
+        float s = 0.f;
+        for (int p = lane; p < P; p += 64) {
+          int ty = p / Wo, tx = p % Wo;
+          s += sDD[(cc * OR + h + ty) * Wo + tx] * sIn[(cc * IR + ty * S + ky * DIL) * IW + tx * S + kx * DIL];
+        }
+        s = wave_sum(s);
+        if (lane == 0) atomicAdd(a.gW + (c0 + cc) * K * K + tap, s);
+      }
+    }
+    // input grads for own input rows
+    for (int i = tid; i < cn * own_in * W; i += 256) {
+      int cc = i / (own_in * W), rr = (i / W) % own_in, ix = i % W;
+      int c = c0 + cc;
+      int iy = oy0 * S + rr;
+      if (iy >= H) continue;
+      float ga = 0.f;
+      const float* wk = a.dw + c * K * K;
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky) {
+        int ty = iy + pad - ky * DIL;  // = oy * S
+        if (ty < 0 || ty % S) continue;
+        int oy = ty / S;
+        if (oy < 0 || oy >= Ho) continue;
+        int srow = oy - (oy0 - h);
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          int tx = ix + pad - kx * DIL;
+          if (tx < 0 || tx % S) continue;
+          int ox = tx / S;
+          if (ox >= Wo) continue;
+          ga += wk[ky * K + kx] * sDD[(cc * OR + srow) * Wo + ox];
+        }
+      }
+      size_t xi = ((size_t)(n * C + c) * H + iy) * W + ix;
+      float xv = a.x[xi];
+      if (PREBN) {
+        float y = (xv - sMean[c]) * sInv[c];
+        float g = y > 0.f ? ga : 0.f;
+        a.gout[xi] = g;
+        if (a.red) {
+          atomicAdd(sRed + cc, g);  // LDS atomics; one global fp64 atomic per channel per block below
+          atomicAdd(sRed + a.chunk + cc, g * y);
+        }
+      } else {
+        if (xv > 0.f) a.gout[xi] += ga;
+      }
+    }
+    __syncthreads();
+    if (PREBN && a.red) {
+      for (int cc = tid; cc < cn; cc += 256) {
+        atomicAdd(a.red + c0 + cc, (double)sRed[cc]);
+        atomicAdd(a.red + C + c0 + cc, (double)sRed[a.chunk + cc]);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// pool_bwd: gx += avg^T(dz_avg) + max^T(dz_max) + wid * dout (identity skip), per (n,c) plane
+// ------------------------------------------------------------------------------------------------
+template <int S>
+__global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdArgs a) {
+  const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int nc = blockIdx.x, c = nc % C;
+  const float* xp = a.x + (size_t)nc * H * W;
+  const size_t ob = (size_t)nc * Ho * Wo;
+  float ma = 0, ia = 1, mm = 0, im = 1;
+  if (a.ga.z) bn_coeffs(a.ga.bn, c, ma, ia);
+  if (a.gm.z) bn_coeffs(a.gm.bn, c, mm, im);
+  float wa = a.ga.w ? a.ga.w[a.ga.widx] : 0.f;
+  float wm = a.gm.w ? a.gm.w[a.gm.widx] : 0.f;
+  float wid = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+  for (int q = threadIdx.x; q < H * W; q += 256) {
+    int iy = q / W, ix = q % W;
+    float g = 0.f;
+    // outputs whose 3x3 window (pad 1) covers (iy, ix): oy*S - 1 <= iy <= oy*S + 1
+    int oy_lo = (iy - 1 + S - 1) / S; if (iy - 1 < 0) oy_lo = 0;
+    int oy_hi = (iy + 1) / S;
+    int ox_lo = (ix - 1 + S - 1) / S; if (ix - 1 < 0) ox_lo = 0;
+    int ox_hi = (ix + 1) / S;
+    for (int oy = oy_lo; oy <= oy_hi && oy < Ho; ++oy) {
+      for (int ox = ox_lo; ox <= ox_hi && ox < Wo; ++ox) {
+        size_t oi = ob + oy * Wo + ox;
+        if (a.ga.z) {
+          int y0 = max(oy * S - 1, 0), y1 = min(oy * S + 1, H - 1);
+          int x0 = max(ox * S - 1, 0), x1 = min(ox * S + 1, W - 1);
+          float cnt = (float)((y1 - y0 + 1) * (x1 - x0 + 1));
+          g += bn_bwd_val(a.ga, oi, c, ma, ia, wa) / cnt;
+        }
+        if (a.gm.z) {
+          // first maximal element in row-major window order (PyTorch max_pool2d semantics)
+          float mx = -INFINITY;
+          int arg = -1;
+          for (int ky = 0; ky < 3; ++ky) {
+            int yy = oy * S - 1 + ky;
+            if (yy < 0 || yy >= H) continue;
+            for (int kx = 0; kx < 3; ++kx) {
+              int xx = ox * S - 1 + kx;
+              if (xx < 0 || xx >= W) continue;
+              float v = xp[yy * W + xx];
+              if (v > mx || v != v) {
+                mx = v;
+                arg = yy * W + xx;
+              }
+            }
+          }
+          if (arg == q) g += bn_bwd_val(a.gm, oi, c, mm, im, wm);
+        }
+      }
+    }
+    if (a.dout_id) g += wid * a.dout_id[(size_t)nc * H * W + q];
+    a.gx[(size_t)nc * H * W + q] += g;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------------
+template <int K, int DIL, int S>
+static void launch_dwpw_fwd_t(const DwPwFwdArgs& a, bool prebn, hipStream_t st) {
+  const int TR = 64 / a.Wo;
+  const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
+  const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
+  size_t lds = sizeof(float) * (a.C * 64 + a.chunk * IR * IW + 2 * a.C);
+  dim3 grid(a.N * (a.Ho / TR));
+  if (prebn) hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, a);
+  else hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, a);
+}
+
+void launch_dwpw_fwd(const DwPwFwdArgs& a, int K, int dil, int S, bool prebn, hipStream_t st) {
+#define DISPATCH(KK, DD, SS) \
+  if (K == KK && dil == DD && S == SS) return launch_dwpw_fwd_t<KK, DD, SS>(a, prebn, st);
+  DISPATCH(3, 1, 1) DISPATCH(3, 1, 2) DISPATCH(5, 1, 1) DISPATCH(5, 1, 2)
+  DISPATCH(3, 2, 1) DISPATCH(3, 2, 2) DISPATCH(5, 2, 1) DISPATCH(5, 2, 2)
+#undef DISPATCH
+}
+
+template <int K, int DIL, int S>
+static void launch_dw_bwd_t(const DwBwdArgs& a, bool prebn, hipStream_t st) {
+  const int TR = 64 / a.Wo;
+  const int r = (K - 1) / 2 * DIL, h = (r + S - 1) / S, OR = TR + 2 * h;
+  const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
+  const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
+  size_t lds = sizeof(float) * (a.chunk * OR * a.Wo + a.chunk * IR * IW + 2 * a.C + 2 * a.chunk);
+  dim3 grid(a.N * (a.Ho / TR));
+  if (prebn) hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, a);
+  else hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, a);
+}
+
+void launch_dw_bwd(const DwBwdArgs& a, int K, int dil, int S, bool prebn, hipStream_t st) {
+#define DISPATCH(KK, DD, SS) \
+  if (K == KK && dil == DD && S == SS) return launch_dw_bwd_t<KK, DD, SS>(a, prebn, st);
+  DISPATCH(3, 1, 1) DISPATCH(3, 1, 2) DISPATCH(5, 1, 1) DISPATCH(5, 1, 2)
+  DISPATCH(3, 2, 1) DISPATCH(3, 2, 2) DISPATCH(5, 2, 1) DISPATCH(5, 2, 2)
+#undef DISPATCH
+}
+
+void launch_pw_fwd(const PwFwdArgs& a, hipStream_t st) {
+  size_t lds = sizeof(float) * a.Cin * 64;
+  hipLaunchKernelGGL(pw_fwd_kernel, dim3(a.N * a.Ho * a.Wo / 64), dim3(256), lds, st, a);
+}
+
+void launch_pool_fwd(const PoolFwdArgs& a, int S, hipStream_t st) {
+  if (S == 1) hipLaunchKernelGGL(pool_fwd_kernel<1>, dim3(a.N * a.C), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(pool_fwd_kernel<2>, dim3(a.N * a.C), dim3(256), 0, st, a);
+}
+
+void launch_pool_bwd(const PoolBwdArgs& a, int S, hipStream_t st) {
+  if (S == 1) hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(a.N * a.C), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(pool_bwd_kernel<2>, dim3(a.N * a.C), dim3(256), 0, st, a);
+}
+
+void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st) {
+  size_t total = (size_t)a.N * a.C * a.HW;
+  int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(combine_fwd_kernel, dim3(blocks), dim3(256), 0, st, a);
+}
+
+void launch_combine_bwd_reduce(const CombineBwdArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(combine_bwd_reduce_kernel, dim3(a.N * a.C), dim3(256), 0, st, a);
+}
+
+void launch_pw_bwd(const PwBwdArgs& a, hipStream_t st) {
+  int ntiles = a.N * a.Ho * a.Wo / 64;
+  int blocks = std::min(ntiles, 1024);
+  size_t lds = sizeof(float) * (a.Cout * 64 + a.Cin * 64 + 2 * a.Cout + 4);
+  hipLaunchKernelGGL(pw_bwd_kernel, dim3(blocks), dim3(256), lds, st, a);
+}
+
+
+}  // namespace katib_hip

@@ -1,0 +1,296 @@
+"""DARTS search step: second-order architect + weight step, data-parallel, graph-captured.
+
+Per step (reference ``run_trial.py:177-222`` + ``architect.py:30-135``):
+
+1. FWD1/BWD1  L_train(w)                 -> g1            (all-reduce)
+   w' = w - xi * (mu*m + g1 + wd*w),  alpha' = alpha
+2. FWD2/BWD2  L_valid(w', alpha')        -> d_alpha, d_w' (all-reduce)
+3. eps = 0.01/||d_w'||; w += eps d_w';  FWD3/BWD3 L_train -> d_alpha+
+   w -= 2 eps d_w';                      FWD4/BWD4 L_train -> d_alpha-
+   w += eps d_w'
+   alpha.grad = d_alpha - xi (d_alpha+ - d_alpha-) / (2 eps)  (all-reduce, merged)
+   Adam(alpha) with L2 weight decay, betas (0.5, 0.999)
+4. FWD5/BWD5  L_train(w)                 -> g5            (all-reduce)
+   clip ||g5|| <= w_grad_clip;  SGD(momentum mu, weight decay wd) on w
+
+Data parallelism is *within* the trial (the reference DARTS trial is single-GPU
+only, ``run_trial.py:81-96``): each rank runs the step on its own shard of the
+train/valid batches and the four gradient vectors are averaged with one RCCL
+all-reduce each over flat buffers. BN statistics stay per-rank (like DDP).
+
+With ``capture=True`` every segment between collectives is captured once as a
+HIP graph (``torch.cuda.CUDAGraph``) and replayed; at world size 1 the whole
+step is a single graph. All scalars (lr, eps, Adam step) live on the device so
+the replay needs no host synchronisation.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..parallel.comm import Comm
+from .darts import BNState, DartsLayout, DartsNetwork, accuracy
+
+DEFAULTS = dict(w_lr=0.025, w_lr_min=0.001, w_momentum=0.9, w_weight_decay=3e-4, w_grad_clip=5.0,
+                alpha_lr=3e-4, alpha_weight_decay=1e-3)
+
+
+class _Leaves:
+    """Parameter leaves that are views of a flat buffer, with grads accumulating
+    into a flat grad buffer (bucket views)."""
+
+    def __init__(self, views: Dict[str, torch.Tensor], grad_views: Dict[str, torch.Tensor]):
+        self.views = views
+        for k, v in views.items():
+            v.requires_grad_(True)
+            v.grad = grad_views[k]
+        self.list = list(views.values())
+
+
+class DartsSearch:
+    def __init__(self, layout: DartsLayout, device, comm: Optional[Comm] = None, seed: int = 2,
+                 settings: Optional[Dict] = None, capture: bool = False, ops=None):
+        self.layout = layout
+        self.device = torch.device(device)
+        self.comm = comm or Comm(device=self.device)
+        self.s = dict(DEFAULTS)
+        if settings:
+            self.s.update({k: float(v) for k, v in settings.items() if k in DEFAULTS})
+        self.capture = capture and self.device.type == "cuda"
+        self.net = DartsNetwork(layout, ops=ops)
+        g = torch.Generator().manual_seed(seed)
+        dev, f32 = self.device, torch.float32
+        nW, nA = layout.n_weights, layout.n_alphas
+        W = torch.zeros(nW, dtype=f32)
+        layout.init_weights(W, g)
+        A = 1e-3 * torch.randn(nA, generator=g)
+        # all ranks start from identical weights (rank 0's)
+        self.W = W.to(dev)
+        self.A = A.to(dev)
+        self.comm.broadcast_(self.W)
+        self.comm.broadcast_(self.A)
+        self.Wv = torch.zeros_like(self.W)
+        self.Av = torch.zeros_like(self.A)
+        self.gW = torch.zeros_like(self.W)  # model weight grads (BWD1 / BWD5)
+        self.gWv = torch.zeros_like(self.W)  # virtual weight grads (BWD2)
+        self.gAv = torch.zeros_like(self.A)  # virtual alpha grads (BWD2)
+        self.gA = torch.zeros_like(self.A)  # alpha grads (BWD3/4/5 scratch)
+        self.gAp = torch.zeros_like(self.A)
+        self.alpha_grad = torch.zeros_like(self.A)
+        self.mom = torch.zeros_like(self.W)
+        self.adam_m = torch.zeros_like(self.A)
+        self.adam_v = torch.zeros_like(self.A)
+        self.adam_t = torch.zeros((), device=dev)
+        self.lr = torch.full((), self.s["w_lr"], device=dev)
+        self.eps = torch.zeros((), device=dev)
+        self.bn = BNState(layout, dev)
+        self.bn_v = BNState(layout, dev)
+        self.loss_out = torch.zeros((), device=dev)
+        self.logits_out = None
+        # leaves
+        self.Pw = _Leaves(layout.views(self.W), layout.views(self.gW))
+        self.Pv = _Leaves(layout.views(self.Wv), layout.views(self.gWv))
+        an, ar = layout.alpha_views(self.A)
+        gn, gr = layout.alpha_views(self.gA)
+        self.An, self.Ar = an, ar
+        for v, gv in zip(an + ar, gn + gr):
+            v.requires_grad_(True)
+            v.grad = gv
+        avn, avr = layout.alpha_views(self.Av)
+        gvn, gvr = layout.alpha_views(self.gAv)
+        self.Avn, self.Avr = avn, avr
+        for v, gv in zip(avn + avr, gvn + gvr):
+            v.requires_grad_(True)
+            v.grad = gv
+        self.W_detached = layout.views(self.W.detach())
+        self.graphs = None
+        self.static = None
+
+    # ------------------------------------------------------------------ pieces
+    def _loss(self, x, y, P, an, ar, bn):
+        logits = self.net.forward(x, P, an, ar, bn, training=True)
+        return F.cross_entropy(logits, y), logits
+
+    def _seg_virtual(self, tx, ty):
+        """FWD1/BWD1 -> gW (not yet reduced)."""
+        self.gW.zero_()
+        loss, _ = self._loss(tx, ty, self.Pw.views, self.An, self.Ar, self.bn)
+        loss.backward(inputs=self.Pw.list)
+
+    def _seg_unrolled(self, vx, vy):
+        """virtual step + FWD2/BWD2 -> gAv, gWv."""
+        s = self.s
+        with torch.no_grad():
+            # w' = w - xi*(mu*m + g + wd*w)
+            self.Wv.copy_(self.mom).mul_(s["w_momentum"]).add_(self.gW).add_(self.W, alpha=s["w_weight_decay"])
+            self.Wv.mul_(-self.lr).add_(self.W)
+            self.Av.copy_(self.A)
+        self.gWv.zero_()
+        self.gAv.zero_()
+        loss, _ = self._loss(vx, vy, self.Pv.views, self.Avn, self.Avr, self.bn_v)
+        loss.backward(inputs=self.Pv.list + self.Avn + self.Avr)
+
+    def _seg_hessian(self, tx, ty):
+        """+/- eps perturbations, FWD3/BWD3 and FWD4/BWD4 w.r.t. alphas only."""
+        with torch.no_grad():
+            self.eps.copy_(0.01 / self.gWv.norm())
+            self.W.add_(self.gWv * self.eps)
+        self.gA.zero_()
+        loss, _ = self._loss(tx, ty, self.W_detached, self.An, self.Ar, self.bn)
+        loss.backward(inputs=self.An + self.Ar)
+        with torch.no_grad():
+            self.gAp.copy_(self.gA)
+            self.W.sub_(self.gWv * (2.0 * self.eps))
+        self.gA.zero_()
+        loss, _ = self._loss(tx, ty, self.W_detached, self.An, self.Ar, self.bn)
+        loss.backward(inputs=self.An + self.Ar)
+        with torch.no_grad():
+            self.W.add_(self.gWv * self.eps)
+            # alpha.grad = d_alpha - xi * (d+ - d-) / (2 eps)
+            h = (self.gAp - self.gA) / (2.0 * self.eps)
+            torch.sub(self.gAv, h * self.lr, out=self.alpha_grad)
+
+    def _seg_alpha_step(self):
+        """Adam(alpha_lr, betas=(0.5, 0.999), weight_decay) on alphas."""
+        s = self.s
+        b1, b2 = 0.5, 0.999
+        with torch.no_grad():
+            g = self.alpha_grad + s["alpha_weight_decay"] * self.A
+            self.adam_t.add_(1.0)
+            self.adam_m.mul_(b1).add_(g, alpha=1 - b1)
+            self.adam_v.mul_(b2).addcmul_(g, g, value=1 - b2)
+            bc1 = 1 - torch.pow(b1, self.adam_t)
+            bc2 = 1 - torch.pow(b2, self.adam_t)
+            denom = (self.adam_v.sqrt() / bc2.sqrt()).add_(1e-8)
+            self.A.sub_(self.adam_m / denom * (s["alpha_lr"] / bc1))
+
+    def _seg_weight(self, tx, ty):
+        """FWD5/BWD5 -> gW (+ alpha grads ignored), logits/loss kept for metrics."""
+        self.gW.zero_()
+        self.gA.zero_()
+        loss, logits = self._loss(tx, ty, self.Pw.views, self.An, self.Ar, self.bn)
+        loss.backward(inputs=self.Pw.list)
+        with torch.no_grad():
+            self.loss_out.copy_(loss.detach())
+            if self.logits_out is None or self.logits_out.shape != logits.shape:
+                self.logits_out = torch.empty_like(logits)
+            self.logits_out.copy_(logits.detach())
+
+    def _seg_weight_update(self):
+        s = self.s
+        with torch.no_grad():
+            total = self.gW.norm()
+            coef = torch.clamp(s["w_grad_clip"] / (total + 1e-6), max=1.0)
+            self.gW.mul_(coef)
+            d = self.gW.add(self.W, alpha=s["w_weight_decay"])
+            self.mom.mul_(s["w_momentum"]).add_(d)
+            self.W.sub_(self.mom * self.lr)
+
+    # ------------------------------------------------------------------ step
+    def _segments(self):
+        """List of (callable, collective-after) in order."""
+        c = self.comm
+        return [
+            (lambda: self._seg_virtual(self.static["tx"], self.static["ty"]), [self.gW]),
+            (lambda: self._seg_unrolled(self.static["vx"], self.static["vy"]), [self.gWv, self.gAv]),
+            (lambda: self._seg_hessian(self.static["tx"], self.static["ty"]), [self.alpha_grad]),
+            (lambda: (self._seg_alpha_step(), self._seg_weight(self.static["tx"], self.static["ty"])), [self.gW]),
+            (lambda: self._seg_weight_update(), []),
+        ]
+
+    def _run_eager(self):
+        for fn, colls in self._segments():
+            fn()
+            for t in colls:
+                self.comm.allreduce_mean_(t)
+
+    def _build_graphs(self):
+        segs = self._segments()
+        # merge segments with no collective in between (all of them at world size 1)
+        groups, cur = [], []
+        for fn, colls in segs:
+            cur.append(fn)
+            if colls and self.comm.distributed:
+                groups.append((cur, colls))
+                cur = []
+        if cur:
+            groups.append((cur, []))
+        # warm up on a side stream (required before capture), then capture
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._snapshot_state()
+                self._run_eager()
+                self._restore_state()
+        torch.cuda.current_stream().wait_stream(s)
+        graphs = []
+        for fns, colls in groups:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for fn in fns:
+                    fn()
+            graphs.append((g, colls))
+        self.graphs = graphs
+
+    def _state_tensors(self):
+        return [self.W, self.A, self.mom, self.adam_m, self.adam_v, self.adam_t, self.bn.mean, self.bn.var,
+                self.bn_v.mean, self.bn_v.var]
+
+    def _snapshot_state(self):
+        self._saved = [t.clone() for t in self._state_tensors()]
+
+    def _restore_state(self):
+        with torch.no_grad():
+            for t, s in zip(self._state_tensors(), self._saved):
+                t.copy_(s)
+        self._saved = None
+
+    def set_lr(self, lr: float):
+        self.lr.fill_(lr)
+
+    def step(self, tx, ty, vx, vy):
+        if self.static is None:
+            self.static = {"tx": tx.clone(), "ty": ty.clone(), "vx": vx.clone(), "vy": vy.clone()}
+        else:
+            self.static["tx"].copy_(tx)
+            self.static["ty"].copy_(ty)
+            self.static["vx"].copy_(vx)
+            self.static["vy"].copy_(vy)
+        if self.capture:
+            if self.graphs is None:
+                # the first capture consumes the current batch: _build_graphs restores the state
+                # after its warm-up runs, so the replay below performs this step exactly once
+                self._build_graphs()
+            for g, colls in self.graphs:
+                g.replay()
+                for t in colls:
+                    self.comm.allreduce_mean_(t)
+        else:
+            self._run_eager()
+        return self.loss_out
+
+    # ------------------------------------------------------------------ eval / genotype
+    @torch.no_grad()
+    def evaluate(self, x, y):
+        logits = self.net.forward(x, self.layout.views(self.W), self.An, self.Ar, self.bn, training=False)
+        loss = F.cross_entropy(logits, y)
+        top1, top5 = accuracy(logits, y)
+        return loss, top1, top5
+
+    def train_metrics(self, y):
+        top1, top5 = accuracy(self.logits_out, y)
+        return float(self.loss_out), float(top1), float(top5)
+
+    def genotype(self):
+        from .darts import Genotype
+
+        sp = self.layout.space
+        normal = sp.parse([a.detach() for a in self.An], k=2)
+        reduce = sp.parse([a.detach() for a in self.Ar], k=2) if self.Ar else []
+        concat = range(2, 2 + self.layout.N)
+        return Genotype(normal=normal, normal_concat=concat, reduce=reduce, reduce_concat=concat)
