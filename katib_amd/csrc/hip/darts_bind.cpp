@@ -90,7 +90,7 @@ void dwpw_fwd(Tensor x, Tensor dw, Tensor pw, int64_t K, int64_t dil, int64_t S,
   a.N = N; a.C = C; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.pad = pad;
   const int TR = 64 / Wo;
   const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
-  a.chunk = pick_chunk(C, IR * IW, C * 64 + 2 * C);
+  a.chunk = pick_chunk(C, IR * IW, C * 64 + 4 * C);
   a.use_mfma = (use_mfma && C % 16 == 0) ? 1 : 0;
   bool prebn = inbn.has_value();
   if (prebn) a.inbn = make_bn(*inbn, C);
@@ -214,7 +214,7 @@ void dw_bwd(Tensor x, c10::optional<py::tuple> inbn, Tensor dw, Tensor dd, Tenso
   a.pad = pad;
   const int TR = 64 / a.Wo, r = (K - 1) / 2 * dil, h = (r + S - 1) / S, OR = TR + 2 * h;
   const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (a.Wo - 1) * S + (K - 1) * dil + 1;
-  a.chunk = pick_chunk(a.C, OR * a.Wo + IR * IW + 2, 2 * a.C);
+  a.chunk = pick_chunk(a.C, OR * a.Wo + IR * IW, 4 * a.C + (a.gW ? a.C * (int)(K * K) : 0));
   bool prebn = inbn.has_value();
   if (prebn) a.inbn = make_bn(*inbn, a.C);
   launch_dw_bwd(a, K, dil, S, prebn, cur_stream());

@@ -30,6 +30,12 @@
 
 namespace katib_hip {
 
+// Persistent grids: 2 blocks per CU. Cross-block sums are accumulated per block in LDS
+// and flushed as ONE lane-contiguous atomic vector per block - global float atomics
+// execute memory-side, and many single-lane adds to the same address serialise
+// (MI355X_MICROARCH.md "Global float atomics").
+constexpr int kMaxBlocks = 512;
+
 __device__ __forceinline__ void bn_coeffs(const BNRef& b, int c, float& mean, float& invstd) {
   if (b.eval) {
     mean = b.rmean[c];
@@ -65,112 +71,115 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdArgs a) {
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int TR = P / Wo;
   const int tiles = Ho / TR;
-  const int n = blockIdx.x / tiles, tile = blockIdx.x % tiles;
-  const int oy0 = tile * TR;
+  const int ntiles = a.N * tiles;
   const int pad = a.pad;
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (Wo - 1) * S + (K - 1) * DIL + 1;
-  const int iy0 = oy0 * S - pad, ix0 = -pad;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sD = smem;                       // [C][P]
   float* sIn = smem + C * P;              // [CH][IR][IW]
   float* sMean = sIn + a.chunk * IR * IW;  // [C]
   float* sInv = sMean + C;                 // [C]
+  float* sStat = sInv + C;                 // [2C] block-local (sum, sum of squares)
   const int tid = threadIdx.x;
-  if (PREBN) {
-    for (int c = tid; c < C; c += 256) bn_coeffs(a.inbn, c, sMean[c], sInv[c]);
-    __syncthreads();
-  }
-  const float* xin = a.x + (size_t)n * C * H * W;
-  for (int c0 = 0; c0 < C; c0 += a.chunk) {
-    const int cn = min(a.chunk, C - c0);
-    const int tot = cn * IR * IW;
-    for (int i = tid; i < tot; i += 256) {
-      int cc = i / (IR * IW), r = (i / IW) % IR, q = i % IW;
-      int iy = iy0 + r, ix = ix0 + q, c = c0 + cc;
-      float v = 0.f;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        v = xin[((size_t)c * H + iy) * W + ix];
-        if (PREBN) v = (v - sMean[c]) * sInv[c];
-        v = fmaxf(v, 0.f);
-      }
-      sIn[i] = v;
-    }
-    __syncthreads();
-    for (int i = tid; i < cn * P; i += 256) {
-      int cc = i / P, p = i % P;
-      int c = c0 + cc;
-      int ty = p / Wo, tx = p % Wo;
-      const float* wk = a.dw + c * K * K;
-      const float* src = sIn + (cc * IR + ty * S) * IW + tx * S;
-      float acc = 0.f;
-#pragma unroll
-      for (int ky = 0; ky < K; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < K; ++kx) acc += wk[ky * K + kx] * src[ky * DIL * IW + kx * DIL];
-      sD[c * P + p] = acc;
-      a.d[(((size_t)n * C + c) * Ho + oy0 + ty) * Wo + tx] = acc;
-    }
-    __syncthreads();
-  }
-  // pointwise: z[co][p] = sum_ci pw[co][ci] * sD[ci][p]
   const int wave = tid >> 6, lane = tid & 63;
-  if (a.use_mfma) {
-    // v_mfma_f32_16x16x4_f32: each wave owns 16 output channels per pass, 4 pixel blocks of 16
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    for (int cob = wave * 16; cob < C; cob += 64) {
-      f4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-      for (int k0 = 0; k0 < C; k0 += 4) {
-        float av = a.pw[(cob + (lane & 15)) * C + k0 + (lane >> 4)];
-#pragma unroll
-        for (int pb = 0; pb < 4; ++pb) {
-          float bv = sD[(k0 + (lane >> 4)) * P + pb * 16 + (lane & 15)];
-          acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[pb], 0, 0, 0);
+  for (int c = tid; c < C; c += 256) {
+    if (PREBN) bn_coeffs(a.inbn, c, sMean[c], sInv[c]);
+    sStat[c] = 0.f;
+    sStat[C + c] = 0.f;
+  }
+  __syncthreads();
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int n = t / tiles, oy0 = (t % tiles) * TR;
+    const int iy0 = oy0 * S - pad, ix0 = -pad;
+    const float* xin = a.x + (size_t)n * C * H * W;
+    for (int c0 = 0; c0 < C; c0 += a.chunk) {
+      const int cn = min(a.chunk, C - c0);
+      const int tot = cn * IR * IW;
+      for (int i = tid; i < tot; i += 256) {
+        int cc = i / (IR * IW), r = (i / IW) % IR, q = i % IW;
+        int iy = iy0 + r, ix = ix0 + q, c = c0 + cc;
+        float v = 0.f;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+          v = xin[((size_t)c * H + iy) * W + ix];
+          if (PREBN) v = (v - sMean[c]) * sInv[c];
+          v = fmaxf(v, 0.f);
         }
+        sIn[i] = v;
       }
-      // C/D map: col (pixel) = lane & 15, row (co) = (lane >> 4) * 4 + r
+      __syncthreads();
+      for (int i = tid; i < cn * P; i += 256) {
+        int cc = i / P, p = i % P;
+        int c = c0 + cc;
+        int ty = p / Wo, tx = p % Wo;
+        const float* wk = a.dw + c * K * K;
+        const float* src = sIn + (cc * IR + ty * S) * IW + tx * S;
+        float acc = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int co = cob + (lane >> 4) * 4 + r;
-        float s = 0.f, s2 = 0.f;
+        for (int ky = 0; ky < K; ++ky)
 #pragma unroll
-        for (int pb = 0; pb < 4; ++pb) {
-          int p = pb * 16 + (lane & 15);
-          float v = acc[pb][r];
-          a.z[(((size_t)n * C + co) * Ho + oy0 + p / Wo) * Wo + p % Wo] = v;
-          s += v;
-          s2 += v * v;
+          for (int kx = 0; kx < K; ++kx) acc += wk[ky * K + kx] * src[ky * DIL * IW + kx * DIL];
+        sD[c * P + p] = acc;
+        a.d[(((size_t)n * C + c) * Ho + oy0 + ty) * Wo + tx] = acc;
+      }
+      __syncthreads();
+    }
+    // pointwise: z[co][p] = sum_ci pw[co][ci] * sD[ci][p]
+    if (a.use_mfma) {
+      // v_mfma_f32_16x16x4_f32: each wave owns 16 output channels per pass, 4 pixel blocks of 16
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      for (int cob = wave * 16; cob < C; cob += 64) {
+        f4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        for (int k0 = 0; k0 < C; k0 += 4) {
+          float av = a.pw[(cob + (lane & 15)) * C + k0 + (lane >> 4)];
+#pragma unroll
+          for (int pb = 0; pb < 4; ++pb) {
+            float bv = sD[(k0 + (lane >> 4)) * P + pb * 16 + (lane & 15)];
+            acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[pb], 0, 0, 0);
+          }
         }
-        if (a.stats) {
-          // reduce over the 16 lanes that share this co (lanes with equal lane>>4)
+        // C/D map: col (pixel) = lane & 15, row (co) = (lane >> 4) * 4 + r
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int co = cob + (lane >> 4) * 4 + r;
+          float s = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int pb = 0; pb < 4; ++pb) {
+            int p = pb * 16 + (lane & 15);
+            float v = acc[pb][r];
+            a.z[(((size_t)n * C + co) * Ho + oy0 + p / Wo) * Wo + p % Wo] = v;
+            s += v;
+            s2 += v * v;
+          }
 #pragma unroll
           for (int o = 8; o > 0; o >>= 1) {
             s += __shfl_xor(s, o, 64);
             s2 += __shfl_xor(s2, o, 64);
           }
-          if ((lane & 15) == 0) {
-            atomicAdd(a.stats + co, (double)s);
-            atomicAdd(a.stats + C + co, (double)s2);
+          if ((lane & 15) == 0) {  // unique owner of channel co in this tile
+            sStat[co] += s;
+            sStat[C + co] += s2;
           }
         }
       }
-    }
-  } else {
-    for (int co = wave; co < C; co += 4) {
-      const int cou = __builtin_amdgcn_readfirstlane(co);
-      const float* wrow = a.pw + cou * C;
-      float v = 0.f;
-      for (int ci = 0; ci < C; ++ci) v += wrow[ci] * sD[ci * P + lane];
-      a.z[(((size_t)n * C + cou) * Ho + oy0 + lane / Wo) * Wo + lane % Wo] = v;
-      if (a.stats) {
+    } else {
+      for (int co = wave; co < C; co += 4) {
+        const int cou = __builtin_amdgcn_readfirstlane(co);
+        const float* wrow = a.pw + cou * C;
+        float v = 0.f;
+        for (int ci = 0; ci < C; ++ci) v += wrow[ci] * sD[ci * P + lane];
+        a.z[(((size_t)n * C + cou) * Ho + oy0 + lane / Wo) * Wo + lane % Wo] = v;
         float s = wave_sum(v), s2 = wave_sum(v * v);
         if (lane == 0) {
-          atomicAdd(a.stats + cou, (double)s);
-          atomicAdd(a.stats + C + cou, (double)s2);
+          sStat[cou] += s;
+          sStat[C + cou] += s2;
         }
       }
     }
+    __syncthreads();  // sD / sIn reuse by the next tile
   }
+  if (a.stats)  // one contiguous f64 atomic vector per block
+    for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.stats + i, (double)sStat[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -181,36 +190,43 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdArgs a) {
   constexpr int P = 64;
   const int Cin = a.Cin, Cout = a.Cout, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int HWo = Ho * Wo;
-  const int pix0 = blockIdx.x * P;  // flat over N*Ho*Wo (HWo % 64 == 0)
-  const int n = pix0 / HWo;
-  const int prem = pix0 % HWo;
+  const int ntiles = a.N * HWo / P;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sX = smem;  // [Cin][P]
+  float* sX = smem;              // [Cin][P]
+  float* sStat = sX + Cin * P;   // [2*Cout]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (int i = tid; i < Cin * P; i += 256) {
-    int ci = i / P, p = i % P;
-    int pp = prem + p, oy = pp / Wo, ox = pp % Wo;
-    int iy = oy * a.S + a.off, ix = ox * a.S + a.off;
-    float v = 0.f;
-    if (iy < H && ix < W) v = fmaxf(a.x[(((size_t)n * Cin + ci) * H + iy) * W + ix], 0.f);
-    sX[i] = v;
-  }
-  __syncthreads();
-  for (int co = wave; co < Cout; co += 4) {
-    const int cou = __builtin_amdgcn_readfirstlane(co);
-    const float* wrow = a.pw + cou * Cin;
-    float v = 0.f;
-    for (int ci = 0; ci < Cin; ++ci) v += wrow[ci] * sX[ci * P + lane];
-    int pp = prem + lane;
-    a.z[((size_t)n * a.CoutTotal + a.co_off + cou) * HWo + pp] = v;
-    if (a.stats) {
+  for (int i = tid; i < 2 * Cout; i += 256) sStat[i] = 0.f;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int pix0 = t * P;  // flat over N*Ho*Wo (HWo % 64 == 0)
+    const int n = pix0 / HWo, prem = pix0 % HWo;
+    for (int i = tid; i < Cin * P; i += 256) {
+      int ci = i / P, p = i % P;
+      int pp = prem + p, oy = pp / Wo, ox = pp % Wo;
+      int iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+      float v = 0.f;
+      if (iy < H && ix < W) v = fmaxf(a.x[(((size_t)n * Cin + ci) * H + iy) * W + ix], 0.f);
+      sX[i] = v;
+    }
+    __syncthreads();
+    for (int co = wave; co < Cout; co += 4) {
+      const int cou = __builtin_amdgcn_readfirstlane(co);
+      const float* wrow = a.pw + cou * Cin;
+      float v = 0.f;
+      for (int ci = 0; ci < Cin; ++ci) v += wrow[ci] * sX[ci * P + lane];
+      a.z[((size_t)n * a.CoutTotal + a.co_off + cou) * HWo + prem + lane] = v;
       float s = wave_sum(v), s2 = wave_sum(v * v);
       if (lane == 0) {
-        atomicAdd(a.stats + a.co_off + cou, (double)s);
-        atomicAdd(a.stats + a.CoutTotal + a.co_off + cou, (double)s2);
+        sStat[cou] += s;
+        sStat[Cout + cou] += s2;
       }
     }
+    __syncthreads();
   }
+  if (a.stats)
+    for (int i = tid; i < 2 * Cout; i += 256) {
+      int hi = i >= Cout;
+      atomicAdd(a.stats + hi * a.CoutTotal + a.co_off + (i - hi * Cout), (double)sStat[i]);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -219,34 +235,37 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdArgs a) {
 template <int S>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdArgs a) {
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
-  const int nc = blockIdx.x, c = nc % C;
-  const float* xp = a.x + (size_t)nc * H * W;
+  const int c = blockIdx.x % C, g0 = blockIdx.x / C, G = gridDim.x / C;
   float sa = 0, sa2 = 0, sm = 0, sm2 = 0;
-  for (int o = threadIdx.x; o < Ho * Wo; o += 256) {
-    int oy = o / Wo, ox = o % Wo;
-    float sum = 0.f, mx = -INFINITY;
-    int cnt = 0;
-    for (int ky = 0; ky < 3; ++ky) {
-      int iy = oy * S - 1 + ky;
-      if (iy < 0 || iy >= H) continue;
-      for (int kx = 0; kx < 3; ++kx) {
-        int ix = ox * S - 1 + kx;
-        if (ix < 0 || ix >= W) continue;
-        float v = xp[iy * W + ix];
-        sum += v;
-        cnt++;
-        mx = (v > mx || v != v) ? v : mx;
+  for (int n = g0; n < a.N; n += G) {
+    const int nc = n * C + c;
+    const float* xp = a.x + (size_t)nc * H * W;
+    for (int o = threadIdx.x; o < Ho * Wo; o += 256) {
+      int oy = o / Wo, ox = o % Wo;
+      float sum = 0.f, mx = -INFINITY;
+      int cnt = 0;
+      for (int ky = 0; ky < 3; ++ky) {
+        int iy = oy * S - 1 + ky;
+        if (iy < 0 || iy >= H) continue;
+        for (int kx = 0; kx < 3; ++kx) {
+          int ix = ox * S - 1 + kx;
+          if (ix < 0 || ix >= W) continue;
+          float v = xp[iy * W + ix];
+          sum += v;
+          cnt++;
+          mx = (v > mx || v != v) ? v : mx;
+        }
       }
+      float av = sum / (float)cnt;
+      a.zavg[(size_t)nc * Ho * Wo + o] = av;
+      a.zmax[(size_t)nc * Ho * Wo + o] = mx;
+      sa += av;
+      sa2 += av * av;
+      sm += mx;
+      sm2 += mx * mx;
     }
-    float av = sum / (float)cnt;
-    a.zavg[(size_t)nc * Ho * Wo + o] = av;
-    a.zmax[(size_t)nc * Ho * Wo + o] = mx;
-    sa += av;
-    sa2 += av * av;
-    sm += mx;
-    sm2 += mx * mx;
   }
-  if (!a.stats_avg) return;
+  if (!a.stats_avg && !a.stats_max) return;
   __shared__ float red[4][4];
   sa = wave_sum(sa);
   sa2 = wave_sum(sa2);
@@ -263,7 +282,7 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdArgs a) {
   if (threadIdx.x < 4) {
     float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     double* dst = threadIdx.x < 2 ? a.stats_avg : a.stats_max;
-    atomicAdd(dst + (threadIdx.x & 1) * C + c, (double)t);
+    if (dst) atomicAdd(dst + (threadIdx.x & 1) * C + c, (double)t);
   }
 }
 
@@ -311,7 +330,7 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdArgs a) {
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdArgs a) {
   const int C = a.C, HW = a.HW;
-  const int nc = blockIdx.x, c = nc % C;
+  const int c = blockIdx.x % C, g0 = blockIdx.x / C, G = gridDim.x / C;
   __shared__ float sMean[kMaxOps], sInv[kMaxOps];
   __shared__ float red[4][kMaxOps + 2];
   if (threadIdx.x < a.nops) bn_coeffs(a.bn[threadIdx.x], c, sMean[threadIdx.x], sInv[threadIdx.x]);
@@ -320,14 +339,16 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdArgs 
   float s2[kMaxOps];
 #pragma unroll
   for (int k = 0; k < kMaxOps; ++k) s2[k] = 0.f;
-  const size_t base = (size_t)nc * HW;
-  for (int i = threadIdx.x; i < HW; i += 256) {
-    float g = a.dout[base + i];
-    s1 += g;
+  for (int n = g0; n < a.N; n += G) {
+    const size_t base = ((size_t)n * C + c) * HW;
+    for (int i = threadIdx.x; i < HW; i += 256) {
+      float g = a.dout[base + i];
+      s1 += g;
 #pragma unroll
-    for (int k = 0; k < kMaxOps; ++k)
-      if (k < a.nops) s2[k] += g * (a.z[k][base + i] - sMean[k]) * sInv[k];
-    if (a.xid) sid += g * a.xid[base + i];
+      for (int k = 0; k < kMaxOps; ++k)
+        if (k < a.nops) s2[k] += g * (a.z[k][base + i] - sMean[k]) * sInv[k];
+      if (a.xid) sid += g * a.xid[base + i];
+    }
   }
   int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   s1 = wave_sum(s1);
@@ -385,7 +406,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
   float* sInv = sMean + Cout;
   float* sW = sInv + Cout;       // [1]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (int c = tid; c < Cout; c += 256) bn_coeffs(a.gs.bn, c, sMean[c], sInv[c]);
+  for (int c = tid; c < Cout; c += 256) bn_coeffs(a.gs.bn, a.co_off + c, sMean[c], sInv[c]);
   if (tid == 0) sW[0] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
   __syncthreads();
   const float wk = sW[0];
@@ -468,112 +489,113 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int TR = P / Wo;
   const int tiles = Ho / TR;
-  const int n = blockIdx.x / tiles, tile = blockIdx.x % tiles;
-  const int oy0 = tile * TR;
+  const int ntiles = a.N * tiles;
   const int pad = a.pad;
   const int r = (K - 1) / 2 * DIL;         // == pad for these ops
   const int h = (r + S - 1) / S;           // halo output rows
   const int OR = TR + 2 * h;               // staged dd rows
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (Wo - 1) * S + (K - 1) * DIL + 1;
-  const int iy0 = oy0 * S - pad;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sDD = smem;                        // [CH][OR][Wo]
   float* sIn = sDD + a.chunk * OR * Wo;     // [CH][IR][IW]
   float* sMean = sIn + a.chunk * IR * IW;   // [C]
   float* sInv = sMean + C;
-  float* sRed = sInv + C;                   // [2][CH] per-block BN-bwd partials (PREBN)
+  float* sRed = sInv + C;                   // [2C] block-local BN-bwd partials (PREBN)
+  float* sGW = sRed + 2 * C;                // [C*K*K] block-local depthwise weight grads
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (PREBN) {
-    for (int c = tid; c < C; c += 256) bn_coeffs(a.inbn, c, sMean[c], sInv[c]);
-    __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    if (PREBN) bn_coeffs(a.inbn, c, sMean[c], sInv[c]);
+    sRed[c] = 0.f;
+    sRed[C + c] = 0.f;
   }
-  const float* xin = a.x + (size_t)n * C * H * W;
-  const float* ddn = a.dd + (size_t)n * C * Ho * Wo;
+  if (a.gW)
+    for (int i = tid; i < C * K * K; i += 256) sGW[i] = 0.f;
+  __syncthreads();
   const int own_in = TR * S;  // own input rows start at oy0*S
-  for (int c0 = 0; c0 < C; c0 += a.chunk) {
-    const int cn = min(a.chunk, C - c0);
-    for (int i = tid; i < cn * OR * Wo; i += 256) {
-      int cc = i / (OR * Wo), rr = (i / Wo) % OR, q = i % Wo;
-      int oy = oy0 - h + rr;
-      sDD[i] = (oy >= 0 && oy < Ho) ? ddn[((size_t)(c0 + cc) * Ho + oy) * Wo + q] : 0.f;
-    }
-    for (int i = tid; i < cn * IR * IW; i += 256) {
-      int cc = i / (IR * IW), rr = (i / IW) % IR, q = i % IW;
-      int iy = iy0 + rr, ix = -pad + q, c = c0 + cc;
-      float v = 0.f;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        v = xin[((size_t)c * H + iy) * W + ix];
-        if (PREBN) v = (v - sMean[c]) * sInv[c];
-        v = fmaxf(v, 0.f);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int n = t / tiles, oy0 = (t % tiles) * TR;
+    const int iy0 = oy0 * S - pad;
+    const float* xin = a.x + (size_t)n * C * H * W;
+    const float* ddn = a.dd + (size_t)n * C * Ho * Wo;
+    for (int c0 = 0; c0 < C; c0 += a.chunk) {
+      const int cn = min(a.chunk, C - c0);
+      for (int i = tid; i < cn * OR * Wo; i += 256) {
+        int cc = i / (OR * Wo), rr = (i / Wo) % OR, q = i % Wo;
+        int oy = oy0 - h + rr;
+        sDD[i] = (oy >= 0 && oy < Ho) ? ddn[((size_t)(c0 + cc) * Ho + oy) * Wo + q] : 0.f;
       }
-      sIn[i] = v;
-    }
-    if (PREBN)
-      for (int i = tid; i < 2 * a.chunk; i += 256) sRed[i] = 0.f;
-    __syncthreads();
-    // weight grads: one (channel, tap) per thread-group, reduce over own output pixels
-    if (a.gW) {
-      for (int job = wave; job < cn * K * K; job += 4) {
-        int cc = job / (K * K), tap = job % (K * K), ky = tap / K, kx = tap % K;
-        float s = 0.f;
-        for (int p = lane; p < P; p += 64) {
-          int ty = p / Wo, tx = p % Wo;
-          s += sDD[(cc * OR + h + ty) * Wo + tx] * sIn[(cc * IR + ty * S + ky * DIL) * IW + tx * S + kx * DIL];
+      if (a.gW) {
+        for (int i = tid; i < cn * IR * IW; i += 256) {
+          int cc = i / (IR * IW), rr = (i / IW) % IR, q = i % IW;
+          int iy = iy0 + rr, ix = -pad + q, c = c0 + cc;
+          float v = 0.f;
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+            v = xin[((size_t)c * H + iy) * W + ix];
+            if (PREBN) v = (v - sMean[c]) * sInv[c];
+            v = fmaxf(v, 0.f);
+          }
+          sIn[i] = v;
         }
-        s = wave_sum(s);
-        if (lane == 0) atomicAdd(a.gW + (c0 + cc) * K * K + tap, s);
       }
-    }
-    // input grads for own input rows
-    for (int i = tid; i < cn * own_in * W; i += 256) {
-      int cc = i / (own_in * W), rr = (i / W) % own_in, ix = i % W;
-      int c = c0 + cc;
-      int iy = oy0 * S + rr;
-      if (iy >= H) continue;
-      float ga = 0.f;
-      const float* wk = a.dw + c * K * K;
+      __syncthreads();
+      // weight grads: one (channel, tap) per wave, reduced over the tile's 64 output pixels;
+      // the (wave, job) assignment is the same for every tile, so lane 0 owns its sGW slot
+      if (a.gW) {
+        for (int job = wave; job < cn * K * K; job += 4) {
+          int cc = job / (K * K), tap = job % (K * K), ky = tap / K, kx = tap % K;
+          int ty = lane / Wo, tx = lane % Wo;
+          float s = sDD[(cc * OR + h + ty) * Wo + tx] * sIn[(cc * IR + ty * S + ky * DIL) * IW + tx * S + kx * DIL];
+          s = wave_sum(s);
+          if (lane == 0) sGW[(c0 + cc) * K * K + tap] += s;
+        }
+      }
+      // input grads for own input rows
+      for (int i = tid; i < cn * own_in * W; i += 256) {
+        int cc = i / (own_in * W), rr = (i / W) % own_in, ix = i % W;
+        int c = c0 + cc;
+        int iy = oy0 * S + rr;
+        if (iy >= H) continue;
+        float ga = 0.f;
+        const float* wk = a.dw + c * K * K;
 #pragma unroll
-      for (int ky = 0; ky < K; ++ky) {
-        int ty = iy + pad - ky * DIL;  // = oy * S
-        if (ty < 0 || ty % S) continue;
-        int oy = ty / S;
-        if (oy < 0 || oy >= Ho) continue;
-        int srow = oy - (oy0 - h);
+        for (int ky = 0; ky < K; ++ky) {
+          int ty = iy + pad - ky * DIL;  // = oy * S
+          if (ty < 0 || ty % S) continue;
+          int oy = ty / S;
+          if (oy < 0 || oy >= Ho) continue;
+          int srow = oy - (oy0 - h);
 #pragma unroll
-        for (int kx = 0; kx < K; ++kx) {
-          int tx = ix + pad - kx * DIL;
-          if (tx < 0 || tx % S) continue;
-          int ox = tx / S;
-          if (ox >= Wo) continue;
-          ga += wk[ky * K + kx] * sDD[(cc * OR + srow) * Wo + ox];
+          for (int kx = 0; kx < K; ++kx) {
+            int tx = ix + pad - kx * DIL;
+            if (tx < 0 || tx % S) continue;
+            int ox = tx / S;
+            if (ox >= Wo) continue;
+            ga += wk[ky * K + kx] * sDD[(cc * OR + srow) * Wo + ox];
+          }
         }
-      }
-      size_t xi = ((size_t)(n * C + c) * H + iy) * W + ix;
-      float xv = a.x[xi];
-      if (PREBN) {
-        float y = (xv - sMean[c]) * sInv[c];
-        float g = y > 0.f ? ga : 0.f;
-        a.gout[xi] = g;
-        if (a.red) {
-          atomicAdd(sRed + cc, g);  // LDS atomics; one global fp64 atomic per channel per block below
-          atomicAdd(sRed + a.chunk + cc, g * y);
+        size_t xi = ((size_t)(n * C + c) * H + iy) * W + ix;
+        float xv = a.x[xi];
+        if (PREBN) {
+          float y = (xv - sMean[c]) * sInv[c];
+          float g = y > 0.f ? ga : 0.f;
+          a.gout[xi] = g;
+          if (a.red) {
+            atomicAdd(sRed + c, g);  // LDS atomics; flushed once per block below
+            atomicAdd(sRed + C + c, g * y);
+          }
+        } else {
+          if (xv > 0.f) a.gout[xi] += ga;
         }
-      } else {
-        if (xv > 0.f) a.gout[xi] += ga;
-      }
-    }
-    __syncthreads();
-    if (PREBN && a.red) {
-      for (int cc = tid; cc < cn; cc += 256) {
-        atomicAdd(a.red + c0 + cc, (double)sRed[cc]);
-        atomicAdd(a.red + C + c0 + cc, (double)sRed[a.chunk + cc]);
       }
       __syncthreads();
     }
   }
+  if (PREBN && a.red)
+    for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.red + i, (double)sRed[i]);
+  if (a.gW)
+    for (int i = tid; i < C * K * K; i += 256) atomicAdd(a.gW + i, sGW[i]);
 }
-
 
 // ------------------------------------------------------------------------------------------------
 // pool_bwd: gx += avg^T(dz_avg) + max^T(dz_max) + wid * dout (identity skip), per (n,c) plane
@@ -641,8 +663,8 @@ static void launch_dwpw_fwd_t(const DwPwFwdArgs& a, bool prebn, hipStream_t st) 
   const int TR = 64 / a.Wo;
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
-  size_t lds = sizeof(float) * (a.C * 64 + a.chunk * IR * IW + 2 * a.C);
-  dim3 grid(a.N * (a.Ho / TR));
+  size_t lds = sizeof(float) * (a.C * 64 + a.chunk * IR * IW + 4 * a.C);
+  dim3 grid(std::min(a.N * (a.Ho / TR), kMaxBlocks));
   if (prebn) hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, a);
   else hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, a);
 }
@@ -661,8 +683,8 @@ static void launch_dw_bwd_t(const DwBwdArgs& a, bool prebn, hipStream_t st) {
   const int r = (K - 1) / 2 * DIL, h = (r + S - 1) / S, OR = TR + 2 * h;
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
-  size_t lds = sizeof(float) * (a.chunk * OR * a.Wo + a.chunk * IR * IW + 2 * a.C + 2 * a.chunk);
-  dim3 grid(a.N * (a.Ho / TR));
+  size_t lds = sizeof(float) * (a.chunk * OR * a.Wo + a.chunk * IR * IW + 4 * a.C + (a.gW ? a.C * K * K : 0));
+  dim3 grid(std::min(a.N * (a.Ho / TR), kMaxBlocks));
   if (prebn) hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, a);
   else hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, a);
 }
@@ -676,13 +698,16 @@ void launch_dw_bwd(const DwBwdArgs& a, int K, int dil, int S, bool prebn, hipStr
 }
 
 void launch_pw_fwd(const PwFwdArgs& a, hipStream_t st) {
-  size_t lds = sizeof(float) * a.Cin * 64;
-  hipLaunchKernelGGL(pw_fwd_kernel, dim3(a.N * a.Ho * a.Wo / 64), dim3(256), lds, st, a);
+  size_t lds = sizeof(float) * (a.Cin * 64 + 2 * a.Cout);
+  hipLaunchKernelGGL(pw_fwd_kernel, dim3(std::min(a.N * a.Ho * a.Wo / 64, kMaxBlocks)), dim3(256), lds, st, a);
 }
 
+static int channel_groups(int N, int C) { return std::max(1, std::min(N, kMaxBlocks / C)); }
+
 void launch_pool_fwd(const PoolFwdArgs& a, int S, hipStream_t st) {
-  if (S == 1) hipLaunchKernelGGL(pool_fwd_kernel<1>, dim3(a.N * a.C), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(pool_fwd_kernel<2>, dim3(a.N * a.C), dim3(256), 0, st, a);
+  dim3 grid(a.C * channel_groups(a.N, a.C));
+  if (S == 1) hipLaunchKernelGGL(pool_fwd_kernel<1>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(pool_fwd_kernel<2>, grid, dim3(256), 0, st, a);
 }
 
 void launch_pool_bwd(const PoolBwdArgs& a, int S, hipStream_t st) {
@@ -697,12 +722,12 @@ void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st) {
 }
 
 void launch_combine_bwd_reduce(const CombineBwdArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(combine_bwd_reduce_kernel, dim3(a.N * a.C), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(combine_bwd_reduce_kernel, dim3(a.C * channel_groups(a.N, a.C)), dim3(256), 0, st, a);
 }
 
 void launch_pw_bwd(const PwBwdArgs& a, hipStream_t st) {
   int ntiles = a.N * a.Ho * a.Wo / 64;
-  int blocks = std::min(ntiles, 1024);
+  int blocks = std::min(ntiles, kMaxBlocks);
   size_t lds = sizeof(float) * (a.Cout * 64 + a.Cin * 64 + 2 * a.Cout + 4);
   hipLaunchKernelGGL(pw_bwd_kernel, dim3(blocks), dim3(256), lds, st, a);
 }
