@@ -112,9 +112,13 @@ void pw_fwd(Tensor x, Tensor pw, Tensor z, OptT stats, int64_t co_off, int64_t S
   launch_pw_fwd(a, cur_stream());
 }
 
-void pool_fwd(Tensor x, Tensor zavg, Tensor zmax, OptT sa, OptT sm, int64_t S) {
+void pool_fwd(Tensor x, Tensor zavg, Tensor zmax, OptT sa, OptT sm, int64_t S, OptT amax) {
   check_f32(x, "x"); check_f32(zavg, "zavg"); check_f32(zmax, "zmax");
   PoolFwdArgs a{};
+  if (amax.has_value() && amax->defined()) {
+    TORCH_CHECK(amax->scalar_type() == at::kByte && amax->numel() == zmax.numel(), "amax must be uint8 like zmax");
+    a.amax = amax->data_ptr<uint8_t>();
+  }
   a.x = x.data_ptr<float>(); a.zavg = zavg.data_ptr<float>(); a.zmax = zmax.data_ptr<float>();
   a.stats_avg = ptr_or_null<double>(sa); a.stats_max = ptr_or_null<double>(sm);
   a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = zavg.size(2); a.Wo = zavg.size(3);
@@ -221,11 +225,17 @@ void dw_bwd(Tensor x, c10::optional<py::tuple> inbn, Tensor dw, Tensor dd, Tenso
 }
 
 void pool_bwd(c10::optional<py::tuple> ga, c10::optional<py::tuple> gm, Tensor x, OptT dout_id, OptT w,
-              int64_t id_idx, Tensor gx, int64_t S) {
+              int64_t id_idx, Tensor gx, int64_t S, OptT amax) {
   check_f32(x, "x"); check_f32(gx, "gx");
   PoolBwdArgs a{};
   a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3);
   a.Ho = (a.H - 1) / S + 1; a.Wo = (a.W - 1) / S + 1;
+  TORCH_CHECK(a.Ho * a.Wo <= 8192, "pool_bwd stages one output plane in LDS (Ho*Wo <= 8192)");
+  TORCH_CHECK(gx.sizes() == x.sizes(), "gx shape");
+  TORCH_CHECK(!gm.has_value() || (amax.has_value() && amax->defined() && amax->scalar_type() == at::kByte &&
+                                  amax->numel() == (int64_t)a.N * a.C * a.Ho * a.Wo),
+              "max-pool backward needs the uint8 argmax from pool_fwd");
+  if (amax.has_value() && amax->defined()) a.amax = amax->data_ptr<uint8_t>();
   if (ga.has_value()) a.ga = make_gs(*ga, a.C);
   if (gm.has_value()) a.gm = make_gs(*gm, a.C);
   a.x = x.data_ptr<float>(); a.dout_id = ptr_or_null<float>(dout_id); a.w = ptr_or_null<float>(w);
@@ -245,4 +255,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pw_bwd", &pw_bwd);
   m.def("dw_bwd", &dw_bwd);
   m.def("pool_bwd", &pool_bwd);
+  m.def("set_max_blocks", &set_max_blocks);
+  m.def("max_blocks", &max_blocks);
 }

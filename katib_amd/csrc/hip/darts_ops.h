@@ -40,7 +40,7 @@ struct PwFwdArgs {
 };
 
 struct PoolFwdArgs {
-  const float* x; float* zavg; float* zmax; double* stats_avg; double* stats_max;
+  const float* x; float* zavg; float* zmax; double* stats_avg; double* stats_max; unsigned char* amax;
   int N, C, H, W, Ho, Wo;
 };
 
@@ -69,6 +69,7 @@ struct DwBwdArgs {
 
 struct PoolBwdArgs {
   GradSrc ga; GradSrc gm; const float* x; const float* dout_id; const float* w; int id_idx; float* gx;
+  const unsigned char* amax;
   int N, C, H, W, Ho, Wo;
 };
 
@@ -80,5 +81,7 @@ void launch_pool_bwd(const PoolBwdArgs& a, int S, hipStream_t st);
 void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st);
 void launch_combine_bwd_reduce(const CombineBwdArgs& a, hipStream_t st);
 void launch_pw_bwd(const PwBwdArgs& a, hipStream_t st);
+int max_blocks();
+void set_max_blocks(int n);
 
 }  // namespace katib_hip

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "darts_ops.h"
 
@@ -34,7 +35,16 @@ namespace katib_hip {
 // and flushed as ONE lane-contiguous atomic vector per block - global float atomics
 // execute memory-side, and many single-lane adds to the same address serialise
 // (MI355X_MICROARCH.md "Global float atomics").
-constexpr int kMaxBlocks = 512;
+// Cap tunable with KATIB_HIP_MAX_BLOCKS (host side, read once).
+static int g_max_blocks = 0;
+int max_blocks() {
+  if (g_max_blocks <= 0) {
+    const char* e = getenv("KATIB_HIP_MAX_BLOCKS");
+    g_max_blocks = e ? std::max(1, atoi(e)) : 1024;
+  }
+  return g_max_blocks;
+}
+void set_max_blocks(int n) { g_max_blocks = n; }
 
 __device__ __forceinline__ void bn_coeffs(const BNRef& b, int c, float& mean, float& invstd) {
   if (b.eval) {
@@ -109,8 +119,9 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdArgs a) {
       }
       __syncthreads();
       for (int i = tid; i < cn * P; i += 256) {
-        int cc = i / P, p = i % P;
-        int c = c0 + cc;
+        const int cc = __builtin_amdgcn_readfirstlane(i / P);  // wave-uniform: weights via scalar loads
+        const int p = i % P;
+        const int c = c0 + cc;
         int ty = p / Wo, tx = p % Wo;
         const float* wk = a.dw + c * K * K;
         const float* src = sIn + (cc * IR + ty * S) * IW + tx * S;
@@ -243,7 +254,7 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdArgs a) {
     for (int o = threadIdx.x; o < Ho * Wo; o += 256) {
       int oy = o / Wo, ox = o % Wo;
       float sum = 0.f, mx = -INFINITY;
-      int cnt = 0;
+      int cnt = 0, arg = 0;
       for (int ky = 0; ky < 3; ++ky) {
         int iy = oy * S - 1 + ky;
         if (iy < 0 || iy >= H) continue;
@@ -253,12 +264,16 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdArgs a) {
           float v = xp[iy * W + ix];
           sum += v;
           cnt++;
-          mx = (v > mx || v != v) ? v : mx;
+          if (v > mx || v != v) {  // first maximal element in row-major order (max_pool2d)
+            mx = v;
+            arg = ky * 3 + kx;
+          }
         }
       }
       float av = sum / (float)cnt;
       a.zavg[(size_t)nc * Ho * Wo + o] = av;
       a.zmax[(size_t)nc * Ho * Wo + o] = mx;
+      if (a.amax) a.amax[(size_t)nc * Ho * Wo + o] = (unsigned char)arg;
       sa += av;
       sa2 += av * av;
       sm += mx;
@@ -395,14 +410,15 @@ __device__ __forceinline__ float bn_bwd_val(const GradSrc& gs, size_t i, int c, 
 // mode 1 (StdConv / FR half): a_in = relu(x) at strided positions; gx += dd * (x > 0).
 // grid: persistent over 64-pixel tiles; weight grads accumulated in registers across tiles.
 // ------------------------------------------------------------------------------------------------
+template <bool MFMA>
 __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
-  constexpr int P = 64;
+  constexpr int P = 64, PS = P + 1;  // padded LDS rows: per-channel row reads hit distinct banks
   const int Cin = a.Cin, Cout = a.Cout, Ho = a.Ho, Wo = a.Wo, HWo = Ho * Wo;
   const int ntiles = a.N * HWo / P;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sDz = smem;             // [Cout][P]
-  float* sA = sDz + Cout * P;    // [Cin][P]
-  float* sMean = sA + Cin * P;   // [Cout]
+  float* sDz = smem;             // [Cout][PS]
+  float* sA = sDz + Cout * PS;   // [Cin][PS]
+  float* sMean = sA + Cin * PS;  // [Cout]
   float* sInv = sMean + Cout;
   float* sW = sInv + Cout;       // [1]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -410,18 +426,24 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
   if (tid == 0) sW[0] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
   __syncthreads();
   const float wk = sW[0];
-  // per-thread weight-grad accumulators: pairs (co, ci) = tid + 256*j
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  // weight-grad accumulators live in registers across tiles.
+  // scalar path: pairs (co, ci) = tid + 256*j; MFMA path: 16x16 blocks b = wave + 4*j
   constexpr int MAXJ = 16;  // Cout*Cin <= 4096
-  float gacc[MAXJ];
+  float gacc[MFMA ? 1 : MAXJ];
+  f4 macc[MFMA ? 4 : 1];
 #pragma unroll
-  for (int j = 0; j < MAXJ; ++j) gacc[j] = 0.f;
+  for (int j = 0; j < (MFMA ? 1 : MAXJ); ++j) gacc[j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < (MFMA ? 4 : 1); ++j) macc[j] = f4{0, 0, 0, 0};
   const int npairs = Cout * Cin;
+  const int nbi = Cin / 16, nblk = (Cout / 16) * nbi;
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int pix0 = t * P, n = pix0 / HWo, prem = pix0 % HWo;
     for (int i = tid; i < Cout * P; i += 256) {
       int co = i / P, p = i % P;
       size_t gi = ((size_t)n * a.CoutTotal + a.co_off + co) * HWo + prem + p;
-      sDz[i] = bn_bwd_val(a.gs, gi, a.co_off + co, sMean[co], sInv[co], wk);
+      sDz[co * PS + p] = bn_bwd_val(a.gs, gi, a.co_off + co, sMean[co], sInv[co], wk);
     }
     for (int i = tid; i < Cin * P; i += 256) {
       int ci = i / P, p = i % P;
@@ -433,35 +455,83 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
         int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
         v = (iy < a.H && ix < a.W) ? fmaxf(a.x[(((size_t)n * Cin + ci) * a.H + iy) * a.W + ix], 0.f) : 0.f;
       }
-      sA[i] = v;
+      sA[ci * PS + p] = v;
     }
     __syncthreads();
     if (a.gW) {
+      if (MFMA) {
+        // gW[co][ci] += sum_p dz[co][p] * a[ci][p]  (M = co, N = ci, K = pixels)
 #pragma unroll
-      for (int j = 0; j < MAXJ; ++j) {
-        int pr = tid + 256 * j;
-        if (pr < npairs) {
-          int co = pr / Cin, ci = pr % Cin;
-          float s = 0.f;
-          for (int p = 0; p < P; ++p) s += sDz[co * P + p] * sA[ci * P + p];
-          gacc[j] += s;
+        for (int j = 0; j < 4; ++j) {
+          int b = wave + 4 * j;
+          if (b < nblk) {
+            int cob = (b / nbi) * 16, cib = (b % nbi) * 16;
+            for (int p0 = 0; p0 < P; p0 += 4) {
+              float av = sDz[(cob + (lane & 15)) * PS + p0 + (lane >> 4)];
+              float bv = sA[(cib + (lane & 15)) * PS + p0 + (lane >> 4)];
+              macc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, macc[j], 0, 0, 0);
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j) {
+          int pr = tid + 256 * j;
+          if (pr < npairs) {
+            int co = pr / Cin, ci = pr % Cin;
+            float s = 0.f;
+            for (int p = 0; p < P; ++p) s += sDz[co * PS + p] * sA[ci * PS + p];
+            gacc[j] += s;
+          }
         }
       }
     }
     // dd[ci][p] = sum_co pw[co][ci] dz[co][p]
     if (a.need_dx) {
-      for (int ci = wave; ci < Cin; ci += 4) {
-        const int ciu = __builtin_amdgcn_readfirstlane(ci);
-        float v = 0.f;
-        for (int co = 0; co < Cout; ++co) v += a.pw[co * Cin + ciu] * sDz[co * P + lane];
-        int pp = prem + lane;
-        if (a.mode == 0) {
-          a.dd[((size_t)n * Cin + ciu) * HWo + pp] = v;
-        } else {
-          int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
-          if (iy < a.H && ix < a.W) {
-            size_t xi = (((size_t)n * Cin + ciu) * a.H + iy) * a.W + ix;
-            if (a.x[xi] > 0.f) a.gx[xi] += v;
+      if (MFMA) {
+        for (int cib = wave * 16; cib < Cin; cib += 64) {
+          f4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+          for (int k0 = 0; k0 < Cout; k0 += 4) {
+            float av = a.pw[(k0 + (lane >> 4)) * Cin + cib + (lane & 15)];
+#pragma unroll
+            for (int pb = 0; pb < 4; ++pb) {
+              float bv = sDz[(k0 + (lane >> 4)) * PS + pb * 16 + (lane & 15)];
+              acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[pb], 0, 0, 0);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            int ci = cib + (lane >> 4) * 4 + r;
+#pragma unroll
+            for (int pb = 0; pb < 4; ++pb) {
+              int pp = prem + pb * 16 + (lane & 15);
+              float v = acc[pb][r];
+              if (a.mode == 0) {
+                a.dd[((size_t)n * Cin + ci) * HWo + pp] = v;
+              } else {
+                int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+                if (iy < a.H && ix < a.W) {
+                  size_t xi = (((size_t)n * Cin + ci) * a.H + iy) * a.W + ix;
+                  if (a.x[xi] > 0.f) a.gx[xi] += v;
+                }
+              }
+            }
+          }
+        }
+      } else {
+        for (int ci = wave; ci < Cin; ci += 4) {
+          const int ciu = __builtin_amdgcn_readfirstlane(ci);
+          float v = 0.f;
+          for (int co = 0; co < Cout; ++co) v += a.pw[co * Cin + ciu] * sDz[co * PS + lane];
+          int pp = prem + lane;
+          if (a.mode == 0) {
+            a.dd[((size_t)n * Cin + ciu) * HWo + pp] = v;
+          } else {
+            int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+            if (iy < a.H && ix < a.W) {
+              size_t xi = (((size_t)n * Cin + ciu) * a.H + iy) * a.W + ix;
+              if (a.x[xi] > 0.f) a.gx[xi] += v;
+            }
           }
         }
       }
@@ -469,10 +539,23 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
     __syncthreads();
   }
   if (a.gW) {
+    if (MFMA) {
 #pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
-      int pr = tid + 256 * j;
-      if (pr < npairs) atomicAdd(a.gW + pr, gacc[j]);
+      for (int j = 0; j < 4; ++j) {
+        int b = wave + 4 * j;
+        if (b < nblk) {
+          int cob = (b / nbi) * 16, cib = (b % nbi) * 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            atomicAdd(a.gW + (cob + (lane >> 4) * 4 + r) * Cin + cib + (lane & 15), macc[j][r]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) {
+        int pr = tid + 256 * j;
+        if (pr < npairs) atomicAdd(a.gW + pr, gacc[j]);
+      }
     }
   }
 }
@@ -485,7 +568,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
 // ------------------------------------------------------------------------------------------------
 template <int K, int DIL, int S, bool PREBN>
 __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
-  constexpr int P = 64;
+  constexpr int P = 64, KK = K * K;
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int TR = P / Wo;
   const int tiles = Ho / TR;
@@ -510,9 +593,10 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
     sRed[C + c] = 0.f;
   }
   if (a.gW)
-    for (int i = tid; i < C * K * K; i += 256) sGW[i] = 0.f;
+    for (int i = tid; i < C * KK; i += 256) sGW[i] = 0.f;
   __syncthreads();
-  const int own_in = TR * S;  // own input rows start at oy0*S
+  const int own_in = TR * S;  // own input rows [oy0*S, oy0*S + own_in)
+  const int nq = own_in * W;
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int n = t / tiles, oy0 = (t % tiles) * TR;
     const int iy0 = oy0 * S - pad;
@@ -539,53 +623,72 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
         }
       }
       __syncthreads();
-      // weight grads: one (channel, tap) per wave, reduced over the tile's 64 output pixels;
-      // the (wave, job) assignment is the same for every tile, so lane 0 owns its sGW slot
+      // weight grads: thread per (channel, tap), summed over the tile's 64 output pixels
       if (a.gW) {
-        for (int job = wave; job < cn * K * K; job += 4) {
-          int cc = job / (K * K), tap = job % (K * K), ky = tap / K, kx = tap % K;
-          int ty = lane / Wo, tx = lane % Wo;
-          float s = sDD[(cc * OR + h + ty) * Wo + tx] * sIn[(cc * IR + ty * S + ky * DIL) * IW + tx * S + kx * DIL];
-          s = wave_sum(s);
-          if (lane == 0) sGW[(c0 + cc) * K * K + tap] += s;
+        for (int job = tid; job < cn * KK; job += 256) {
+          const int cc = job / KK, tap = job % KK, ky = tap / K, kx = tap % K;
+          const float* dd = sDD + (cc * OR + h) * Wo;
+          const float* in = sIn + (cc * IR + ky * DIL) * IW + kx * DIL;
+          float s = 0.f;
+          for (int ty = 0; ty < TR; ++ty)
+            for (int tx = 0; tx < Wo; ++tx) s += dd[ty * Wo + tx] * in[ty * S * IW + tx * S];
+          sGW[(c0 + cc) * KK + tap] += s;  // unique owner
         }
       }
-      // input grads for own input rows
-      for (int i = tid; i < cn * own_in * W; i += 256) {
-        int cc = i / (own_in * W), rr = (i / W) % own_in, ix = i % W;
-        int c = c0 + cc;
-        int iy = oy0 * S + rr;
-        if (iy >= H) continue;
-        float ga = 0.f;
-        const float* wk = a.dw + c * K * K;
+      // input grads for own input rows: the tap geometry depends only on the pixel q, so it
+      // is computed once per pixel (branch-free masks) and reused for every channel
+      for (int q0 = 0; q0 < nq; q0 += 256) {
+        const int q = q0 + tid;
+        const int rr = q / W, ix = q - rr * W;
+        const int iy = oy0 * S + rr;
+        const bool ok = q < nq && iy < H;
+        int srow[K], ocol[K];
+        float mrow[K], mcol[K];
 #pragma unroll
-        for (int ky = 0; ky < K; ++ky) {
-          int ty = iy + pad - ky * DIL;  // = oy * S
-          if (ty < 0 || ty % S) continue;
-          int oy = ty / S;
-          if (oy < 0 || oy >= Ho) continue;
-          int srow = oy - (oy0 - h);
-#pragma unroll
-          for (int kx = 0; kx < K; ++kx) {
-            int tx = ix + pad - kx * DIL;
-            if (tx < 0 || tx % S) continue;
-            int ox = tx / S;
-            if (ox >= Wo) continue;
-            ga += wk[ky * K + kx] * sDD[(cc * OR + srow) * Wo + ox];
-          }
+        for (int k = 0; k < K; ++k) {
+          int ty = iy + pad - k * DIL;  // = oy * S when valid
+          int oy = ty >= 0 ? ty / S : -1;
+          bool v = ok && ty >= 0 && (ty % S) == 0 && oy < Ho;
+          srow[k] = v ? oy - (oy0 - h) : 0;
+          mrow[k] = v ? 1.f : 0.f;
+          int tx = ix + pad - k * DIL;
+          int ox = tx >= 0 ? tx / S : -1;
+          bool u = ok && tx >= 0 && (tx % S) == 0 && ox < Wo;
+          ocol[k] = u ? ox : 0;
+          mcol[k] = u ? 1.f : 0.f;
         }
-        size_t xi = ((size_t)(n * C + c) * H + iy) * W + ix;
-        float xv = a.x[xi];
-        if (PREBN) {
-          float y = (xv - sMean[c]) * sInv[c];
-          float g = y > 0.f ? ga : 0.f;
-          a.gout[xi] = g;
-          if (a.red) {
-            atomicAdd(sRed + c, g);  // LDS atomics; flushed once per block below
-            atomicAdd(sRed + C + c, g * y);
+        for (int cc = 0; cc < cn; ++cc) {
+          const int c = c0 + cc;
+          const float* wk = a.dw + c * KK;  // wave-uniform -> scalar loads
+          const float* dd = sDD + cc * OR * Wo;
+          float ga = 0.f;
+#pragma unroll
+          for (int ky = 0; ky < K; ++ky) {
+            float rowacc = 0.f;
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) rowacc += mcol[kx] * wk[ky * K + kx] * dd[srow[ky] * Wo + ocol[kx]];
+            ga += mrow[ky] * rowacc;
           }
-        } else {
-          if (xv > 0.f) a.gout[xi] += ga;
+          const size_t xi = ((size_t)(n * C + c) * H + iy) * W + ix;
+          if (PREBN) {
+            float g = 0.f, gy = 0.f;
+            if (ok) {
+              float y = (a.x[xi] - sMean[c]) * sInv[c];
+              g = y > 0.f ? ga : 0.f;
+              gy = g * y;
+              a.gout[xi] = g;
+            }
+            if (a.red) {
+              g = wave_sum(g);
+              gy = wave_sum(gy);
+              if (lane == 0) {
+                atomicAdd(sRed + c, g);  // one LDS atomic per wave per channel
+                atomicAdd(sRed + C + c, gy);
+              }
+            }
+          } else if (ok) {
+            if (a.x[xi] > 0.f) a.gout[xi] += ga;
+          }
         }
       }
       __syncthreads();
@@ -594,7 +697,7 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
   if (PREBN && a.red)
     for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.red + i, (double)sRed[i]);
   if (a.gW)
-    for (int i = tid; i < C * K * K; i += 256) atomicAdd(a.gW + i, sGW[i]);
+    for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + i, sGW[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -602,52 +705,49 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
 // ------------------------------------------------------------------------------------------------
 template <int S>
 __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdArgs a) {
-  const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, HWo = Ho * Wo;
   const int nc = blockIdx.x, c = nc % C;
-  const float* xp = a.x + (size_t)nc * H * W;
-  const size_t ob = (size_t)nc * Ho * Wo;
+  const size_t ob = (size_t)nc * HWo;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sGa = smem;                                          // [HWo] dz_avg / window count
+  float* sGm = smem + HWo;                                    // [HWo] dz_max
+  unsigned char* sArg = (unsigned char*)(smem + 2 * HWo);     // [HWo] argmax tap
   float ma = 0, ia = 1, mm = 0, im = 1;
   if (a.ga.z) bn_coeffs(a.ga.bn, c, ma, ia);
   if (a.gm.z) bn_coeffs(a.gm.bn, c, mm, im);
-  float wa = a.ga.w ? a.ga.w[a.ga.widx] : 0.f;
-  float wm = a.gm.w ? a.gm.w[a.gm.widx] : 0.f;
-  float wid = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+  const float wa = a.ga.w ? a.ga.w[a.ga.widx] : 0.f;
+  const float wm = a.gm.w ? a.gm.w[a.gm.widx] : 0.f;
+  const float wid = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+  for (int o = threadIdx.x; o < HWo; o += 256) {
+    int oy = o / Wo, ox = o % Wo;
+    if (a.ga.z) {
+      int y0 = max(oy * S - 1, 0), y1 = min(oy * S + 1, H - 1);
+      int x0 = max(ox * S - 1, 0), x1 = min(ox * S + 1, W - 1);
+      sGa[o] = bn_bwd_val(a.ga, ob + o, c, ma, ia, wa) / (float)((y1 - y0 + 1) * (x1 - x0 + 1));
+    } else {
+      sGa[o] = 0.f;
+    }
+    if (a.gm.z) {
+      sGm[o] = bn_bwd_val(a.gm, ob + o, c, mm, im, wm);
+      sArg[o] = a.amax[ob + o];
+    } else {
+      sGm[o] = 0.f;
+      sArg[o] = 255;
+    }
+  }
+  __syncthreads();
   for (int q = threadIdx.x; q < H * W; q += 256) {
     int iy = q / W, ix = q % W;
     float g = 0.f;
     // outputs whose 3x3 window (pad 1) covers (iy, ix): oy*S - 1 <= iy <= oy*S + 1
-    int oy_lo = (iy - 1 + S - 1) / S; if (iy - 1 < 0) oy_lo = 0;
-    int oy_hi = (iy + 1) / S;
-    int ox_lo = (ix - 1 + S - 1) / S; if (ix - 1 < 0) ox_lo = 0;
-    int ox_hi = (ix + 1) / S;
-    for (int oy = oy_lo; oy <= oy_hi && oy < Ho; ++oy) {
-      for (int ox = ox_lo; ox <= ox_hi && ox < Wo; ++ox) {
-        size_t oi = ob + oy * Wo + ox;
-        if (a.ga.z) {
-          int y0 = max(oy * S - 1, 0), y1 = min(oy * S + 1, H - 1);
-          int x0 = max(ox * S - 1, 0), x1 = min(ox * S + 1, W - 1);
-          float cnt = (float)((y1 - y0 + 1) * (x1 - x0 + 1));
-          g += bn_bwd_val(a.ga, oi, c, ma, ia, wa) / cnt;
-        }
-        if (a.gm.z) {
-          // first maximal element in row-major window order (PyTorch max_pool2d semantics)
-          float mx = -INFINITY;
-          int arg = -1;
-          for (int ky = 0; ky < 3; ++ky) {
-            int yy = oy * S - 1 + ky;
-            if (yy < 0 || yy >= H) continue;
-            for (int kx = 0; kx < 3; ++kx) {
-              int xx = ox * S - 1 + kx;
-              if (xx < 0 || xx >= W) continue;
-              float v = xp[yy * W + xx];
-              if (v > mx || v != v) {
-                mx = v;
-                arg = yy * W + xx;
-              }
-            }
-          }
-          if (arg == q) g += bn_bwd_val(a.gm, oi, c, mm, im, wm);
-        }
+    int oy_lo = iy - 1 < 0 ? 0 : (iy - 1 + S - 1) / S, oy_hi = min((iy + 1) / S, Ho - 1);
+    int ox_lo = ix - 1 < 0 ? 0 : (ix - 1 + S - 1) / S, ox_hi = min((ix + 1) / S, Wo - 1);
+    for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+      for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+        int o = oy * Wo + ox;
+        g += sGa[o];
+        int tap = (iy - oy * S + 1) * 3 + (ix - ox * S + 1);
+        if (sArg[o] == tap) g += sGm[o];
       }
     }
     if (a.dout_id) g += wid * a.dout_id[(size_t)nc * H * W + q];
@@ -664,7 +764,7 @@ static void launch_dwpw_fwd_t(const DwPwFwdArgs& a, bool prebn, hipStream_t st) 
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
   size_t lds = sizeof(float) * (a.C * 64 + a.chunk * IR * IW + 4 * a.C);
-  dim3 grid(std::min(a.N * (a.Ho / TR), kMaxBlocks));
+  dim3 grid(std::min(a.N * (a.Ho / TR), max_blocks()));
   if (prebn) hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, a);
   else hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, a);
 }
@@ -684,7 +784,7 @@ static void launch_dw_bwd_t(const DwBwdArgs& a, bool prebn, hipStream_t st) {
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
   size_t lds = sizeof(float) * (a.chunk * OR * a.Wo + a.chunk * IR * IW + 4 * a.C + (a.gW ? a.C * K * K : 0));
-  dim3 grid(std::min(a.N * (a.Ho / TR), kMaxBlocks));
+  dim3 grid(std::min(a.N * (a.Ho / TR), max_blocks()));
   if (prebn) hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, a);
   else hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, a);
 }
@@ -699,10 +799,10 @@ void launch_dw_bwd(const DwBwdArgs& a, int K, int dil, int S, bool prebn, hipStr
 
 void launch_pw_fwd(const PwFwdArgs& a, hipStream_t st) {
   size_t lds = sizeof(float) * (a.Cin * 64 + 2 * a.Cout);
-  hipLaunchKernelGGL(pw_fwd_kernel, dim3(std::min(a.N * a.Ho * a.Wo / 64, kMaxBlocks)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(pw_fwd_kernel, dim3(std::min(a.N * a.Ho * a.Wo / 64, max_blocks())), dim3(256), lds, st, a);
 }
 
-static int channel_groups(int N, int C) { return std::max(1, std::min(N, kMaxBlocks / C)); }
+static int channel_groups(int N, int C) { return std::max(1, std::min(N, max_blocks() / C)); }
 
 void launch_pool_fwd(const PoolFwdArgs& a, int S, hipStream_t st) {
   dim3 grid(a.C * channel_groups(a.N, a.C));
@@ -711,8 +811,9 @@ void launch_pool_fwd(const PoolFwdArgs& a, int S, hipStream_t st) {
 }
 
 void launch_pool_bwd(const PoolBwdArgs& a, int S, hipStream_t st) {
-  if (S == 1) hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(a.N * a.C), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(pool_bwd_kernel<2>, dim3(a.N * a.C), dim3(256), 0, st, a);
+  size_t lds = sizeof(float) * 2 * a.Ho * a.Wo + a.Ho * a.Wo + 16;
+  if (S == 1) hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(a.N * a.C), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL(pool_bwd_kernel<2>, dim3(a.N * a.C), dim3(256), lds, st, a);
 }
 
 void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st) {
@@ -727,9 +828,11 @@ void launch_combine_bwd_reduce(const CombineBwdArgs& a, hipStream_t st) {
 
 void launch_pw_bwd(const PwBwdArgs& a, hipStream_t st) {
   int ntiles = a.N * a.Ho * a.Wo / 64;
-  int blocks = std::min(ntiles, kMaxBlocks);
-  size_t lds = sizeof(float) * (a.Cout * 64 + a.Cin * 64 + 2 * a.Cout + 4);
-  hipLaunchKernelGGL(pw_bwd_kernel, dim3(blocks), dim3(256), lds, st, a);
+  int blocks = std::min(ntiles, max_blocks());
+  size_t lds = sizeof(float) * (a.Cout * 65 + a.Cin * 65 + 2 * a.Cout + 4);
+  const bool mfma = a.Cin % 16 == 0 && a.Cout % 16 == 0 && (a.Cin / 16) * (a.Cout / 16) <= 16;
+  if (mfma) hipLaunchKernelGGL(pw_bwd_kernel<true>, dim3(blocks), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL(pw_bwd_kernel<false>, dim3(blocks), dim3(256), lds, st, a);
 }
 
 

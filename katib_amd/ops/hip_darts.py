@@ -117,10 +117,11 @@ class _MixedEdge(torch.autograd.Function):
                 if "pool" not in saved:
                     za = torch.empty(N, C, Ho, Wo, device=dev)
                     zm = torch.empty_like(za)
+                    am = torch.empty(N, C, Ho, Wo, dtype=torch.uint8, device=dev)
                     sa = spec.slots.get("avg_pooling_3x3")
                     sm = spec.slots.get("max_pooling_3x3")
-                    _K.pool_fwd(x, za, zm, st(sa[0]) if sa else None, st(sm[0]) if sm else None, S)
-                    saved["pool"] = (za, zm)
+                    _K.pool_fwd(x, za, zm, st(sa[0]) if sa else None, st(sm[0]) if sm else None, S, am)
+                    saved["pool"] = (za, zm, am)
                 zs.append(saved["pool"][0 if prim == "avg_pooling_3x3" else 1])
                 bns.append(refs[sl[0]])
             elif prim == "skip_connection":
@@ -208,14 +209,14 @@ class _MixedEdge(torch.autograd.Function):
                 if pool_done or not need_x:
                     continue
                 pool_done = True
-                za, zm = saved["pool"]
+                za, zm, am = saved["pool"]
                 ga = gm = None
                 for kk, pp in enumerate(spec.prims):
                     if pp == "avg_pooling_3x3":
                         ga = src(kk, za)
                     elif pp == "max_pooling_3x3":
                         gm = src(kk, zm)
-                _K.pool_bwd(ga, gm, x, dout if id_idx >= 0 else None, w, id_idx, gx, S)
+                _K.pool_bwd(ga, gm, x, dout if id_idx >= 0 else None, w, id_idx, gx, S, am)
             elif prim == "skip_connection" and S != 1:
                 (z,) = saved[prim]
                 gs = src(k, z)
