@@ -26,12 +26,18 @@ T* ptr_or_null(const OptT& t) {
   return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
 }
 
-// bn tuple: (sums: Optional[f64 tensor], rmean, rvar, inv_count, eval, eps)
+// bn tuple: (sums: Optional[f64 tensor], rmean, rvar, inv_count, eval, eps, rep, rstride)
 BNRef make_bn(const py::tuple& b, int C) {
   BNRef r{};
+  TORCH_CHECK(b.size() == 8, "bn tuple has 8 fields");
   OptT sums = b[0].cast<OptT>(), rm = b[1].cast<OptT>(), rv = b[2].cast<OptT>();
+  r.rep = b[6].cast<int>();
+  r.rstride = b[7].cast<int>();
+  TORCH_CHECK(r.rep >= 1 && r.rep <= kRep && r.rstride >= 2 * C, "bn replica layout");
   if (sums.has_value() && sums->defined()) {
-    TORCH_CHECK(sums->scalar_type() == at::kDouble && sums->numel() >= 2 * C, "bn sums must be f64 [2C]");
+    TORCH_CHECK(sums->scalar_type() == at::kDouble && sums->is_contiguous() &&
+                    sums->numel() >= (int64_t)(r.rep - 1) * r.rstride + 2 * C,
+                "bn sums must be f64 with rep x rstride doubles");
   }
   r.sums = ptr_or_null<double>(sums);
   r.rmean = ptr_or_null<float>(rm);
@@ -44,9 +50,15 @@ BNRef make_bn(const py::tuple& b, int C) {
   return r;
 }
 
-// grad source tuple: (g, z, S1 (f64 view [C]), S2 (f64 view [C]), bn tuple, w: Optional, widx)
+// grad source tuple: (g, z, S1 (f64 view), S2 (f64 view), bn tuple, w: Optional, widx, rep, rstride)
+// replica r of S1/S2 starts r*rstride doubles after the view's first element
+int64_t storage_doubles_after(const Tensor& t) {
+  return (int64_t)(t.storage().nbytes() / sizeof(double)) - t.storage_offset();
+}
+
 GradSrc make_gs(const py::tuple& t, int C) {
   GradSrc g{};
+  TORCH_CHECK(t.size() == 9, "grad-source tuple has 9 fields");
   Tensor gt = t[0].cast<Tensor>(), zt = t[1].cast<Tensor>();
   check_f32(gt, "g");
   check_f32(zt, "z");
@@ -61,6 +73,17 @@ GradSrc make_gs(const py::tuple& t, int C) {
   OptT w = t[5].cast<OptT>();
   g.w = ptr_or_null<float>(w);
   g.widx = t[6].cast<int>();
+  g.rep = t[7].cast<int>();
+  g.rstride = t[8].cast<int>();
+  TORCH_CHECK(g.rep >= 1 && g.rep <= kRep, "replicas");
+  if (!g.eval) {
+    for (int k = 2; k <= 3; ++k) {
+      Tensor sv = *t[k].cast<OptT>();
+      TORCH_CHECK(sv.scalar_type() == at::kDouble &&
+                      storage_doubles_after(sv) >= (int64_t)(g.rep - 1) * g.rstride + C,
+                  "S1/S2 replicas exceed their buffer");
+    }
+  }
   return g;
 }
 
@@ -86,7 +109,7 @@ void dwpw_fwd(Tensor x, Tensor dw, Tensor pw, int64_t K, int64_t dil, int64_t S,
   DwPwFwdArgs a{};
   a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.pw = pw.data_ptr<float>();
   a.d = d.data_ptr<float>(); a.z = z.data_ptr<float>(); a.stats = ptr_or_null<double>(stats);
-  if (a.stats) TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= 2 * C, "stats f64 [2C]");
+  if (a.stats) TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * C, "stats f64 [kRep][2C]");
   a.N = N; a.C = C; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.pad = pad;
   const int TR = 64 / Wo;
   const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
@@ -107,6 +130,8 @@ void pw_fwd(Tensor x, Tensor pw, Tensor z, OptT stats, int64_t co_off, int64_t S
   PwFwdArgs a{};
   a.x = x.data_ptr<float>(); a.pw = pw.data_ptr<float>(); a.z = z.data_ptr<float>();
   a.stats = ptr_or_null<double>(stats);
+  if (a.stats)
+    TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * z.size(1), "stats [kRep][2Ctot]");
   a.N = N; a.Cin = Cin; a.Cout = Cout; a.CoutTotal = z.size(1); a.co_off = co_off;
   a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off;
   launch_pw_fwd(a, cur_stream());
@@ -121,6 +146,8 @@ void pool_fwd(Tensor x, Tensor zavg, Tensor zmax, OptT sa, OptT sm, int64_t S, O
   }
   a.x = x.data_ptr<float>(); a.zavg = zavg.data_ptr<float>(); a.zmax = zmax.data_ptr<float>();
   a.stats_avg = ptr_or_null<double>(sa); a.stats_max = ptr_or_null<double>(sm);
+  if (a.stats_avg) TORCH_CHECK(sa->scalar_type() == at::kDouble && sa->numel() >= kRep * 2 * x.size(1), "stats");
+  if (a.stats_max) TORCH_CHECK(sm->scalar_type() == at::kDouble && sm->numel() >= kRep * 2 * x.size(1), "stats");
   a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = zavg.size(2); a.Wo = zavg.size(3);
   TORCH_CHECK(a.Ho == (a.H - 1) / S + 1 && zmax.sizes() == zavg.sizes(), "pool shapes");
   launch_pool_fwd(a, S, cur_stream());
@@ -160,7 +187,8 @@ void combine_bwd_reduce(Tensor dout, std::vector<Tensor> zs, std::vector<py::tup
   CombineBwdArgs a{};
   a.N = dout.size(0); a.C = dout.size(1); a.HW = dout.size(2) * dout.size(3);
   a.nops = zs.size();
-  TORCH_CHECK(a.nops <= kMaxOps && red.numel() >= (a.nops + 1) * a.C + 1, "red size");
+  a.rstride = (a.nops + 1) * a.C + 1;
+  TORCH_CHECK(a.nops <= kMaxOps && red.numel() >= (int64_t)kRep * a.rstride, "red size [kRep][(nops+1)C+1]");
   for (int k = 0; k < a.nops; ++k) {
     TORCH_CHECK(zs[k].sizes() == dout.sizes(), "z shape");
     a.z[k] = zs[k].data_ptr<float>();
@@ -169,19 +197,29 @@ void combine_bwd_reduce(Tensor dout, std::vector<Tensor> zs, std::vector<py::tup
   a.dout = dout.data_ptr<float>(); a.xid = ptr_or_null<float>(xid); a.red = red.data_ptr<double>();
   a.gw = ptr_or_null<double>(gw); a.id_idx = id_idx;
   if (a.gw) {
-    TORCH_CHECK(gw->scalar_type() == at::kDouble, "gw must be f64");
+    TORCH_CHECK(gw->scalar_type() == at::kDouble && gw->numel() % kRep == 0, "gw must be f64 [kRep][nw]");
+    a.gwstride = gw->numel() / kRep;
     TORCH_CHECK((int)widx.size() == a.nops, "widx per op");
     for (int k = 0; k < a.nops; ++k) {
-      TORCH_CHECK(widx[k] >= 0 && widx[k] < gw->numel(), "widx out of range");
+      TORCH_CHECK(widx[k] >= 0 && widx[k] < a.gwstride, "widx out of range");
       a.widx[k] = widx[k];
     }
-    TORCH_CHECK(id_idx < gw->numel(), "id_idx out of range");
+    TORCH_CHECK(id_idx < a.gwstride, "id_idx out of range");
   }
   launch_combine_bwd_reduce(a, cur_stream());
 }
 
+// gW replica r lives gstride floats after replica 0 (gstride == 0: one accumulator)
+void check_grad_sink(const OptT& gW, int64_t numel, int64_t gstride) {
+  if (!gW.has_value() || !gW->defined()) return;
+  TORCH_CHECK(gW->scalar_type() == at::kFloat && gW->is_contiguous() && gW->numel() == numel, "gW shape");
+  TORCH_CHECK(gstride == 0 || (gstride >= numel && (int64_t)(gW->storage().nbytes() / sizeof(float)) -
+                                                           gW->storage_offset() >= (kRep - 1) * gstride + numel),
+              "gW replicas exceed their buffer");
+}
+
 void pw_bwd(py::tuple gs, Tensor pw, OptT ain, Tensor x, OptT dd, OptT gx, OptT gW, int64_t co_off,
-            int64_t S, int64_t off, int64_t mode, bool need_dx) {
+            int64_t S, int64_t off, int64_t mode, bool need_dx, int64_t gstride) {
   check_f32(pw, "pw"); check_f32(x, "x");
   PwBwdArgs a{};
   const int Cout = pw.size(0), Cin = pw.size(1);
@@ -201,12 +239,13 @@ void pw_bwd(py::tuple gs, Tensor pw, OptT ain, Tensor x, OptT dd, OptT gx, OptT 
   } else {
     TORCH_CHECK(!need_dx || a.gx, "mode 1 needs gx");
   }
-  if (a.gW) TORCH_CHECK(gW->numel() == Cin * Cout, "gW size");
+  check_grad_sink(gW, (int64_t)Cin * Cout, gstride);
+  a.gstride = gstride;
   launch_pw_bwd(a, cur_stream());
 }
 
 void dw_bwd(Tensor x, c10::optional<py::tuple> inbn, Tensor dw, Tensor dd, Tensor gout, OptT gW, OptT red,
-            int64_t K, int64_t dil, int64_t S, int64_t pad) {
+            int64_t K, int64_t dil, int64_t S, int64_t pad, int64_t gstride) {
   check_f32(x, "x"); check_f32(dw, "dw"); check_f32(dd, "dd"); check_f32(gout, "gout");
   DwBwdArgs a{};
   a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = dd.size(2); a.Wo = dd.size(3);
@@ -215,6 +254,9 @@ void dw_bwd(Tensor x, c10::optional<py::tuple> inbn, Tensor dw, Tensor dd, Tenso
   TORCH_CHECK(gout.sizes() == x.sizes(), "gout shape");
   a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.dd = dd.data_ptr<float>();
   a.gout = gout.data_ptr<float>(); a.gW = ptr_or_null<float>(gW); a.red = ptr_or_null<double>(red);
+  check_grad_sink(gW, (int64_t)a.C * K * K, gstride);
+  a.gstride = gstride;
+  if (a.red) TORCH_CHECK(red->scalar_type() == at::kDouble && red->numel() >= kRep * 2 * a.C, "red [kRep][2C]");
   a.pad = pad;
   const int TR = 64 / a.Wo, r = (K - 1) / 2 * dil, h = (r + S - 1) / S, OR = TR + 2 * h;
   const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (a.Wo - 1) * S + (K - 1) * dil + 1;
@@ -243,6 +285,34 @@ void pool_bwd(c10::optional<py::tuple> ga, c10::optional<py::tuple> gm, Tensor x
   launch_pool_bwd(a, S, cur_stream());
 }
 
+void fold_rows(Tensor buf) {
+  check_f32(buf, "buf");
+  TORCH_CHECK(buf.dim() == 2, "buf must be [rows][n]");
+  FoldArgs a{};
+  a.buf = buf.data_ptr<float>();
+  a.rows = buf.size(0);
+  a.n = buf.size(1);
+  launch_fold_rows(a, cur_stream());
+}
+
+// segments: (f64 tensor holding kRep replicas, n, rstride)
+void fold_f64(std::vector<py::tuple> segs) {
+  TORCH_CHECK(!segs.empty() && (int)segs.size() <= kMaxSeg, "1..kMaxSeg segments");
+  FoldF64Args a{};
+  a.nseg = segs.size();
+  for (int k = 0; k < a.nseg; ++k) {
+    Tensor t = segs[k][0].cast<Tensor>();
+    int n = segs[k][1].cast<int>(), rs = segs[k][2].cast<int>();
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kDouble && t.is_contiguous(), "fold segment must be f64");
+    TORCH_CHECK(n >= 1 && rs >= n && t.numel() >= (int64_t)(kRep - 1) * rs + n, "fold segment size");
+    a.p[k] = t.data_ptr<double>();
+    a.n[k] = n;
+    a.rstride[k] = rs;
+    a.total += n;
+  }
+  launch_fold_f64(a, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -256,5 +326,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dw_bwd", &dw_bwd);
   m.def("pool_bwd", &pool_bwd);
   m.def("set_max_blocks", &set_max_blocks);
+  m.def("fold_rows", &fold_rows);
+  m.def("fold_f64", &fold_f64);
+  m.attr("REP") = kRep;
   m.def("max_blocks", &max_blocks);
 }

@@ -6,42 +6,52 @@ namespace katib_hip {
 
 constexpr int kMaxOps = 8;
 constexpr int kMaxC = 256;
+// Cross-workgroup sums (BN statistics, BN-backward reductions, weight gradients) go to kRep
+// replicas of the accumulator, workgroup b adding into replica b % kRep: global float atomics
+// execute memory-side and same-address adds serialise, so bounding the adders per address
+// (grid / kRep) keeps every flush short. Consumers sum the replicas (bn_moments / prologues);
+// weight-gradient replicas are folded once per backward pass (fold_rows).
+constexpr int kRep = 32;
 
 struct BNRef {              // where a BN layer's normalisation statistics come from
-  const double* sums;       // training: [2*C] = (sum, sum of squares) of the pre-BN tensor
+  const double* sums;       // training: replica r at sums + r*rstride: [2*C] = (sum, sum of squares)
   float* rmean;             // running stats (read in eval, updated by combine in training)
   float* rvar;
   float inv_count;          // 1 / (N*H*W)
   float eps;
   int eval;
   int C;
+  int rep;                  // replicas to sum (1 or kRep)
+  int rstride;              // doubles between replicas
 };
 
 struct GradSrc {            // d(loss)/d(z) evaluated on the fly: BN backward of a weighted op
   const float* g;           // upstream gradient (dout of the edge, or a stored stage gradient)
   const float* z;           // pre-BN tensor
-  const double* S1;         // [C] sum g
+  const double* S1;         // [C] sum g            (replica r at + r*rstride)
   const double* S2;         // [C] sum g * zhat
   BNRef bn;
   const float* w;           // softmax weights (nullptr -> 1)
   int widx;
   int eval;
+  int rep;
+  int rstride;
 };
 
 struct DwPwFwdArgs {
   const float* x; BNRef inbn; const float* dw; const float* pw;
-  float* d; float* z; double* stats;
+  float* d; float* z; double* stats;  // stats: kRep replicas of [2C]
   int N, C, H, W, Ho, Wo, pad, chunk, use_mfma;
 };
 
 struct PwFwdArgs {
-  const float* x; const float* pw; float* z; double* stats;
+  const float* x; const float* pw; float* z; double* stats;  // stats: kRep replicas of [2*CoutTotal]
   int N, Cin, Cout, CoutTotal, co_off, H, W, Ho, Wo, S, off;
 };
 
 struct PoolFwdArgs {
   const float* x; float* zavg; float* zmax; double* stats_avg; double* stats_max; unsigned char* amax;
-  int N, C, H, W, Ho, Wo;
+  int N, C, H, W, Ho, Wo;  // stats: kRep replicas of [2C] each
 };
 
 struct CombineFwdArgs {
@@ -53,18 +63,30 @@ struct CombineFwdArgs {
 
 struct CombineBwdArgs {
   const float* dout; const float* z[kMaxOps]; BNRef bn[kMaxOps]; int nops;
-  const float* xid; double* red; int N, C, HW;
-  double* gw; int widx[kMaxOps]; int id_idx;  // optional: d(loss)/d(softmax weight) per primitive
+  const float* xid; double* red; int N, C, HW;  // red: kRep replicas of [(nops+1)*C + 1]
+  double* gw; int widx[kMaxOps]; int id_idx;  // optional: d(loss)/d(softmax weight), kRep replicas of [nw]
+  int rstride, gwstride;
 };
 
 struct PwBwdArgs {
   GradSrc gs; const float* pw; const float* ain; const float* x; float* dd; float* gx; float* gW;
+  int gstride;  // floats between gW replicas (0: single accumulator)
   int N, Cin, Cout, CoutTotal, co_off, H, W, Ho, Wo, S, off, mode, need_dx;
 };
 
 struct DwBwdArgs {
   const float* x; BNRef inbn; const float* dw; const float* dd; float* gout; float* gW; double* red;
+  int gstride;  // floats between gW replicas (0: single accumulator); red: kRep replicas of [2C]
   int N, C, H, W, Ho, Wo, pad, chunk;
+};
+
+struct FoldArgs {  // buf[0][i] = sum_r buf[r][i]; rows 1.. zeroed
+  float* buf; int n; int rows;
+};
+
+constexpr int kMaxSeg = 16;
+struct FoldF64Args {  // per segment: p[i] = sum_{r < kRep} p[r*rstride + i]; replicas 1.. zeroed
+  double* p[kMaxSeg]; int n[kMaxSeg]; int rstride[kMaxSeg]; int nseg; int total;
 };
 
 struct PoolBwdArgs {
@@ -82,6 +104,8 @@ void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st);
 void launch_combine_bwd_reduce(const CombineBwdArgs& a, hipStream_t st);
 void launch_pw_bwd(const PwBwdArgs& a, hipStream_t st);
 int max_blocks();
+void launch_fold_rows(const FoldArgs& a, hipStream_t st);
+void launch_fold_f64(const FoldF64Args& a, hipStream_t st);
 void set_max_blocks(int n);
 
 }  // namespace katib_hip

@@ -46,18 +46,46 @@ int max_blocks() {
 }
 void set_max_blocks(int n) { g_max_blocks = n; }
 
+// batch mean / biased variance of channel c from the replicated (sum, sum of squares)
+__device__ __forceinline__ void bn_moments(const BNRef& b, int c, double& m, double& v) {
+  double s = 0.0, s2 = 0.0;
+  for (int r = 0; r < b.rep; ++r) {
+    s += b.sums[(size_t)r * b.rstride + c];
+    s2 += b.sums[(size_t)r * b.rstride + b.C + c];
+  }
+  m = s * (double)b.inv_count;
+  v = s2 * (double)b.inv_count - m * m;
+  if (v < 0) v = 0;
+}
+
 __device__ __forceinline__ void bn_coeffs(const BNRef& b, int c, float& mean, float& invstd) {
   if (b.eval) {
     mean = b.rmean[c];
     invstd = rsqrtf(b.rvar[c] + b.eps);
   } else {
-    double m = b.sums[c] * (double)b.inv_count;
-    double v = b.sums[b.C + c] * (double)b.inv_count - m * m;
-    if (v < 0) v = 0;
+    double m, v;
+    bn_moments(b, c, m, v);
     mean = (float)m;
     invstd = rsqrtf((float)v + b.eps);
   }
 }
+
+// per-channel means of the BN-backward reductions: m1 = mean(g), m2 = mean(g * zhat)
+__device__ __forceinline__ void gs_means(const GradSrc& gs, int c, float& m1, float& m2) {
+  if (gs.eval) {
+    m1 = m2 = 0.f;
+    return;
+  }
+  double s1 = 0.0, s2 = 0.0;
+  for (int r = 0; r < gs.rep; ++r) {
+    s1 += gs.S1[(size_t)r * gs.rstride + c];
+    s2 += gs.S2[(size_t)r * gs.rstride + c];
+  }
+  m1 = (float)(s1 * (double)gs.bn.inv_count);
+  m2 = (float)(s2 * (double)gs.bn.inv_count);
+}
+
+__device__ __forceinline__ int rep_slot() { return blockIdx.x % kRep; }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -190,7 +218,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdArgs a) {
     __syncthreads();  // sD / sIn reuse by the next tile
   }
   if (a.stats)  // one contiguous f64 atomic vector per block
-    for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.stats + i, (double)sStat[i]);
+    for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.stats + rep_slot() * 2 * C + i, (double)sStat[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -236,7 +264,8 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdArgs a) {
   if (a.stats)
     for (int i = tid; i < 2 * Cout; i += 256) {
       int hi = i >= Cout;
-      atomicAdd(a.stats + hi * a.CoutTotal + a.co_off + (i - hi * Cout), (double)sStat[i]);
+      atomicAdd(a.stats + rep_slot() * 2 * a.CoutTotal + hi * a.CoutTotal + a.co_off + (i - hi * Cout),
+                (double)sStat[i]);
     }
 }
 
@@ -297,7 +326,7 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdArgs a) {
   if (threadIdx.x < 4) {
     float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     double* dst = threadIdx.x < 2 ? a.stats_avg : a.stats_max;
-    if (dst) atomicAdd(dst + (threadIdx.x & 1) * C + c, (double)t);
+    if (dst) atomicAdd(dst + rep_slot() * 2 * C + (threadIdx.x & 1) * C + c, (double)t);
   }
 }
 
@@ -320,9 +349,8 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdArgs a) {
       int k = i / C, c = i % C;
       const BNRef& b = k < a.nops ? a.bn[k] : a.upd[k - a.nops];
       if (!b.rmean || b.eval) continue;
-      double m = b.sums[c] * (double)b.inv_count;
-      double v = b.sums[C + c] * (double)b.inv_count - m * m;
-      if (v < 0) v = 0;
+      double m, v;
+      bn_moments(b, c, m, v);
       double cnt = 1.0 / (double)b.inv_count;
       double vu = cnt > 1 ? v * cnt / (cnt - 1) : v;
       b.rmean[c] = (1.f - a.momentum) * b.rmean[c] + a.momentum * (float)m;
@@ -347,7 +375,7 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdArgs 
   const int C = a.C, HW = a.HW;
   const int c = blockIdx.x % C, g0 = blockIdx.x / C, G = gridDim.x / C;
   __shared__ float sMean[kMaxOps], sInv[kMaxOps];
-  __shared__ float red[4][kMaxOps + 2];
+  __shared__ float part[4][kMaxOps + 2];
   if (threadIdx.x < a.nops) bn_coeffs(a.bn[threadIdx.x], c, sMean[threadIdx.x], sInv[threadIdx.x]);
   __syncthreads();
   float s1 = 0.f, sid = 0.f;
@@ -371,37 +399,37 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdArgs 
 #pragma unroll
   for (int k = 0; k < kMaxOps; ++k) s2[k] = wave_sum(s2[k]);
   if (lane == 0) {
-    red[wave][0] = s1;
-    red[wave][1] = sid;
+    part[wave][0] = s1;
+    part[wave][1] = sid;
 #pragma unroll
-    for (int k = 0; k < kMaxOps; ++k) red[wave][2 + k] = s2[k];
+    for (int k = 0; k < kMaxOps; ++k) part[wave][2 + k] = s2[k];
   }
   __syncthreads();
+  double* red = a.red + (size_t)rep_slot() * a.rstride;
+  double* gw = a.gw ? a.gw + (size_t)rep_slot() * a.gwstride : nullptr;
   if (threadIdx.x < a.nops + 2) {
     int j = threadIdx.x;
-    float t = red[0][j] + red[1][j] + red[2][j] + red[3][j];
+    float t = part[0][j] + part[1][j] + part[2][j] + part[3][j];
     if (j == 0) {
-      atomicAdd(a.red + c, (double)t);
+      atomicAdd(red + c, (double)t);
     } else if (j == 1) {
       if (a.xid) {
-        atomicAdd(a.red + (size_t)(1 + a.nops) * C, (double)t);
-        if (a.gw && a.id_idx >= 0) atomicAdd(a.gw + a.id_idx, (double)t);
+        atomicAdd(red + (size_t)(1 + a.nops) * C, (double)t);
+        if (gw && a.id_idx >= 0) atomicAdd(gw + a.id_idx, (double)t);
       }
     } else {
-      atomicAdd(a.red + (size_t)(j - 1) * C + c, (double)t);
-      if (a.gw) atomicAdd(a.gw + a.widx[j - 2], (double)t);
+      atomicAdd(red + (size_t)(j - 1) * C + c, (double)t);
+      if (gw) atomicAdd(gw + a.widx[j - 2], (double)t);
     }
   }
 }
 
 // on-the-fly BN backward: dz = wk * invstd * (g - S1/cnt - zhat * S2/cnt)
-__device__ __forceinline__ float bn_bwd_val(const GradSrc& gs, size_t i, int c, float mean, float inv, float wk) {
+__device__ __forceinline__ float bn_bwd_val(const GradSrc& gs, size_t i, float mean, float inv, float wk, float m1,
+                                           float m2) {
   float zh = (gs.z[i] - mean) * inv;
   float g = gs.g[i];
-  if (gs.eval) return wk * inv * g;
-  float m1 = (float)(gs.S1[c] * (double)gs.bn.inv_count);
-  float m2 = (float)(gs.S2[c] * (double)gs.bn.inv_count);
-  return wk * inv * (g - m1 - zh * m2);
+  return wk * inv * (g - m1 - zh * m2);  // eval: m1 = m2 = 0
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -420,9 +448,14 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
   float* sA = sDz + Cout * PS;   // [Cin][PS]
   float* sMean = sA + Cin * PS;  // [Cout]
   float* sInv = sMean + Cout;
-  float* sW = sInv + Cout;       // [1]
+  float* sM1 = sInv + Cout;      // [Cout]
+  float* sM2 = sM1 + Cout;
+  float* sW = sM2 + Cout;        // [1]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (int c = tid; c < Cout; c += 256) bn_coeffs(a.gs.bn, a.co_off + c, sMean[c], sInv[c]);
+  for (int c = tid; c < Cout; c += 256) {
+    bn_coeffs(a.gs.bn, a.co_off + c, sMean[c], sInv[c]);
+    gs_means(a.gs, a.co_off + c, sM1[c], sM2[c]);
+  }
   if (tid == 0) sW[0] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
   __syncthreads();
   const float wk = sW[0];
@@ -443,7 +476,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
     for (int i = tid; i < Cout * P; i += 256) {
       int co = i / P, p = i % P;
       size_t gi = ((size_t)n * a.CoutTotal + a.co_off + co) * HWo + prem + p;
-      sDz[co * PS + p] = bn_bwd_val(a.gs, gi, a.co_off + co, sMean[co], sInv[co], wk);
+      sDz[co * PS + p] = bn_bwd_val(a.gs, gi, sMean[co], sInv[co], wk, sM1[co], sM2[co]);
     }
     for (int i = tid; i < Cin * P; i += 256) {
       int ci = i / P, p = i % P;
@@ -539,6 +572,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
     __syncthreads();
   }
   if (a.gW) {
+    float* gW = a.gW + (size_t)rep_slot() * a.gstride;
     if (MFMA) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -547,14 +581,14 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
           int cob = (b / nbi) * 16, cib = (b % nbi) * 16;
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            atomicAdd(a.gW + (cob + (lane >> 4) * 4 + r) * Cin + cib + (lane & 15), macc[j][r]);
+            atomicAdd(gW + (cob + (lane >> 4) * 4 + r) * Cin + cib + (lane & 15), macc[j][r]);
         }
       }
     } else {
 #pragma unroll
       for (int j = 0; j < MAXJ; ++j) {
         int pr = tid + 256 * j;
-        if (pr < npairs) atomicAdd(a.gW + pr, gacc[j]);
+        if (pr < npairs) atomicAdd(gW + pr, gacc[j]);
       }
     }
   }
@@ -695,9 +729,9 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
     }
   }
   if (PREBN && a.red)
-    for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.red + i, (double)sRed[i]);
+    for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.red + rep_slot() * 2 * C + i, (double)sRed[i]);
   if (a.gW)
-    for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + i, sGW[i]);
+    for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + (size_t)rep_slot() * a.gstride + i, sGW[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -712,9 +746,15 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdArgs a) {
   float* sGa = smem;                                          // [HWo] dz_avg / window count
   float* sGm = smem + HWo;                                    // [HWo] dz_max
   unsigned char* sArg = (unsigned char*)(smem + 2 * HWo);     // [HWo] argmax tap
-  float ma = 0, ia = 1, mm = 0, im = 1;
-  if (a.ga.z) bn_coeffs(a.ga.bn, c, ma, ia);
-  if (a.gm.z) bn_coeffs(a.gm.bn, c, mm, im);
+  float ma = 0, ia = 1, mm = 0, im = 1, a1 = 0, a2 = 0, m1 = 0, m2 = 0;
+  if (a.ga.z) {
+    bn_coeffs(a.ga.bn, c, ma, ia);
+    gs_means(a.ga, c, a1, a2);
+  }
+  if (a.gm.z) {
+    bn_coeffs(a.gm.bn, c, mm, im);
+    gs_means(a.gm, c, m1, m2);
+  }
   const float wa = a.ga.w ? a.ga.w[a.ga.widx] : 0.f;
   const float wm = a.gm.w ? a.gm.w[a.gm.widx] : 0.f;
   const float wid = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
@@ -723,12 +763,12 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdArgs a) {
     if (a.ga.z) {
       int y0 = max(oy * S - 1, 0), y1 = min(oy * S + 1, H - 1);
       int x0 = max(ox * S - 1, 0), x1 = min(ox * S + 1, W - 1);
-      sGa[o] = bn_bwd_val(a.ga, ob + o, c, ma, ia, wa) / (float)((y1 - y0 + 1) * (x1 - x0 + 1));
+      sGa[o] = bn_bwd_val(a.ga, ob + o, ma, ia, wa, a1, a2) / (float)((y1 - y0 + 1) * (x1 - x0 + 1));
     } else {
       sGa[o] = 0.f;
     }
     if (a.gm.z) {
-      sGm[o] = bn_bwd_val(a.gm, ob + o, c, mm, im, wm);
+      sGm[o] = bn_bwd_val(a.gm, ob + o, mm, im, wm, m1, m2);
       sArg[o] = a.amax[ob + o];
     } else {
       sGm[o] = 0.f;
@@ -829,11 +869,53 @@ void launch_combine_bwd_reduce(const CombineBwdArgs& a, hipStream_t st) {
 void launch_pw_bwd(const PwBwdArgs& a, hipStream_t st) {
   int ntiles = a.N * a.Ho * a.Wo / 64;
   int blocks = std::min(ntiles, max_blocks());
-  size_t lds = sizeof(float) * (a.Cout * 65 + a.Cin * 65 + 2 * a.Cout + 4);
+  size_t lds = sizeof(float) * (a.Cout * 65 + a.Cin * 65 + 4 * a.Cout + 4);
   const bool mfma = a.Cin % 16 == 0 && a.Cout % 16 == 0 && (a.Cin / 16) * (a.Cout / 16) <= 16;
   if (mfma) hipLaunchKernelGGL(pw_bwd_kernel<true>, dim3(blocks), dim3(256), lds, st, a);
   else hipLaunchKernelGGL(pw_bwd_kernel<false>, dim3(blocks), dim3(256), lds, st, a);
 }
 
+
+__global__ void __launch_bounds__(256) fold_rows_kernel(FoldArgs a) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += gridDim.x * 256) {
+    float acc = a.buf[i];
+    for (int r = 1; r < a.rows; ++r) {
+      float* q = a.buf + (size_t)r * a.n + i;
+      acc += *q;
+      *q = 0.f;
+    }
+    a.buf[i] = acc;
+  }
+}
+
+// Replica fold for the f64 reductions (BN statistics, BN-backward sums, d alpha): run between a
+// producer and its consumers so that every consumer reads ONE value per channel (rep = 1).
+__global__ void __launch_bounds__(256) fold_f64_kernel(FoldF64Args a) {
+  for (int g = blockIdx.x * 256 + threadIdx.x; g < a.total; g += gridDim.x * 256) {
+    int seg = 0, i = g;
+    while (seg < a.nseg - 1 && i >= a.n[seg]) i -= a.n[seg++];
+    double* p = a.p[seg] + i;
+    const int rs = a.rstride[seg];
+    double v[kRep];
+#pragma unroll
+    for (int r = 0; r < kRep; ++r) v[r] = p[(size_t)r * rs];  // all loads in flight together
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < kRep; ++r) acc += v[r];
+    p[0] = acc;
+#pragma unroll
+    for (int r = 1; r < kRep; ++r) p[(size_t)r * rs] = 0.0;
+  }
+}
+
+void launch_fold_f64(const FoldF64Args& a, hipStream_t st) {
+  int blocks = std::max(1, std::min((a.total + 255) / 256, 1024));
+  hipLaunchKernelGGL(fold_f64_kernel, dim3(blocks), dim3(256), 0, st, a);
+}
+
+void launch_fold_rows(const FoldArgs& a, hipStream_t st) {
+  int blocks = std::max(1, std::min((a.n + 255) / 256, 2048));
+  hipLaunchKernelGGL(fold_rows_kernel, dim3(blocks), dim3(256), 0, st, a);
+}
 
 }  // namespace katib_hip

@@ -75,8 +75,20 @@ class DartsSearch:
         self.comm.broadcast_(self.A)
         self.Wv = torch.zeros_like(self.W)
         self.Av = torch.zeros_like(self.A)
-        self.gW = torch.zeros_like(self.W)  # model weight grads (BWD1 / BWD5)
-        self.gWv = torch.zeros_like(self.W)  # virtual weight grads (BWD2)
+        # weight-gradient buckets: [R][nW], row 0 is the gradient; with the HIP edge kernels
+        # R = hip_darts.REP replica rows absorb the cross-workgroup atomics and are folded
+        # into row 0 after every backward pass (_fold)
+        self.hd = None
+        if self.device.type == "cuda" and self.net.ops.backend() == "hip":
+            self.hd = self.net.ops.hip_module()
+        R = self.hd.REP if self.hd is not None else 1
+        self.gW_rep = torch.zeros(R, nW, device=dev)
+        self.gWv_rep = torch.zeros(R, nW, device=dev)
+        if self.hd is not None:
+            self.hd.register_grad_replicas(self.gW_rep)
+            self.hd.register_grad_replicas(self.gWv_rep)
+        self.gW = self.gW_rep[0]  # model weight grads (BWD1 / BWD5)
+        self.gWv = self.gWv_rep[0]  # virtual weight grads (BWD2)
         self.gAv = torch.zeros_like(self.A)  # virtual alpha grads (BWD2)
         self.gA = torch.zeros_like(self.A)  # alpha grads (BWD3/4/5 scratch)
         self.gAp = torch.zeros_like(self.A)
@@ -115,11 +127,16 @@ class DartsSearch:
         logits = self.net.forward(x, P, an, ar, bn, training=True)
         return F.cross_entropy(logits, y), logits
 
+    def _fold(self, rep):
+        if self.hd is not None:
+            self.hd.fold(rep)
+
     def _seg_virtual(self, tx, ty):
         """FWD1/BWD1 -> gW (not yet reduced)."""
         self.gW.zero_()
         loss, _ = self._loss(tx, ty, self.Pw.views, self.An, self.Ar, self.bn)
         loss.backward(inputs=self.Pw.list)
+        self._fold(self.gW_rep)
 
     def _seg_unrolled(self, vx, vy):
         """virtual step + FWD2/BWD2 -> gAv, gWv."""
@@ -133,6 +150,7 @@ class DartsSearch:
         self.gAv.zero_()
         loss, _ = self._loss(vx, vy, self.Pv.views, self.Avn, self.Avr, self.bn_v)
         loss.backward(inputs=self.Pv.list + self.Avn + self.Avr)
+        self._fold(self.gWv_rep)
 
     def _seg_hessian(self, tx, ty):
         """+/- eps perturbations, FWD3/BWD3 and FWD4/BWD4 w.r.t. alphas only."""
@@ -174,6 +192,7 @@ class DartsSearch:
         self.gA.zero_()
         loss, logits = self._loss(tx, ty, self.Pw.views, self.An, self.Ar, self.bn)
         loss.backward(inputs=self.Pw.list)
+        self._fold(self.gW_rep)
         with torch.no_grad():
             self.loss_out.copy_(loss.detach())
             if self.logits_out is None or self.logits_out.shape != logits.shape:

@@ -11,12 +11,17 @@ forward   dwpw_fwd x (sep stage 1, sep stage 2, dil3, dil5), pool_fwd (avg+max),
 backward  combine_bwd_reduce (BN-backward reductions + d softmax-weights),
           pw_bwd/dw_bwd per conv stage, pool_bwd (+ identity skip)
 
-Weight gradients are accumulated by the kernels directly into each weight leaf's
-``.grad`` when it exists (the flat gradient bucket of
-:class:`katib_amd.models.darts_search.DartsSearch`), so no AccumulateGrad
-launches follow; detached weights (the Hessian passes) skip weight-gradient work.
-Callers that drive autograd with ``backward(inputs=...)`` must list every weight
-leaf that requires grad (DartsSearch does).
+Cross-workgroup sums go to ``REP`` replicas of each accumulator (workgroup b adds
+into replica b % REP) so that no address sees more than grid/REP atomic adds; a
+``fold_f64`` launch sums the replicas of BN statistics / BN-backward reductions
+into replica 0 before their consumers run (which then read one value). Weight gradients are accumulated by the kernels
+directly into each weight leaf's ``.grad`` when that is a row-0 view of a buffer
+registered with :func:`register_grad_replicas` (the flat gradient bucket of
+:class:`katib_amd.models.darts_search.DartsSearch`, folded once per backward pass
+with :func:`fold`), so no AccumulateGrad launches follow; detached weights (the
+Hessian passes) skip weight-gradient work. Callers that drive autograd with
+``backward(inputs=...)`` must list every weight leaf that requires grad
+(DartsSearch does).
 
 Importing this module raises if the extension is missing: the HIP path never
 silently degrades to PyTorch ops.
@@ -25,6 +30,7 @@ silently degrades to PyTorch ops.
 from __future__ import annotations
 
 import importlib
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -35,6 +41,34 @@ except ImportError as e:  # pragma: no cover - machines without the build
     raise ImportError("katib_amd._hipkern is not built (run __graft_entry__.build()): %s" % e)
 
 F64 = torch.float64
+REP = int(_K.REP)
+_REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
+
+
+def register_grad_replicas(buf: torch.Tensor):
+    """Declare ``buf`` ([REP][n] fp32, contiguous) a replicated gradient accumulator:
+    ``.grad`` views into its row 0 receive kernel atomics into all REP rows."""
+    if buf.dim() != 2 or buf.shape[0] != REP or not buf.is_contiguous() or buf.dtype != torch.float32:
+        raise ValueError("replicated gradient buffer must be contiguous fp32 [%d][n]" % REP)
+    _REPLICATED.append((weakref.ref(buf), buf.shape[1]))
+
+
+def fold(buf: torch.Tensor):
+    """row 0 <- sum of all replica rows; rows 1.. <- 0 (one kernel)."""
+    _K.fold_rows(buf)
+
+
+def _replica_stride(g: torch.Tensor) -> int:
+    ptr = g.data_ptr()
+    for ref, n in list(_REPLICATED):
+        buf = ref()
+        if buf is None:
+            _REPLICATED.remove((ref, n))
+            continue
+        base = buf.data_ptr()
+        if base <= ptr and ptr + g.numel() * 4 <= base + n * 4:
+            return n
+    return 0
 
 
 class EdgeSpec:
@@ -53,22 +87,47 @@ class EdgeSpec:
         self.pidx = {n: i for i, n in enumerate(pnames)}
 
 
-def _bn(stats: Optional[torch.Tensor], rm, rv, count: int, training: bool, eps: float):
+def _bn(stats: Optional[torch.Tensor], rm, rv, count: int, training: bool, eps: float, C: int):
+    """BN reference tuple for the kernels; ``stats`` ([REP][2C]) is folded before use."""
     if training:
-        return (stats, rm, rv, 1.0 / count, False, eps)
-    return (None, rm, rv, 1.0 / count, True, eps)
+        return (stats, rm, rv, 1.0 / count, False, eps, 1, 2 * C)
+    return (None, rm, rv, 1.0 / count, True, eps, 1, 2 * C)
 
 
-def _sink(p: torch.Tensor, extra: Dict[int, torch.Tensor], key: int):
-    """Where a weight gradient goes: the leaf's existing .grad (bucket view), a fresh
-    buffer returned through autograd, or nowhere (weight does not require grad)."""
-    if not p.requires_grad:
-        return None
-    if p.grad is not None and p.is_leaf:
-        return p.grad
-    g = torch.zeros_like(p)
-    extra[key] = g
-    return g
+def _fold_slots(stats, slot: int, idx, n: int):
+    segs = [(stats[i * slot:(i + 1) * slot], n, n) for i in idx]
+    if segs:
+        _K.fold_f64(segs)
+
+
+class _Sinks:
+    """Weight-gradient destinations of one backward call."""
+
+    def __init__(self):
+        self.temps = []
+
+    def get(self, p: torch.Tensor, key: int):
+        """(pointer tensor, replica stride): the leaf's registered replicated .grad, else
+        a temporary [REP][numel] buffer summed in :meth:`finish`; (None, 0) when the
+        weight does not require grad."""
+        if not p.requires_grad:
+            return None, 0
+        g = p.grad if p.is_leaf else None
+        if g is not None and g.is_contiguous():
+            stride = _replica_stride(g)
+            if stride:
+                return g, stride
+        t = torch.zeros(REP, p.numel(), device=p.device, dtype=torch.float32)
+        self.temps.append((key, t, g, p))
+        return t[0].view_as(p), p.numel()
+
+    def finish(self, grads: List):
+        for key, t, g, p in self.temps:
+            s = t.sum(0).view_as(p)
+            if g is not None:
+                g.add_(s)
+            else:
+                grads[key] = s
 
 
 class _MixedEdge(torch.autograd.Function):
@@ -81,38 +140,36 @@ class _MixedEdge(torch.autograd.Function):
         cnt = N * Ho * Wo
         P = dict(zip(spec.pnames, params))
         dev = x.device
-        stats = torch.zeros(max(spec.nbn, 1) * 2 * C, dtype=F64, device=dev) if training else None
+        slot = REP * 2 * C
+        stats = torch.zeros(max(spec.nbn, 1) * slot, dtype=F64, device=dev) if training else None
 
         def st(i):
-            return stats[i * 2 * C:(i + 1) * 2 * C] if training else None
+            return stats[i * slot:(i + 1) * slot] if training else None
 
-        refs = [_bn(st(i), bn[i][0], bn[i][1], cnt, training, eps) for i in range(spec.nbn)]
-        zs, bns, widx, upd, saved = [], [], [], [], {}
+        refs = [_bn(st(i), bn[i][0], bn[i][1], cnt, training, eps, C) for i in range(spec.nbn)]
+        zs, bns, widx, upd, saved = {}, {}, [], [], {}
         id_idx, xid = -1, None
+        stage1, stage2 = [], []  # BN slots produced before / by the separable convs' second stage
         for k, prim in enumerate(spec.prims):
             if prim == "none":
                 continue
             sl = spec.slots.get(prim, ())
             if prim.startswith("separable_convolution"):
                 K = int(prim[-1])
-                pad = K // 2
                 d1 = torch.empty(N, C, Ho, Wo, device=dev)
-                z1, d2, z2 = torch.empty_like(d1), torch.empty_like(d1), torch.empty_like(d1)
-                _K.dwpw_fwd(x, P[prim + ".0.dw"], P[prim + ".0.pw"], K, 1, S, pad, None, d1, z1, st(sl[0]), True)
-                _K.dwpw_fwd(z1, P[prim + ".1.dw"], P[prim + ".1.pw"], K, 1, 1, pad, refs[sl[0]], d2, z2,
-                            st(sl[1]), True)
-                upd.append(refs[sl[0]])
-                zs.append(z2)
-                bns.append(refs[sl[1]])
-                saved[prim] = (d1, z1, d2, z2)
+                z1 = torch.empty_like(d1)
+                _K.dwpw_fwd(x, P[prim + ".0.dw"], P[prim + ".0.pw"], K, 1, S, K // 2, None, d1, z1, st(sl[0]), True)
+                saved[prim] = [d1, z1]
+                stage1.append(sl[0])
+                stage2.append(sl[1])
             elif prim.startswith("dilated_convolution"):
                 K = int(prim[-1])
                 d = torch.empty(N, C, Ho, Wo, device=dev)
                 z = torch.empty_like(d)
                 _K.dwpw_fwd(x, P[prim + ".dw"], P[prim + ".pw"], K, 2, S, (K // 2) * 2, None, d, z, st(sl[0]), True)
-                zs.append(z)
-                bns.append(refs[sl[0]])
+                zs[k], bns[k] = z, refs[sl[0]]
                 saved[prim] = (d, z)
+                stage1.append(sl[0])
             elif prim in ("avg_pooling_3x3", "max_pooling_3x3"):
                 if "pool" not in saved:
                     za = torch.empty(N, C, Ho, Wo, device=dev)
@@ -122,8 +179,9 @@ class _MixedEdge(torch.autograd.Function):
                     sm = spec.slots.get("max_pooling_3x3")
                     _K.pool_fwd(x, za, zm, st(sa[0]) if sa else None, st(sm[0]) if sm else None, S, am)
                     saved["pool"] = (za, zm, am)
-                zs.append(saved["pool"][0 if prim == "avg_pooling_3x3" else 1])
-                bns.append(refs[sl[0]])
+                zs[k] = saved["pool"][0 if prim == "avg_pooling_3x3" else 1]
+                bns[k] = refs[sl[0]]
+                stage1.append(sl[0])
             elif prim == "skip_connection":
                 if S == 1:
                     id_idx, xid = k, x
@@ -131,12 +189,29 @@ class _MixedEdge(torch.autograd.Function):
                 z = torch.empty(N, C, Ho, Wo, device=dev)
                 _K.pw_fwd(x, P[prim + ".conv1"], z, st(sl[0]), 0, 2, 0)
                 _K.pw_fwd(x, P[prim + ".conv2"], z, st(sl[0]), C // 2, 2, 1)
-                zs.append(z)
-                bns.append(refs[sl[0]])
+                zs[k], bns[k] = z, refs[sl[0]]
                 saved[prim] = (z,)
+                stage1.append(sl[0])
             else:
                 raise ValueError(prim)
             widx.append(k)
+        if training:
+            _fold_slots(stats, slot, stage1, 2 * C)
+        for k, prim in enumerate(spec.prims):
+            if prim.startswith("separable_convolution"):
+                K = int(prim[-1])
+                sl = spec.slots[prim]
+                d1, z1 = saved[prim]
+                d2, z2 = torch.empty_like(d1), torch.empty_like(d1)
+                _K.dwpw_fwd(z1, P[prim + ".1.dw"], P[prim + ".1.pw"], K, 1, 1, K // 2, refs[sl[0]], d2, z2,
+                            st(sl[1]), True)
+                upd.append(refs[sl[0]])
+                zs[k], bns[k] = z2, refs[sl[1]]
+                saved[prim] = (d1, z1, d2, z2)
+        if training:
+            _fold_slots(stats, slot, stage2, 2 * C)
+        zs = [zs[k] for k in widx]
+        bns = [bns[k] for k in widx]
         out = torch.empty(N, C, Ho, Wo, device=dev)
         _K.combine_fwd(zs, bns, widx, w, id_idx, xid, None, None, out, momentum, training, False,
                        upd if training else [])
@@ -157,24 +232,44 @@ class _MixedEdge(torch.autograd.Function):
         dout = dout.contiguous()
         nops = len(zs)
         nred = (nops + 1) * C + 1
-        buf = torch.zeros(nred + w.numel(), dtype=F64, device=dev)
-        red, gw = buf[:nred], buf[nred:]
-        _K.combine_bwd_reduce(dout, zs, bns, x if id_idx >= 0 else None, red, widx, id_idx, gw)
+        nw = w.numel()
+        buf = torch.zeros(REP * (nred + nw), dtype=F64, device=dev)
+        red, gw_rep = buf[:REP * nred], buf[REP * nred:]
+        _K.combine_bwd_reduce(dout, zs, bns, x if id_idx >= 0 else None, red, widx, id_idx, gw_rep)
+        _K.fold_f64([(red, nred, nred), (gw_rep, nw, nw)])
         S1 = red[:C]
         jpos = {k: j for j, k in enumerate(widx)}
 
         def src(k, z):  # GradSrc of a weighted, BN'd op output
             j = jpos[k]
-            return (dout, z, S1, red[(1 + j) * C:(2 + j) * C], bns[j], w, k)
+            return (dout, z, S1, red[(1 + j) * C:(2 + j) * C], bns[j], w, k, 1, nred)
 
         need_x = ctx.needs_input_grad[0]
         gx = torch.zeros_like(x) if need_x else None
         scratch = None
-        extra: Dict[int, torch.Tensor] = {}
+        sinks = _Sinks()
 
         def sink(name):
-            return _sink(P[name], extra, spec.pidx[name])
+            return sinks.get(P[name], spec.pidx[name])
 
+        # separable convs: both second stages first, one fold of their BN-backward sums, then stage 1
+        seps = [(k, p) for k, p in enumerate(spec.prims) if p.startswith("separable_convolution")]
+        red1 = torch.zeros(max(len(seps), 1) * REP * 2 * C, dtype=F64, device=dev) if training else None
+        stage_grad = {}
+        for i, (k, prim) in enumerate(seps):
+            K = int(prim[-1])
+            d1, z1, d2, z2 = saved[prim]
+            b1 = refs[spec.slots[prim][0]]
+            dd2 = torch.empty_like(d2)
+            gp, gst = sink(prim + ".1.pw")
+            _K.pw_bwd(src(k, z2), P[prim + ".1.pw"], d2, z1, dd2, None, gp, 0, 1, 0, 0, True, gst)
+            g1 = torch.empty_like(z1)
+            r1 = red1[i * REP * 2 * C:(i + 1) * REP * 2 * C] if training else None
+            gp, gst = sink(prim + ".1.dw")
+            _K.dw_bwd(z1, b1, P[prim + ".1.dw"], dd2, g1, gp, r1, K, 1, 1, K // 2, gst)
+            stage_grad[prim] = (g1, r1, b1)
+        if training and seps:
+            _K.fold_f64([(red1[i * REP * 2 * C:(i + 1) * REP * 2 * C], 2 * C, 2 * C) for i in range(len(seps))])
         pool_done = False
         for k, prim in enumerate(spec.prims):
             if prim == "none":
@@ -183,28 +278,26 @@ class _MixedEdge(torch.autograd.Function):
                 K = int(prim[-1])
                 pad = K // 2
                 d1, z1, d2, z2 = saved[prim]
-                b1 = refs[spec.slots[prim][0]]
-                dd2 = torch.empty_like(d2)
-                _K.pw_bwd(src(k, z2), P[prim + ".1.pw"], d2, z1, dd2, None, sink(prim + ".1.pw"), 0, 1, 0, 0, True)
-                g1 = torch.empty_like(z1)
-                red1 = torch.zeros(2 * C, dtype=F64, device=dev) if training else None
-                _K.dw_bwd(z1, b1, P[prim + ".1.dw"], dd2, g1, sink(prim + ".1.dw"), red1, K, 1, 1, pad)
-                gs1 = (g1, z1, red1[:C] if training else None, red1[C:] if training else None, b1, None, 0)
+                g1, r1, b1 = stage_grad[prim]
+                gs1 = (g1, z1, r1[:C] if training else None, r1[C:2 * C] if training else None, b1, None, 0, 1, 2 * C)
                 dd1 = torch.empty_like(d1)
-                _K.pw_bwd(gs1, P[prim + ".0.pw"], d1, x, dd1, None, sink(prim + ".0.pw"), 0, 1, 0, 0, True)
+                gp, gst = sink(prim + ".0.pw")
+                _K.pw_bwd(gs1, P[prim + ".0.pw"], d1, x, dd1, None, gp, 0, 1, 0, 0, True, gst)
                 if not need_x and scratch is None:
                     scratch = torch.empty_like(x)
-                _K.dw_bwd(x, None, P[prim + ".0.dw"], dd1, gx if need_x else scratch, sink(prim + ".0.dw"), None,
-                          K, 1, S, pad)
+                gp, gst = sink(prim + ".0.dw")
+                _K.dw_bwd(x, None, P[prim + ".0.dw"], dd1, gx if need_x else scratch, gp, None, K, 1, S, pad, gst)
             elif prim.startswith("dilated_convolution"):
                 K = int(prim[-1])
                 d, z = saved[prim]
                 dd = torch.empty_like(d)
-                _K.pw_bwd(src(k, z), P[prim + ".pw"], d, x, dd, None, sink(prim + ".pw"), 0, 1, 0, 0, True)
+                gp, gst = sink(prim + ".pw")
+                _K.pw_bwd(src(k, z), P[prim + ".pw"], d, x, dd, None, gp, 0, 1, 0, 0, True, gst)
                 if not need_x and scratch is None:
                     scratch = torch.empty_like(x)
-                _K.dw_bwd(x, None, P[prim + ".dw"], dd, gx if need_x else scratch, sink(prim + ".dw"), None,
-                          K, 2, S, (K // 2) * 2)
+                gp, gst = sink(prim + ".dw")
+                _K.dw_bwd(x, None, P[prim + ".dw"], dd, gx if need_x else scratch, gp, None, K, 2, S, (K // 2) * 2,
+                          gst)
             elif prim in ("avg_pooling_3x3", "max_pooling_3x3"):
                 if pool_done or not need_x:
                     continue
@@ -220,14 +313,15 @@ class _MixedEdge(torch.autograd.Function):
             elif prim == "skip_connection" and S != 1:
                 (z,) = saved[prim]
                 gs = src(k, z)
-                _K.pw_bwd(gs, P[prim + ".conv1"], None, x, None, gx, sink(prim + ".conv1"), 0, 2, 0, 1, need_x)
-                _K.pw_bwd(gs, P[prim + ".conv2"], None, x, None, gx, sink(prim + ".conv2"), C // 2, 2, 1, 1, need_x)
+                gp, gst = sink(prim + ".conv1")
+                _K.pw_bwd(gs, P[prim + ".conv1"], None, x, None, gx, gp, 0, 2, 0, 1, need_x, gst)
+                gp, gst = sink(prim + ".conv2")
+                _K.pw_bwd(gs, P[prim + ".conv2"], None, x, None, gx, gp, C // 2, 2, 1, 1, need_x, gst)
         if need_x and id_idx >= 0 and not pool_done:
             gx.add_(dout * w[id_idx])
         grads = [None] * len(params)
-        for i, g in extra.items():
-            grads[i] = g
-        gw_out = gw.to(w.dtype) if ctx.needs_input_grad[1] else None
+        sinks.finish(grads)
+        gw_out = gw_rep[:nw].to(w.dtype) if ctx.needs_input_grad[1] else None
         return (gx, gw_out, None, None, None, None, None, *grads)
 
 
@@ -250,14 +344,16 @@ class _StdConvBN(torch.autograd.Function):
         Cout = w1.shape[0] * (2 if fr else 1)
         Ho, Wo = (H // 2, W // 2) if fr else (H, W)
         cnt = N * Ho * Wo
-        stats = torch.zeros(2 * Cout, dtype=F64, device=x.device) if training else None
+        stats = torch.zeros(REP * 2 * Cout, dtype=F64, device=x.device) if training else None
         z = torch.empty(N, Cout, Ho, Wo, device=x.device)
         if fr:
             _K.pw_fwd(x, w1, z, stats, 0, 2, 0)
             _K.pw_fwd(x, w2, z, stats, Cout // 2, 2, 1)
         else:
             _K.pw_fwd(x, w1, z, stats, 0, 1, 0)
-        bn = _bn(stats, rm, rv, cnt, training, eps)
+        if training:
+            _K.fold_f64([(stats, 2 * Cout, 2 * Cout)])
+        bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
         out = torch.empty_like(z)
         _K.combine_fwd([z], [bn], [0], None, -1, None, None, None, out, momentum, training, False, [])
         ctx.meta = (bn, fr, Cout, training)
@@ -270,21 +366,25 @@ class _StdConvBN(torch.autograd.Function):
         w2 = rest[0] if rest else None
         bn, fr, Cout, training = ctx.meta
         dout = dout.contiguous()
-        red = torch.zeros(2 * Cout + 1, dtype=F64, device=x.device)
+        nred = 2 * Cout + 1
+        red = torch.zeros(REP * nred, dtype=F64, device=x.device)
         if training:
             _K.combine_bwd_reduce(dout, [z], [bn], None, red, [0], -1, None)
-        gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0)
+            _K.fold_f64([(red, nred, nred)])
+        gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0, 1, nred)
         need_x = ctx.needs_input_grad[0]
         gx = torch.zeros_like(x) if need_x else None
-        extra: Dict[int, torch.Tensor] = {}
-        s1 = _sink(w1, extra, 1)
+        sinks = _Sinks()
+        grads = [None, None, None]
+        g1, s1 = sinks.get(w1, 1)
         if fr:
-            s2 = _sink(w2, extra, 2)
-            _K.pw_bwd(gs, w1, None, x, None, gx, s1, 0, 2, 0, 1, need_x)
-            _K.pw_bwd(gs, w2, None, x, None, gx, s2, Cout // 2, 2, 1, 1, need_x)
+            g2, s2 = sinks.get(w2, 2)
+            _K.pw_bwd(gs, w1, None, x, None, gx, g1, 0, 2, 0, 1, need_x, s1)
+            _K.pw_bwd(gs, w2, None, x, None, gx, g2, Cout // 2, 2, 1, 1, need_x, s2)
         else:
-            _K.pw_bwd(gs, w1, None, x, None, gx, s1, 0, 1, 0, 1, need_x)
-        return gx, None, None, None, None, None, extra.get(1), extra.get(2)
+            _K.pw_bwd(gs, w1, None, x, None, gx, g1, 0, 1, 0, 1, need_x, s1)
+        sinks.finish(grads)
+        return gx, None, None, None, None, None, grads[1], grads[2]
 
 
 def relu_conv_bn(x, w, rm, rv, training, momentum=0.1, eps=1e-5):
