@@ -9,6 +9,15 @@ Master bracket: ``n`` uniform samples with the resource parameter set to ``r``.
 Child bracket: top ``ceil(n_i/eta)`` of the last ``evaluating_trials`` trials
 (sorted by start time) with the resource set to ``r*eta^i``.
 ``n`` is overwritten by ``current_request_number`` (the reference's "hack").
+
+Documented divergence: the reference raises while the previous rung's trials are
+still running (``_get_top_trial``) and its controller rejects a reply with fewer
+assignments than requested (``suggestionclient.go:124-128``), so a child bracket
+smaller than ``parallelTrialCount`` livelocks there. Here a pending rung returns an
+empty reply (the scheduler waits; :meth:`finished_on_empty` tells it the outer loop
+is not done) and the scheduler accepts short batches from this service
+(``partial_batches``), lowering the Suggestion's request count to what was served.
+Completed-but-unsuccessful trials of a rung rank last instead of blocking it.
 """
 
 from __future__ import annotations
@@ -79,12 +88,21 @@ class HyperBandParam:
         return p
 
 
+class _RungPending(Exception):
+    pass
+
+
 class HyperbandService(SuggestionService):
     algorithm_names = ("hyperband",)
+    partial_batches = True
 
     def __init__(self, seed=None):
         self.rng = np.random.RandomState(seed)
         self.all_trials = []
+        self.finished = False
+
+    def finished_on_empty(self) -> bool:
+        return self.finished
 
     def GetSuggestions(self, request, context=None):
         reply = api.GetSuggestionsReply()
@@ -92,9 +110,14 @@ class HyperbandService(SuggestionService):
         self.all_trials = list(request.trials)
         param = HyperBandParam.convert(experiment.spec.algorithm.algorithm_settings)
         if param.current_s < 0:
+            self.finished = True
             return reply  # outer loop finished
         param.n = request.current_request_number
-        for spec in self._make_bracket(experiment, param):
+        try:
+            specs = self._make_bracket(experiment, param)
+        except _RungPending:
+            return api.GetSuggestionsReply()  # state unchanged; asked again once the rung completes
+        for spec in specs:
             reply.parameter_assignments.add(assignments=spec)
         reply.algorithm.CopyFrom(HyperBandParam.generate(param))
         return reply
@@ -133,20 +156,26 @@ class HyperbandService(SuggestionService):
     def _top_trials(self, latest_n, top_n, experiment):
         obj = experiment.spec.objective.objective_metric_name
 
+        rev = experiment.spec.objective.type == api.MAXIMIZE
+        worst = float("-inf") if rev else float("inf")
+
         def value(t):
+            if t.status.condition != api.TrialStatus.SUCCEEDED:
+                return worst
             for m in t.status.observation.metrics:
                 if m.name == obj:
-                    return float(m.value)
-            return float("nan")
+                    try:
+                        return float(m.value)
+                    except ValueError:
+                        return worst
+            return worst
 
         latest = sorted(self.all_trials, key=lambda t: t.status.start_time)
         if len(latest) > latest_n:
             latest = latest[-latest_n:]
-        for t in latest:
-            if t.status.condition != api.TrialStatus.SUCCEEDED:
-                raise RuntimeError(
-                    "There are some trials which are not completed yet for experiment %s." % experiment.name)
-        rev = experiment.spec.objective.type == api.MAXIMIZE
+        if len(latest) < latest_n or any(t.status.condition in (api.TrialStatus.CREATED, api.TrialStatus.RUNNING)
+                                         for t in latest):
+            raise _RungPending()
         return sorted(latest, key=value, reverse=rev)[:top_n]
 
     def _master(self, experiment, p):

@@ -268,6 +268,10 @@ class SuggestionService:
     def is_exhausted(self) -> bool:
         return False
 
+    # an empty GetSuggestions reply means "search finished" unless a service overrides this
+    def finished_on_empty(self) -> bool:
+        return True
+
 
 def abort(context, code: str, message: str):
     """Report an error the gRPC way when a context exists, else raise."""

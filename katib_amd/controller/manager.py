@@ -674,10 +674,14 @@ class Manager:
             return False
         got = list(reply.parameter_assignments)
         if not got:
-            return True  # algorithm finished (e.g. HyperBand outer loop done, ENAS all-failed)
+            # algorithm finished (grid exhausted, HyperBand outer loop done) - or, for services
+            # that serve partial batches, simply nothing to hand out yet
+            return svc.finished_on_empty()
         if len(got) != need:
-            self._event(sug, "Warning", C.RECONCILE_ERROR_REASON, "The response contains unexpected trials")
-            return False
+            if not (getattr(svc, "partial_batches", False) and len(got) < need):
+                self._event(sug, "Warning", C.RECONCILE_ERROR_REASON, "The response contains unexpected trials")
+                return False
+            sug.spec.requests = (sug.status.suggestion_count or 0) + len(got)
         rules = []
         es = self.es_services.get(key)
         if es is not None:

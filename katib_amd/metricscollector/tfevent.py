@@ -209,5 +209,9 @@ class EventWriter:
         self.f.write(hdr + struct.pack("<I", _masked_crc(hdr)) + ev + struct.pack("<I", _masked_crc(ev)))
         self.f.flush()
 
+    def add_scalar(self, tag: str, scalar_value: float, global_step: int = 0, walltime: Optional[float] = None):
+        """``torch.utils.tensorboard.SummaryWriter.add_scalar`` signature."""
+        self.scalar(tag, scalar_value, global_step, walltime)
+
     def close(self):
         self.f.close()

@@ -1,0 +1,355 @@
+"""End-to-end control plane: experiments run through the in-process scheduler with real
+trial subprocesses (reference e2e strategy: test/e2e/v1beta1/scripts/gh-actions/run-e2e-experiment.py
+asserts the experiment reaches Succeeded with the expected trial counts and an optimal trial)."""
+import json
+import os
+import sys
+import textwrap
+
+import pytest
+import yaml
+
+from katib_amd.api import constants as C
+from katib_amd.api.conditions import ExperimentConditions as EC
+from katib_amd.api.yaml_io import load_experiment
+
+PY = sys.executable
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def quadratic_yaml(name="q", algorithm="random", settings=None, parallel=2, max_trials=6, max_failed=3, goal=None,
+                   params=None, command=None, extra_spec=""):
+    settings = settings or []
+    max_failed = min(max_failed, max_trials)
+    params = params or [
+        {"name": "a", "parameterType": "double", "feasibleSpace": {"min": "0", "max": "2"}},
+        {"name": "b", "parameterType": "double", "feasibleSpace": {"min": "-1", "max": "1"}},
+    ]
+    names = [p["name"] for p in params]
+    if command is None:
+        assigns = "; ".join("%s=${trialParameters.%s}" % (n, n) for n in names)
+        command = [PY, "-c", "%s; print('result=%%s' %% (4*float(a) - float(b)**2))" % assigns]
+    spec = {
+        "apiVersion": "kubeflow.org/v1beta1", "kind": "Experiment", "metadata": {"name": name},
+        "spec": {
+            "objective": {"type": "maximize", "objectiveMetricName": "result"},
+            "algorithm": {"algorithmName": algorithm, "algorithmSettings": settings},
+            "parallelTrialCount": parallel, "maxTrialCount": max_trials, "maxFailedTrialCount": max_failed,
+            "parameters": params,
+            "trialTemplate": {
+                "primaryContainerName": "training-container",
+                "trialParameters": [{"name": n, "reference": n} for n in names],
+                "trialSpec": {"apiVersion": "batch/v1", "kind": "Job", "spec": {"template": {"spec": {
+                    "containers": [{"name": "training-container", "image": "python", "command": command,
+                                    "env": [{"name": "TRIAL_PARAMS", "value": " ".join(
+                                        "%s=${trialParameters.%s}" % (n, n) for n in names)}]}],
+                    "restartPolicy": "Never"}}}},
+            },
+        },
+    }
+    if goal is not None:
+        spec["spec"]["objective"]["goal"] = goal
+    text = yaml.safe_dump(spec)
+    if extra_spec:
+        d = yaml.safe_load(text)
+        d["spec"].update(yaml.safe_load(extra_spec))
+        text = yaml.safe_dump(d)
+    return load_experiment(text)
+
+
+def _reason(e):
+    return [c.reason for c in e.status.conditions if c.status == "True"][-1]
+
+
+def test_random_quadratic_example_completes(manager):
+    import os
+
+    e = load_experiment(os.path.join(os.path.dirname(__file__), "..", "examples", "hp-tuning",
+                                     "random-quadratic.yaml"))
+    e.spec.trial_template.trial_spec["spec"]["template"]["spec"]["containers"][0]["command"][0] = PY
+    manager.create_experiment(e)
+    done = manager.run_until_complete("random-quadratic", timeout=120)
+    assert EC.is_succeeded(done)
+    assert _reason(done) in (C.EXPERIMENT_MAX_TRIALS_REACHED_REASON, C.EXPERIMENT_GOAL_REACHED_REASON)
+    assert done.status.trials_succeeded >= 1
+    best = done.status.current_optimal_trial
+    assert best.best_trial_name
+    vals = {m.name: float(m.latest) for m in best.observation.metrics}
+    a = float([p.value for p in best.parameter_assignments if p.name == "a"][0])
+    b = float([p.value for p in best.parameter_assignments if p.name == "b"][0])
+    assert abs(vals["result"] - (4 * a - b * b)) < 1e-6
+    # every other succeeded trial is no better than the optimum
+    for t in manager.list_trials("random-quadratic"):
+        if t.status.observation and t.status.observation.metrics:
+            assert float(t.status.observation.metrics[0].max) <= vals["result"] + 1e-9
+    logs = manager.get_observation_log(best.best_trial_name, "result")
+    assert len(logs) == 1 and logs[0][1] == "result"
+
+
+@pytest.mark.parametrize("algorithm,settings,params", [
+    ("random", [{"name": "random_state", "value": "3"}], None),
+    ("tpe", [{"name": "random_state", "value": "3"}, {"name": "gamma", "value": "0.3"}], None),
+    ("multivariate-tpe", [{"name": "n_startup_trials", "value": "2"}], None),
+    ("cmaes", [{"name": "random_state", "value": "3"}], None),
+    ("sobol", [], None),
+    ("bayesianoptimization", [{"name": "random_state", "value": "3"}, {"name": "n_initial_points", "value": "2"}],
+     None),
+    ("grid", [], [{"name": "a", "parameterType": "double", "feasibleSpace": {"min": "0", "max": "2", "step": "1"}},
+                  {"name": "b", "parameterType": "int", "feasibleSpace": {"min": "-1", "max": "1"}}]),
+])
+def test_algorithms_end_to_end(manager, algorithm, settings, params):
+    e = quadratic_yaml(name="alg-" + algorithm, algorithm=algorithm, settings=settings, params=params,
+                       parallel=2, max_trials=6)
+    manager.create_experiment(e)
+    done = manager.run_until_complete(e.metadata.name, timeout=180)
+    assert EC.is_succeeded(done), done.status.conditions
+    assert done.status.trials_succeeded == 6
+    trials = manager.list_trials(e.metadata.name)
+    assert len(trials) == 6
+    seen = set()
+    for t in trials:
+        pa = tuple((p.name, p.value) for p in t.spec.parameter_assignments)
+        seen.add(pa)
+        for p in t.spec.parameter_assignments:
+            v = float(p.value)
+            if p.name == "a":
+                assert 0 <= v <= 2
+            else:
+                assert -1 <= v <= 1
+    if algorithm == "grid":
+        assert len(seen) == 6  # 3 x 3 grid, no repeats
+
+
+def test_goal_reached(manager):
+    e = quadratic_yaml(name="goal", goal=-100.0, parallel=1, max_trials=10)
+    manager.create_experiment(e)
+    done = manager.run_until_complete("goal", timeout=60)
+    assert _reason(done) == C.EXPERIMENT_GOAL_REACHED_REASON
+    assert done.status.trials_succeeded == 1
+
+
+def test_max_failed_trials(manager):
+    e = quadratic_yaml(name="failing", command=[PY, "-c", "import sys; sys.exit(3)"], parallel=2, max_trials=6,
+                       max_failed=2)
+    manager.create_experiment(e)
+    done = manager.run_until_complete("failing", timeout=60)
+    assert EC.is_failed(done)
+    assert _reason(done) == C.EXPERIMENT_FAILED_REASON
+    assert done.status.trials_failed >= 2
+
+
+def test_metrics_unavailable(manager):
+    e = quadratic_yaml(name="nometrics", command=[PY, "-c", "print('nothing here')"], parallel=1, max_trials=2,
+                       max_failed=2)
+    manager.create_experiment(e)
+    done = manager.run_until_complete("nometrics", timeout=60)
+    trials = manager.list_trials("nometrics")
+    assert all(any(c.type == "MetricsUnavailable" and c.status == "True" for c in t.status.conditions)
+               for t in trials)
+    assert EC.is_failed(done)
+
+
+def test_file_collector_json_format(manager, tmp_path):
+    path = str(tmp_path / "metrics.json")
+    code = textwrap.dedent("""
+        import json, sys
+        a = float(sys.argv[1]); b = float(sys.argv[2])
+        with open(%r, "a") as f:
+            for step in range(3):
+                f.write(json.dumps({"result": str(4*a - b*b - (2 - step)), "step": str(step)}) + "\\n")
+    """ % path)
+    e = quadratic_yaml(name="filejson", command=[PY, "-c", code, "${trialParameters.a}", "${trialParameters.b}"],
+                       parallel=1, max_trials=2,
+                       extra_spec=yaml.safe_dump({"metricsCollectorSpec": {
+                           "collector": {"kind": "File"},
+                           "source": {"fileSystemPath": {"path": path, "kind": "File", "format": "JSON"}}}}))
+    manager.create_experiment(e)
+    done = manager.run_until_complete("filejson", timeout=60)
+    assert EC.is_succeeded(done)
+    t = manager.get_trial(done.status.current_optimal_trial.best_trial_name)
+    m = t.status.observation.metrics[0]
+    assert float(m.max) - float(m.min) == pytest.approx(2.0)
+
+
+def test_stdout_custom_filter(manager):
+    code = "print('epoch 1 acc: 0.5'); print('epoch 2 acc: 0.75')"
+    e = quadratic_yaml(name="filter", command=[PY, "-c", code], parallel=1, max_trials=1,
+                       params=[{"name": "a", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                       extra_spec=yaml.safe_dump({
+                           "objective": {"type": "maximize", "objectiveMetricName": "acc"},
+                           "metricsCollectorSpec": {"collector": {"kind": "StdOut"},
+                                                    "source": {"filter": {"metricsFormat": [r"(\w+):\s*([\d.]+)"]}}}}))
+    e.spec.trial_template.trial_spec["spec"]["template"]["spec"]["containers"][0]["command"].append(
+        "${trialParameters.a}")
+    manager.create_experiment(e)
+    done = manager.run_until_complete("filter", timeout=60)
+    m = done.status.current_optimal_trial.observation.metrics[0]
+    assert (m.name, m.min, m.max, m.latest) == ("acc", "0.5", "0.75", "0.75")
+
+
+def test_tfevent_collector(manager, tmp_path):
+    logdir = str(tmp_path / "tb")
+    code = textwrap.dedent("""
+        import sys
+        sys.path.insert(0, %r)
+        from katib_amd.metricscollector.tfevent import EventWriter
+        w = EventWriter(%r + "/test")
+        for s in range(3):
+            w.add_scalar("accuracy", 0.5 + 0.1 * s, s)
+        w.close()
+    """ % (ROOT, logdir))
+    e = quadratic_yaml(name="tfevent", command=[PY, "-c", code, "${trialParameters.a}"], parallel=1, max_trials=1,
+                       params=[{"name": "a", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                       extra_spec=yaml.safe_dump({
+                           "objective": {"type": "maximize", "objectiveMetricName": "test/accuracy"},
+                           "metricsCollectorSpec": {"collector": {"kind": "TensorFlowEvent"},
+                                                    "source": {"fileSystemPath": {"path": logdir,
+                                                                                  "kind": "Directory"}}}}))
+    manager.create_experiment(e)
+    done = manager.run_until_complete("tfevent", timeout=60)
+    assert EC.is_succeeded(done), done.status.conditions
+    m = done.status.current_optimal_trial.observation.metrics[0]
+    assert m.name == "test/accuracy" and float(m.max) == pytest.approx(0.7) and float(m.min) == pytest.approx(0.5)
+
+
+def test_medianstop_early_stopping(manager):
+    # trials print 10 decreasing-quality steps; later trials worse than the running mean get stopped
+    code = textwrap.dedent("""
+        import sys, time
+        a = float(sys.argv[1])
+        for s in range(12):
+            print("loss=%f" % (a + 0.01 * s), flush=True)
+            time.sleep(0.05)
+    """)
+    e = quadratic_yaml(name="medianstop", command=[PY, "-u", "-c", code, "${trialParameters.a}"], parallel=1,
+                       max_trials=7,
+                       params=[{"name": "a", "parameterType": "double", "feasibleSpace": {"min": "0", "max": "10"}}],
+                       extra_spec=yaml.safe_dump({
+                           "objective": {"type": "minimize", "objectiveMetricName": "loss"},
+                           "algorithm": {"algorithmName": "grid"},
+                           "earlyStopping": {"algorithmName": "medianstop", "algorithmSettings": [
+                               {"name": "min_trials_required", "value": "2"}, {"name": "start_step", "value": "2"}]}}))
+    e.spec.parameters[0].feasible_space.step = "1"
+    manager.create_experiment(e)
+    done = manager.run_until_complete("medianstop", timeout=120)
+    trials = sorted(manager.list_trials("medianstop"), key=lambda t: t.metadata.creation_timestamp)
+    stopped = [t for t in trials if any(c.type == "EarlyStopped" and c.status == "True" for c in t.status.conditions)]
+    # grid order is 0,1,2,...: after 2 trials the rule is loss > mean(first two) -> later trials stop early
+    assert stopped, [t.status.conditions for t in trials]
+    assert all(t.spec.early_stopping_rules for t in stopped)
+    assert EC.is_succeeded(done)
+    assert done.status.trials_early_stopped == len(stopped)
+
+
+def test_resume_long_running(manager):
+    e = quadratic_yaml(name="resume", parallel=1, max_trials=2,
+                       extra_spec=yaml.safe_dump({"resumePolicy": "LongRunning"}))
+    manager.create_experiment(e)
+    done = manager.run_until_complete("resume", timeout=60)
+    assert _reason(done) == C.EXPERIMENT_MAX_TRIALS_REACHED_REASON
+    done.spec.max_trial_count = 4
+    manager.update_experiment(done)
+    done = manager.run_until_complete("resume", timeout=60)
+    assert done.status.trials_succeeded == 4 and EC.is_succeeded(done)
+
+
+def test_resume_never_is_not_restartable(manager):
+    e = quadratic_yaml(name="never", parallel=1, max_trials=1)
+    manager.create_experiment(e)
+    done = manager.run_until_complete("never", timeout=60)
+    done.spec.max_trial_count = 3
+    from katib_amd.api.validation import ValidationError
+
+    with pytest.raises(ValidationError):
+        manager.update_experiment(done)
+
+
+def test_delete_experiment_cleans_up(manager):
+    e = quadratic_yaml(name="del", parallel=1, max_trials=1)
+    manager.create_experiment(e)
+    done = manager.run_until_complete("del", timeout=60)
+    tname = done.status.current_optimal_trial.best_trial_name
+    assert manager.get_observation_log(tname)
+    manager.delete_experiment("del")
+    assert not manager.list_trials("del")
+    assert manager.get_observation_log(tname) == []
+
+
+def test_hyperband_end_to_end(manager):
+    code = "import sys; r=int(sys.argv[2]); print('acc=%f' % (float(sys.argv[1]) * r / 9.0))"
+    params = [{"name": "lr", "parameterType": "double", "feasibleSpace": {"min": "0.1", "max": "1.0"}},
+              {"name": "epochs", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "9"}}]
+    e = quadratic_yaml(name="hb", algorithm="hyperband",
+                       settings=[{"name": "resource_name", "value": "epochs"}, {"name": "eta", "value": "3"},
+                                 {"name": "r_l", "value": "9"}],
+                       params=params, parallel=9, max_trials=20,
+                       command=[PY, "-c", code, "${trialParameters.lr}", "${trialParameters.epochs}"],
+                       extra_spec=yaml.safe_dump({"objective": {"type": "maximize", "objectiveMetricName": "acc"}}))
+    manager.create_experiment(e)
+    done = manager.run_until_complete("hb", timeout=180)
+    assert EC.is_succeeded(done), done.status.conditions
+    epochs = sorted({int(p.value) for t in manager.list_trials("hb") for p in t.spec.parameter_assignments
+                     if p.name == "epochs"})
+    assert epochs[0] == 1 and 9 in epochs  # first bracket r=1 rung, promoted trials at r_l
+    sugg = manager.get_suggestion("hb")
+    names = {s.name for s in sugg.status.algorithm_settings}
+    assert {"eta", "s_max", "r_l", "current_s", "current_i", "evaluating_trials"} <= names
+
+
+def test_pbt_end_to_end(manager, tmp_path):
+    code = textwrap.dedent("""
+        import os, sys, json
+        lr = float(sys.argv[1]); d = os.environ.get("KATIB_TRIAL_CHECKPOINT_DIR", sys.argv[2])
+        os.makedirs(d, exist_ok=True)
+        p = os.path.join(d, "ckpt.json")
+        st = json.load(open(p)) if os.path.exists(p) else {"step": 0, "acc": 0.0}
+        for _ in range(3):
+            st["step"] += 1
+            st["acc"] += lr * (1.0 - st["acc"])
+            print("Validation-accuracy=%f" % st["acc"])
+        json.dump(st, open(p, "w"))
+    """)
+    params = [{"name": "lr", "parameterType": "double", "feasibleSpace": {"min": "0.01", "max": "0.5",
+                                                                          "step": "0.01"}}]
+    e = quadratic_yaml(name="pbt", algorithm="pbt",
+                       settings=[{"name": "suggestion_trial_dir", "value": str(tmp_path / "pbt")},
+                                 {"name": "n_population", "value": "5"},
+                                 {"name": "truncation_threshold", "value": "0.4"}],
+                       params=params, parallel=5, max_trials=15, max_failed=3,
+                       command=[PY, "-c", code, "${trialParameters.lr}", str(tmp_path / "ckpt")],
+                       extra_spec=yaml.safe_dump({"objective": {"type": "maximize",
+                                                                "objectiveMetricName": "Validation-accuracy"}}))
+    manager.create_experiment(e)
+    done = manager.run_until_complete("pbt", timeout=240)
+    assert EC.is_succeeded(done), done.status.conditions
+    trials = manager.list_trials("pbt")
+    gens = {t.metadata.labels.get("pbt.suggestion.katib.kubeflow.org/generation") for t in trials}
+    assert len(gens) >= 2
+    # children resumed from a parent checkpoint keep improving
+    assert float(done.status.current_optimal_trial.observation.metrics[0].max) > 0.5
+
+
+def test_prometheus_counters(manager):
+    e = quadratic_yaml(name="prom", parallel=2, max_trials=3)
+    manager.create_experiment(e)
+    manager.run_until_complete("prom", timeout=60)
+    text = manager.metrics.expose()
+    assert 'katib_trial_created_total{namespace="default"} 3' in text
+    assert 'katib_experiment_succeeded_total{namespace="default"} 1' in text
+
+
+def test_function_kind_via_sdk_tune(manager):
+    from katib_amd.sdk import KatibClient, search
+
+    def objective(parameters):
+        x = float(parameters["x"])
+        print("score=%f" % (-(x - 1.0) ** 2))
+
+    client = KatibClient(manager=manager)
+    client.tune(name="tune", objective=objective, parameters={"x": search.double(min=-2, max=3)},
+                objective_metric_name="score", max_trial_count=4, parallel_trial_count=2,
+                algorithm_name="random")
+    done = manager.run_until_complete("tune", timeout=120)
+    assert EC.is_succeeded(done), done.status.conditions
+    assert client.get_optimal_hyperparameters("tune").best_trial_name
+    assert done.status.trials_succeeded == 4
