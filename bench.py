@@ -64,6 +64,8 @@ def main():
                 print("hip ops unavailable (%s); using torch ops" % e, file=sys.stderr)
             dops.set_backend("torch")
             args.ops = "torch"
+    if dev.type != "cuda":
+        args.ops = "torch"
     cfg = CONFIGS[args.config]
     layout = DartsLayout(PRIMS, init_channels=cfg["init_channels"], num_layers=cfg["num_layers"],
                          num_nodes=cfg["num_nodes"], stem_multiplier=cfg["stem_multiplier"])
