@@ -882,7 +882,8 @@ class Manager:
         base_env = {"KATIB_TRIAL_NAME": name, "KATIB_EXPERIMENT_NAME": exp_name, "KATIB_TRIAL_DIR": run.trial_dir,
                     "KATIB_NAMESPACE": ns, "PYTHONUNBUFFERED": "1",
                     "HIP_VISIBLE_DEVICES": ",".join(str(d) for d in run.devices) if run.devices else "",
-                    "KATIB_AMD_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or ""}
+                    "KATIB_AMD_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or "",
+                    "KATIB_TRIAL_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or ""}
         # each replica gets its share of the trial's devices
         dev_iter = iter(run.devices)
         plan = run.plan

@@ -1,0 +1,133 @@
+"""ResNet-18 on CIFAR-10-shaped data (BASELINE config 3: HyperBand + median-stop).
+
+``--epochs`` is the HyperBand resource. The network is the CIFAR ResNet-18 variant
+(3x3 stem, no max-pool, [2, 2, 2, 2] basic blocks, 64-512 channels). MI355X
+specifics: channels-last activations, bf16 autocast (fp32 master weights, MFMA
+convolutions through MIOpen), device-resident synthetic data, and the whole train
+step (forward, loss, backward, SGD+Nesterov momentum) captured as one HIP graph.
+
+Per epoch it prints ``epoch=<e> loss=<l> Validation-accuracy=<a>``; the median-stop
+rule compares the objective after ``start_step`` reports.
+"""
+
+from __future__ import annotations
+
+import argparse
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .common import CapturedStep, Timer, device, pattern_images, report
+
+
+def parse_args(argv):
+    p = argparse.ArgumentParser(description="ResNet-18 CIFAR-10 trial (katib-amd)")
+    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--weight-decay", type=float, default=5e-4)
+    p.add_argument("--batch-size", type=int, default=256)
+    p.add_argument("--epochs", type=int, default=3)
+    p.add_argument("--num-train", type=int, default=50000)
+    p.add_argument("--num-valid", type=int, default=10000)
+    p.add_argument("--width", type=int, default=64)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--capture", type=int, default=1)
+    p.add_argument("--max-steps", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
+    return p.parse_args(argv)
+
+
+class BasicBlock(nn.Module):
+    def __init__(self, cin, cout, stride):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.short = None
+        if stride != 1 or cin != cout:
+            self.short = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return F.relu(out + (x if self.short is None else self.short(x)))
+
+
+class ResNet18(nn.Module):
+    def __init__(self, width=64, classes=10):
+        super().__init__()
+        w = width
+        self.stem = nn.Sequential(nn.Conv2d(3, w, 3, 1, 1, bias=False), nn.BatchNorm2d(w), nn.ReLU())
+        layers, cin = [], w
+        for i, cout in enumerate((w, 2 * w, 4 * w, 8 * w)):
+            stride = 1 if i == 0 else 2
+            layers += [BasicBlock(cin, cout, stride), BasicBlock(cout, cout, 1)]
+            cin = cout
+        self.layers = nn.Sequential(*layers)
+        self.fc = nn.Linear(cin, classes)
+
+    def forward(self, x):
+        x = self.layers(self.stem(x))
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+
+def main(argv=None):
+    args = parse_args(argv if argv is not None else [])
+    dev = device()
+    torch.manual_seed(args.seed)
+    cuda = dev.type == "cuda"
+    mf = torch.channels_last if cuda else torch.contiguous_format
+    x, y = pattern_images(args.num_train + args.num_valid, seed=4321, dev=dev,
+                          dtype=torch.bfloat16 if cuda else torch.float32)
+    x = x.contiguous(memory_format=mf)
+    tx, ty, vx, vy = x[:args.num_train], y[:args.num_train], x[args.num_train:], y[args.num_train:]
+    model = ResNet18(args.width).to(dev).to(memory_format=mf)
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay,
+                          nesterov=True)
+    for p_ in model.parameters():
+        p_.grad = torch.zeros_like(p_)
+    bs = min(args.batch_size, args.num_train)
+    steps = args.num_train // bs
+    if args.max_steps:
+        steps = min(steps, args.max_steps)
+    idx = torch.zeros(bs, dtype=torch.long, device=dev)
+    loss_buf = torch.zeros((), device=dev)
+
+    def train_step():
+        xb = tx.index_select(0, idx).contiguous(memory_format=mf)
+        yb = ty.index_select(0, idx)
+        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda):
+            loss = F.cross_entropy(model(xb.float() if not cuda else xb), yb)
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        opt.step()
+        loss_buf.add_(loss.detach().float())
+        return loss_buf
+
+    step = CapturedStep(train_step, enabled=bool(args.capture))
+    gen = torch.Generator(device=dev).manual_seed(args.seed)
+    timer = Timer()
+    acc = 0.0
+    for epoch in range(args.epochs):
+        model.train()
+        perm = torch.randperm(args.num_train, device=dev, generator=gen)[:steps * bs].view(steps, bs)
+        loss_buf.zero_()
+        for s in range(steps):
+            idx.copy_(perm[s])
+            step()
+        model.eval()
+        correct = torch.zeros((), device=dev)
+        with torch.no_grad(), torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda):
+            for i in range(0, args.num_valid, 1024):
+                correct += (model(vx[i:i + 1024]).argmax(1) == vy[i:i + 1024]).sum()
+        acc = float(correct) / max(args.num_valid, 1)
+        report(epoch=epoch, loss=float(loss_buf) / max(steps, 1), **{"Validation-accuracy": acc})
+    report(train_seconds=timer.elapsed())
+    return acc
+
+
+if __name__ == "__main__":
+    import sys
+
+    main(sys.argv[1:])

@@ -299,7 +299,7 @@ def test_hyperband_end_to_end(manager):
 def test_pbt_end_to_end(manager, tmp_path):
     code = textwrap.dedent("""
         import os, sys, json
-        lr = float(sys.argv[1]); d = os.environ.get("KATIB_TRIAL_CHECKPOINT_DIR", sys.argv[2])
+        lr = float(sys.argv[1]); d = sys.argv[2]  # suggestion_trial_dir, mapped to the member's dir
         os.makedirs(d, exist_ok=True)
         p = os.path.join(d, "ckpt.json")
         st = json.load(open(p)) if os.path.exists(p) else {"step": 0, "acc": 0.0}
@@ -316,7 +316,7 @@ def test_pbt_end_to_end(manager, tmp_path):
                                  {"name": "n_population", "value": "5"},
                                  {"name": "truncation_threshold", "value": "0.4"}],
                        params=params, parallel=5, max_trials=15, max_failed=3,
-                       command=[PY, "-c", code, "${trialParameters.lr}", str(tmp_path / "ckpt")],
+                       command=[PY, "-c", code, "${trialParameters.lr}", str(tmp_path / "pbt")],
                        extra_spec=yaml.safe_dump({"objective": {"type": "maximize",
                                                                 "objectiveMetricName": "Validation-accuracy"}}))
     manager.create_experiment(e)
