@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Trials/hour benchmark (36.3 completed trials/hour, random search on an
+MNIST MLP, parallelTrialCount=3, K8s CPU jobs).
+
+Runs BASELINE config 2 end to end through the in-process scheduler: a TPE
+Experiment over (lr, batch size, hidden width) of the MNIST MLP workload with
+``--parallel`` trials spread over the node's GPUs (``--slots-per-gpu`` warm workers
+per GPU), and reports completed trials per hour of wall clock from experiment
+creation to completion. One process drives all GPUs (no torchrun).
+
+    python bench_trials.py --trials 48 --parallel 8 [--epochs 3] [--num-train 60000]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+B1_TRIALS_PER_HOUR = 36.3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trials", type=int, default=48)
+    ap.add_argument("--parallel", type=int, default=8)
+    ap.add_argument("--gpus", type=int, default=0, help="0 = all visible")
+    ap.add_argument("--slots-per-gpu", type=int, default=0, help="0 = ceil(parallel / gpus)")
+    ap.add_argument("--epochs", type=int, default=3)
+    ap.add_argument("--num-train", type=int, default=60000)
+    ap.add_argument("--algorithm", default="tpe")
+    ap.add_argument("--state-dir", default="")
+    args = ap.parse_args()
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from katib_amd.api.conditions import ExperimentConditions as EC
+    from katib_amd.api.yaml_io import load_experiment
+    from katib_amd.controller.config import detect_gpus
+    from katib_amd.controller.manager import Manager
+
+    n_gpus = args.gpus or detect_gpus()
+    slots = args.slots_per_gpu or (max(1, -(-args.parallel // n_gpus)) if n_gpus else 1)
+    state = args.state_dir or tempfile.mkdtemp(prefix="katib-amd-bench-")
+    m = Manager(state_dir=state, num_devices=n_gpus, journal=False)
+    m.config.amd.slots_per_device = slots
+    m.slots = m.N.SlotPool(m.n_devices, slots)
+    e = load_experiment(os.path.join(os.path.dirname(os.path.abspath(__file__)), "examples", "hp-tuning",
+                                     "tpe-mnist-mlp.yaml"))
+    e.spec.max_trial_count = args.trials
+    e.spec.parallel_trial_count = args.parallel
+    e.spec.objective.goal = None
+    e.spec.algorithm.algorithm_name = args.algorithm
+    if args.algorithm != "tpe":
+        e.spec.algorithm.algorithm_settings = []
+    spec = e.spec.trial_template.trial_spec["spec"]
+    spec["gpus"] = 1 if n_gpus else 0
+    spec["args"] = [a for a in spec["args"] if not a.startswith("--epochs")] + [
+        "--epochs=%d" % args.epochs, "--num-train=%d" % args.num_train]
+    t0 = time.time()
+    m.create_experiment(e)
+    done = m.run_until_complete(e.metadata.name, timeout=3 * 3600)
+    wall = time.time() - t0
+    completed = (done.status.trials_succeeded or 0) + (done.status.trials_failed or 0) + \
+        (done.status.trials_early_stopped or 0) + (done.status.trials_killed or 0)
+    best = done.status.current_optimal_trial
+    best_acc = None
+    if best is not None and best.observation is not None:
+        for mt in best.observation.metrics or []:
+            if mt.name == "Validation-accuracy":
+                best_acc = float(mt.max)
+    m.shutdown()
+    tph = completed / wall * 3600.0
+    print(json.dumps({
+        "metric": "completed_trials_per_hour", "value": round(tph, 1), "unit": "trials/h", "n_gpus": n_gpus,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": round(tph / B1_TRIALS_PER_HOUR, 2),
+        "dtype": "bf16", "data": "synthetic (MNIST-shaped teacher task, device-resident)",
+        "wall_s": round(wall, 2), "trials_completed": completed, "trials_succeeded": done.status.trials_succeeded,
+        "succeeded": EC.is_succeeded(done), "best_validation_accuracy": best_acc,
+        "config": {"experiment": "tpe-mnist-mlp", "algorithm": args.algorithm, "parallel": args.parallel,
+                   "max_trials": args.trials, "epochs": args.epochs, "num_train": args.num_train,
+                   "slots_per_gpu": slots}}))
+
+
+if __name__ == "__main__":
+    main()
