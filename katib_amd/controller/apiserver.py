@@ -1,0 +1,264 @@
+"""HTTP JSON API over a :class:`~katib_amd.controller.manager.Manager` - the node's
+replacement for the Kubernetes API server (CRUD on Experiments/Trials/Suggestions)
+plus the Katib UI backend endpoints (reference ``pkg/ui/v1beta1/backend.go:49-772``,
+``hp.go:38-320``, ``nas.go:30-109``) and the Prometheus ``/metrics`` endpoint
+(reference ``cmd/katib-controller`` metricsAddr ``:8080``).
+
+Routes (``{ns}`` = namespace):
+
+* ``GET/POST /apis/kubeflow.org/v1beta1/namespaces/{ns}/experiments`` (POST body YAML or JSON)
+* ``GET/PUT/DELETE /apis/kubeflow.org/v1beta1/namespaces/{ns}/experiments/{name}``
+* ``GET /apis/kubeflow.org/v1beta1/namespaces/{ns}/trials[?labelSelector=katib.kubeflow.org/experiment=X]``
+* ``GET /apis/kubeflow.org/v1beta1/namespaces/{ns}/trials/{name}``, ``.../suggestions[/{name}]``
+* ``POST /api/v1/namespaces/{ns}/configmaps`` (trial templates), ``GET`` to list
+* ``GET /katib/observation_logs?trialName=&metricName=&startTime=&endTime=``
+* ``GET /katib/fetch_hp_job_info/?experimentName=&namespace=`` - JSON-encoded CSV
+  ``Status,trialName,<objective>,<additional...>,<params...>`` with the best value per
+  metric, as the reference UI backend returns it
+* ``GET /katib/fetch_hp_job_trial_info/?trialName=&namespace=`` - JSON-encoded CSV
+  ``metricName,time,value``
+* ``GET /katib/fetch_nas_job_info/?experimentName=&namespace=`` - per-trial architecture
+* ``GET /metrics``, ``/healthz``, ``/readyz``
+
+Errors come back as ``{"kind": "Status", "code": c, "reason": r, "message": m}``
+(400 invalid, 404 not found, 409 already exists) so the remote client can raise the
+same exceptions as the in-process one.
+"""
+
+from __future__ import annotations
+
+import json
+import re
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Optional
+from urllib.parse import parse_qs, urlparse
+
+import yaml
+
+from ..api import constants as C
+from ..api.models import V1beta1Experiment
+from ..api.validation import ValidationError
+
+_API = re.compile(r"^/apis/kubeflow\.org/v1beta1/namespaces/([^/]+)/(experiments|trials|suggestions)(?:/([^/]+))?/?$")
+_CM = re.compile(r"^/api/v1/namespaces/([^/]+)/configmaps/?$")
+
+
+class _Err(Exception):
+    def __init__(self, code, reason, message):
+        super().__init__(message)
+        self.code, self.reason, self.message = code, reason, message
+
+
+def _best_values(trial, logs):
+    """Best value per metric by objective direction (hp.go:140-166)."""
+    best = {}
+    minimize = trial.spec.objective.type == "minimize"
+    for _, name, value in logs:
+        if name not in best:
+            best[name] = value
+            continue
+        try:
+            cur, prev = float(value), float(best[name])
+        except ValueError:
+            continue
+        if (minimize and cur < prev) or (not minimize and cur > prev):
+            best[name] = value
+    return best
+
+
+class ApiServer:
+    def __init__(self, manager, address: str = "127.0.0.1", port: int = 8080):
+        self.m = manager
+        handler = self._make_handler()
+        self.httpd = ThreadingHTTPServer((address, port), handler)
+        self.port = self.httpd.server_address[1]
+        self._thread: Optional[threading.Thread] = None
+
+    def start(self):
+        self._thread = threading.Thread(target=self.httpd.serve_forever, name="katib-amd-api", daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self):
+        self.httpd.shutdown()
+        self.httpd.server_close()
+
+    # ------------------------------------------------------------------ dispatch
+    def handle(self, method: str, path: str, query: dict, body: bytes):
+        m = self.m
+        if path in ("/healthz", "/readyz"):
+            return 200, "text/plain", b"ok"
+        if path == "/metrics":
+            return 200, "text/plain; version=0.0.4", m.metrics.expose().encode()
+        if path == "/katib/observation_logs":
+            logs = m.get_observation_log(_q(query, "trialName"), _q(query, "metricName", ""),
+                                         _q(query, "startTime", ""), _q(query, "endTime", ""))
+            return _json({"metricLogs": [{"timeStamp": t, "metric": {"name": n, "value": v}} for t, n, v in logs]})
+        if path.rstrip("/") == "/katib/fetch_hp_job_info":
+            return _json(self._hp_job_info(_q(query, "experimentName"), _q(query, "namespace")))
+        if path.rstrip("/") == "/katib/fetch_hp_job_trial_info":
+            return _json(self._hp_trial_info(_q(query, "trialName"), _q(query, "namespace")))
+        if path.rstrip("/") == "/katib/fetch_nas_job_info":
+            return _json(self._nas_job_info(_q(query, "experimentName"), _q(query, "namespace")))
+        mm = _CM.match(path)
+        if mm:
+            ns = mm.group(1)
+            if method == "POST":
+                cm = _load_body(body)
+                md = cm.get("metadata") or {}
+                m.add_configmap(md.get("namespace") or ns, md["name"], cm.get("data") or {}, md.get("labels"))
+                return _json(cm, 201)
+            return _json({"items": [{"metadata": {"namespace": n_, "name": name_}, "data": data}
+                                    for n_, name_, data in m.configmaps.list() if n_ == ns]})
+        mm = _API.match(path)
+        if not mm:
+            raise _Err(404, "NotFound", "the server could not find the requested resource")
+        ns, kind, name = mm.groups()
+        if kind == "experiments":
+            if method == "GET" and name:
+                return _json(self._get(m.get_experiment, name, ns, "experiments").to_k8s())
+            if method == "GET":
+                return _json({"items": [e.to_k8s() for e in m.list_experiments(ns)]})
+            if method == "POST":
+                exp = V1beta1Experiment.from_k8s(_load_body(body))
+                try:
+                    out = m.create_experiment(exp, ns)
+                except ValidationError as e:
+                    raise _Err(400, "Invalid", str(e))
+                except ValueError as e:
+                    if "already exists" in str(e):
+                        raise _Err(409, "AlreadyExists", str(e))
+                    raise _Err(400, "BadRequest", str(e))
+                return _json(out.to_k8s(), 201)
+            if method == "PUT" and name:
+                exp = V1beta1Experiment.from_k8s(_load_body(body))
+                exp.metadata.namespace = exp.metadata.namespace or ns
+                try:
+                    return _json(m.update_experiment(exp).to_k8s())
+                except ValidationError as e:
+                    raise _Err(400, "Invalid", str(e))
+                except KeyError:
+                    raise _Err(404, "NotFound", 'experiments.kubeflow.org "%s" not found' % name)
+            if method == "DELETE" and name:
+                self._get(m.get_experiment, name, ns, "experiments")
+                m.delete_experiment(name, ns)
+                return _json({"kind": "Status", "status": "Success"})
+        if kind == "trials":
+            if name:
+                return _json(self._get(m.get_trial, name, ns, "trials").to_k8s())
+            exp = None
+            sel = _q(query, "labelSelector", "")
+            if sel.startswith(C.LABEL_EXPERIMENT_NAME + "="):
+                exp = sel.split("=", 1)[1]
+            return _json({"items": [t.to_k8s() for t in m.list_trials(exp, ns)]})
+        if kind == "suggestions":
+            if name:
+                return _json(self._get(m.get_suggestion, name, ns, "suggestions").to_k8s())
+            return _json({"items": [s.to_k8s() for s in m.list_suggestions(ns)]})
+        raise _Err(405, "MethodNotAllowed", "%s not allowed on %s" % (method, path))
+
+    @staticmethod
+    def _get(fn, name, ns, plural):
+        try:
+            return fn(name, ns)
+        except KeyError:
+            raise _Err(404, "NotFound", '%s.kubeflow.org "%s" not found' % (plural, name))
+
+    def _hp_job_info(self, name, ns):
+        e = self._get(self.m.get_experiment, name, ns, "experiments")
+        metrics = [e.spec.objective.objective_metric_name] + list(e.spec.objective.additional_metric_names or [])
+        params = [p.name for p in e.spec.parameters or []]
+        lines = [",".join(["Status", "trialName"] + metrics + params)]
+        for t in self.m.list_trials(name, ns):
+            last = t.status.conditions[-1].type if t.status and t.status.conditions else ""
+            row = {}
+            if any(c.type in ("Succeeded", "EarlyStopped") and c.status == "True" for c in t.status.conditions or []):
+                row = _best_values(t, self.m.get_observation_log(t.metadata.name))
+            for pa in t.spec.parameter_assignments or []:
+                row.setdefault(pa.name, pa.value)
+            lines.append(",".join([last, t.metadata.name] + [row.get(k, "") for k in metrics + params]))
+        return "\n".join(lines)
+
+    def _hp_trial_info(self, name, ns):
+        self._get(self.m.get_trial, name, ns, "trials")
+        lines = ["metricName,time,value"]
+        for ts, n, v in self.m.get_observation_log(name):
+            lines.append("%s,%s,%s" % (n, ts[:19], v))
+        return "\n".join(lines)
+
+    def _nas_job_info(self, name, ns):
+        self._get(self.m.get_experiment, name, ns, "experiments")
+        out = []
+        for t in self.m.list_trials(name, ns):
+            arch = {pa.name: pa.value for pa in t.spec.parameter_assignments or []}
+            metrics = {}
+            if t.status.observation is not None:
+                metrics = {mt.name: mt.latest for mt in t.status.observation.metrics or []}
+            out.append({"trialName": t.metadata.name, "assignments": arch, "metrics": metrics,
+                        "status": t.status.conditions[-1].type if t.status.conditions else ""})
+        return out
+
+    def _make_handler(self):
+        server = self
+
+        class Handler(BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, fmt, *args):  # quiet
+                pass
+
+            def _do(self, method):
+                u = urlparse(self.path)
+                n = int(self.headers.get("Content-Length") or 0)
+                body = self.rfile.read(n) if n else b""
+                try:
+                    code, ctype, data = server.handle(method, u.path, parse_qs(u.query), body)
+                except _Err as e:
+                    code, ctype = e.code, "application/json"
+                    data = json.dumps({"kind": "Status", "code": e.code, "reason": e.reason,
+                                       "message": e.message}).encode()
+                except Exception as e:  # noqa: BLE001 - reported to the client
+                    code, ctype = 500, "application/json"
+                    data = json.dumps({"kind": "Status", "code": 500, "reason": "InternalError",
+                                       "message": str(e)}).encode()
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(data)))
+                self.end_headers()
+                self.wfile.write(data)
+
+            def do_GET(self):
+                self._do("GET")
+
+            def do_POST(self):
+                self._do("POST")
+
+            def do_PUT(self):
+                self._do("PUT")
+
+            def do_DELETE(self):
+                self._do("DELETE")
+
+        return Handler
+
+
+def _q(query, key, default=None):
+    v = query.get(key)
+    if not v:
+        if default is None:
+            raise _Err(400, "BadRequest", "no '%s' provided" % key)
+        return default
+    return v[0]
+
+
+def _json(obj, code=200):
+    return code, "application/json", json.dumps(obj).encode()
+
+
+def _load_body(body: bytes):
+    text = body.decode()
+    try:
+        return json.loads(text)
+    except json.JSONDecodeError:
+        return yaml.safe_load(text)

@@ -43,8 +43,18 @@ def _shared_manager():
 
 
 class KatibClient:
-    def __init__(self, namespace: str = "default", manager=None, config_file: Optional[str] = None, **_):
+    def __init__(self, namespace: str = "default", manager=None, config_file: Optional[str] = None,
+                 host: Optional[str] = None, **_):
+        """``manager``: an in-process scheduler; ``host``: URL of a ``katib-amd serve`` daemon
+        (also taken from ``$KATIB_AMD_HOST``); neither: a shared in-process scheduler."""
+        import os
+
         self.namespace = namespace
+        host = host or os.environ.get("KATIB_AMD_HOST")
+        if manager is None and host:
+            from .remote import RemoteManager
+
+            manager = RemoteManager(host, namespace)
         if manager is None:
             manager = _shared_manager()
             if config_file:
