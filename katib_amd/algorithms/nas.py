@@ -34,11 +34,16 @@ DARTS_DEFAULT_SETTINGS = {
 
 
 # ------------------------------------------------------------------------------- common validation
-def validate_operations(operations) -> (bool, str):
-    """``nas/common/validation.py:18-63``."""
+def validate_operations(operations, parameterless=()) -> (bool, str):
+    """``nas/common/validation.py:18-63``. ``parameterless``: operation types accepted
+    without parameters - documented divergence for DARTS' ``skip_connection``, which the
+    reference's own darts examples declare without parameters but its shared validator
+    rejects ("Missing ParameterConfigs")."""
     for op in operations:
         if not op.operation_type:
             return False, "Missing operationType in Operation:\n{}".format(op)
+        if not op.parameter_specs.parameters and op.operation_type in parameterless:
+            continue
         if not op.parameter_specs.parameters:
             return False, "Missing ParameterConfigs in Operation:\n{}".format(op)
         for p in op.parameter_specs.parameters:
@@ -107,7 +112,7 @@ class DartsService(SuggestionService):
 
     def ValidateAlgorithmSettings(self, request, context=None):
         spec = request.experiment.spec
-        ok, msg = validate_operations(spec.nas_config.operations.operation)
+        ok, msg = validate_operations(spec.nas_config.operations.operation, parameterless=("skip_connection",))
         if ok:
             ok, msg = validate_darts_settings(spec.algorithm.algorithm_settings)
         if not ok:

@@ -50,6 +50,7 @@ from .converters import comparison_from_pb, convert_experiment, convert_trials
 from .jobs import JobSpecError, LaunchPlan, job_status, make_plan, map_paths, path_mapping
 from .manifest import ConfigMapStore, Generator
 
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 log = logging.getLogger("katib_amd.controller")
 
 _RAND_ALPHABET = "bcdfghjklmnpqrstvwxz2456789"  # k8s utilrand.String alphabet
@@ -883,7 +884,9 @@ class Manager:
                     "KATIB_NAMESPACE": ns, "PYTHONUNBUFFERED": "1",
                     "HIP_VISIBLE_DEVICES": ",".join(str(d) for d in run.devices) if run.devices else "",
                     "KATIB_AMD_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or "",
-                    "KATIB_TRIAL_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or ""}
+                    "KATIB_TRIAL_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or "",
+                    # trials may run the built-in workloads with `python -m katib_amd.workloads.X`
+                    "PYTHONPATH": os.pathsep.join(p for p in (_PKG_ROOT, os.environ.get("PYTHONPATH", "")) if p)}
         # each replica gets its share of the trial's devices
         dev_iter = iter(run.devices)
         plan = run.plan
@@ -899,6 +902,8 @@ class Manager:
             if run.devices:
                 env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devs) if devs else ""
             env.update({k: map_paths([v], run.path_map)[0] for k, v in rep.env.items()})
+            if "PYTHONPATH" in rep.env:
+                env["PYTHONPATH"] = os.pathsep.join((env["PYTHONPATH"], _PKG_ROOT))
             argv = map_paths(rep.argv, run.path_map)
             cwd = rep.cwd or run.trial_dir
             proc_name = name if rep.primary else "%s~%s-%d" % (name, rep.role, rep.index)
@@ -958,9 +963,8 @@ class Manager:
         env = ["HIP_VISIBLE_DEVICES=%s" % dkey, "PYTHONUNBUFFERED=1"]
         wlog = os.path.join(self.state_dir, "workers", "worker-%s-%d.log" % (dkey or "cpu", len(self.workers)))
         os.makedirs(os.path.dirname(wlog), exist_ok=True)
-        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env.append("PYTHONPATH=%s%s" % (pkg_root, (":" + os.environ["PYTHONPATH"]) if os.environ.get("PYTHONPATH")
-                                        else ""))
+        env.append("PYTHONPATH=%s%s" % (_PKG_ROOT, (":" + os.environ["PYTHONPATH"]) if os.environ.get("PYTHONPATH")
+                                         else ""))
         wid = self.runtime.spawn_worker([py, "-m", "katib_amd.controller.worker"] + (["--warm"] if dkey else []),
                                         env, self.state_dir, wlog)
         if wid < 0:

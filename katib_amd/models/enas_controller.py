@@ -128,7 +128,8 @@ class EnasController(torch.nn.Module):
         self.opt.step()
         self.train_step += 1
         norm = self.num_layers * (self.num_layers - 1) / 2
-        return {"loss": float(loss), "entropy": float(ent), "grad_norm": gn, "baseline": float(self.baseline),
+        return {"loss": float(loss.detach()), "entropy": float(ent.detach()), "grad_norm": gn,
+                "baseline": float(self.baseline),
                 "skip_rate": float(skip_count) / norm if norm else 0.0}
 
     def state(self):
