@@ -212,33 +212,41 @@ def test_tfevent_collector(manager, tmp_path):
     assert m.name == "test/accuracy" and float(m.max) == pytest.approx(0.7) and float(m.min) == pytest.approx(0.5)
 
 
-def test_medianstop_early_stopping(manager):
-    # trials print 10 decreasing-quality steps; later trials worse than the running mean get stopped
+def test_medianstop_early_stopping(manager, tmp_path):
+    # the k-th trial to start reports loss k + 0.01*step: once two trials have succeeded the
+    # median-stop rule (loss > mean of their first start_step values) stops every later one
+    counter = str(tmp_path / "counter")
     code = textwrap.dedent("""
-        import sys, time
-        a = float(sys.argv[1])
+        import fcntl, os, sys, time
+        with open(%r, "a+") as f:
+            fcntl.flock(f, fcntl.LOCK_EX)
+            f.seek(0)
+            k = len(f.read())
+            f.write("x")
         for s in range(12):
-            print("loss=%f" % (a + 0.01 * s), flush=True)
+            print("loss=%%f" %% (k + 0.01 * s), flush=True)
             time.sleep(0.05)
-    """)
+    """ % counter)
     e = quadratic_yaml(name="medianstop", command=[PY, "-u", "-c", code, "${trialParameters.a}"], parallel=1,
-                       max_trials=7,
+                       max_trials=6,
                        params=[{"name": "a", "parameterType": "double", "feasibleSpace": {"min": "0", "max": "10"}}],
                        extra_spec=yaml.safe_dump({
                            "objective": {"type": "minimize", "objectiveMetricName": "loss"},
-                           "algorithm": {"algorithmName": "grid"},
                            "earlyStopping": {"algorithmName": "medianstop", "algorithmSettings": [
                                {"name": "min_trials_required", "value": "2"}, {"name": "start_step", "value": "2"}]}}))
-    e.spec.parameters[0].feasible_space.step = "1"
     manager.create_experiment(e)
     done = manager.run_until_complete("medianstop", timeout=120)
     trials = sorted(manager.list_trials("medianstop"), key=lambda t: t.metadata.creation_timestamp)
     stopped = [t for t in trials if any(c.type == "EarlyStopped" and c.status == "True" for c in t.status.conditions)]
-    # grid order is 0,1,2,...: after 2 trials the rule is loss > mean(first two) -> later trials stop early
     assert stopped, [t.status.conditions for t in trials]
     assert all(t.spec.early_stopping_rules for t in stopped)
+    rule = stopped[0].spec.early_stopping_rules[0]
+    assert rule.name == "loss" and rule.comparison == "greater" and rule.start_step == 2
+    assert float(rule.value) == pytest.approx(0.505)  # mean of (0.005, 1.005)
     assert EC.is_succeeded(done)
     assert done.status.trials_early_stopped == len(stopped)
+    for t in stopped:  # stopped after start_step reports, long before the 12 steps end
+        assert len(manager.get_observation_log(t.metadata.name, "loss")) < 12
 
 
 def test_resume_long_running(manager):
