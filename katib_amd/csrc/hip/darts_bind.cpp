@@ -95,62 +95,107 @@ int pick_chunk(int C, int per_channel_floats, int fixed_floats) {
   return std::max(ch, 1);
 }
 
-void dwpw_fwd(Tensor x, Tensor dw, Tensor pw, int64_t K, int64_t dil, int64_t S, int64_t pad,
-              c10::optional<py::tuple> inbn, Tensor d, Tensor z, OptT stats, bool use_mfma) {
-  check_f32(x, "x"); check_f32(dw, "dw"); check_f32(pw, "pw"); check_f32(d, "d"); check_f32(z, "z");
-  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
-  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  const int Ho = z.size(2), Wo = z.size(3);
-  TORCH_CHECK(dw.numel() == C * K * K && pw.numel() == C * C, "weight shapes");
-  TORCH_CHECK(z.size(0) == N && z.size(1) == C && d.sizes() == z.sizes(), "output shapes");
-  TORCH_CHECK(64 % Wo == 0 && Ho % (64 / Wo) == 0, "tile constraint: 64 % Wo == 0 and Ho % (64/Wo) == 0");
-  TORCH_CHECK(C <= kMaxC, "C too large");
-  TORCH_CHECK(Ho == (H + 2 * pad - dil * (K - 1) - 1) / S + 1, "output height mismatch");
-  DwPwFwdArgs a{};
-  a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.pw = pw.data_ptr<float>();
-  a.d = d.data_ptr<float>(); a.z = z.data_ptr<float>(); a.stats = ptr_or_null<double>(stats);
-  if (a.stats) TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * C, "stats f64 [kRep][2C]");
-  a.N = N; a.C = C; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.pad = pad;
-  const int TR = 64 / Wo;
-  const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
-  a.chunk = pick_chunk(C, IR * IW, C * 64 + 4 * C);
-  a.use_mfma = (use_mfma && C % 16 == 0) ? 1 : 0;
-  bool prebn = inbn.has_value();
-  if (prebn) a.inbn = make_bn(*inbn, C);
-  launch_dwpw_fwd(a, K, dil, S, prebn, cur_stream());
+// ------------------------------------------------------------------------------------------------
+// Edge-batched entry points: `calls` is a list of per-edge argument tuples that share shapes;
+// one launch covers all of them (blockIdx.y = edge).
+// ------------------------------------------------------------------------------------------------
+template <typename Bt>
+void check_batch(const std::vector<py::tuple>& calls) {
+  TORCH_CHECK(!calls.empty() && (int)calls.size() <= Bt::kCap, "batch of 1..", Bt::kCap, " edges");
 }
 
-void pw_fwd(Tensor x, Tensor pw, Tensor z, OptT stats, int64_t co_off, int64_t S, int64_t off) {
-  check_f32(x, "x"); check_f32(pw, "pw"); check_f32(z, "z");
-  const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
-  const int Cout = pw.size(0), Ho = z.size(2), Wo = z.size(3);
-  TORCH_CHECK(pw.size(1) == Cin && co_off + Cout <= z.size(1) && z.size(0) == N, "pw shapes");
-  TORCH_CHECK((Ho * Wo) % 64 == 0, "Ho*Wo must be a multiple of 64");
-  TORCH_CHECK(Cin <= kMaxC && Cout <= kMaxC, "channels");
-  PwFwdArgs a{};
-  a.x = x.data_ptr<float>(); a.pw = pw.data_ptr<float>(); a.z = z.data_ptr<float>();
-  a.stats = ptr_or_null<double>(stats);
-  if (a.stats)
-    TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * z.size(1), "stats [kRep][2Ctot]");
-  a.N = N; a.Cin = Cin; a.Cout = Cout; a.CoutTotal = z.size(1); a.co_off = co_off;
-  a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off;
-  launch_pw_fwd(a, cur_stream());
-}
+#define SAME_SHAPE(b, fld) TORCH_CHECK(b.e[i].fld == b.e[0].fld, "edges in a batch must share " #fld)
 
-void pool_fwd(Tensor x, Tensor zavg, Tensor zmax, OptT sa, OptT sm, int64_t S, OptT amax) {
-  check_f32(x, "x"); check_f32(zavg, "zavg"); check_f32(zmax, "zmax");
-  PoolFwdArgs a{};
-  if (amax.has_value() && amax->defined()) {
-    TORCH_CHECK(amax->scalar_type() == at::kByte && amax->numel() == zmax.numel(), "amax must be uint8 like zmax");
-    a.amax = amax->data_ptr<uint8_t>();
+// (x, dw, pw, inbn|None, d, z, stats|None)
+void dwpw_fwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, int64_t pad, bool use_mfma) {
+  check_batch<DwPwFwdBatch>(calls);
+  DwPwFwdBatch bt{};
+  bt.n = calls.size();
+  bool prebn = false;
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    Tensor x = t[0].cast<Tensor>(), dw = t[1].cast<Tensor>(), pw = t[2].cast<Tensor>();
+    auto inbn = t[3].cast<c10::optional<py::tuple>>();
+    Tensor d = t[4].cast<Tensor>(), z = t[5].cast<Tensor>();
+    OptT stats = t[6].cast<OptT>();
+    check_f32(x, "x"); check_f32(dw, "dw"); check_f32(pw, "pw"); check_f32(d, "d"); check_f32(z, "z");
+    TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+    const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+    const int Ho = z.size(2), Wo = z.size(3);
+    TORCH_CHECK(dw.numel() == C * K * K && pw.numel() == C * C, "weight shapes");
+    TORCH_CHECK(z.size(0) == N && z.size(1) == C && d.sizes() == z.sizes(), "output shapes");
+    TORCH_CHECK(64 % Wo == 0 && Ho % (64 / Wo) == 0, "tile constraint: 64 % Wo == 0 and Ho % (64/Wo) == 0");
+    TORCH_CHECK(C <= kMaxC, "C too large");
+    TORCH_CHECK(Ho == (H + 2 * pad - dil * (K - 1) - 1) / S + 1, "output height mismatch");
+    DwPwFwdArgs& a = bt.e[i];
+    a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.pw = pw.data_ptr<float>();
+    a.d = d.data_ptr<float>(); a.z = z.data_ptr<float>(); a.stats = ptr_or_null<double>(stats);
+    if (a.stats) TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * C, "stats f64 [kRep][2C]");
+    a.N = N; a.C = C; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.pad = pad;
+    const int TR = 64 / Wo;
+    const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
+    a.chunk = pick_chunk(C, IR * IW, C * 64 + 4 * C);
+    a.use_mfma = (use_mfma && C % 16 == 0) ? 1 : 0;
+    if (i == 0) prebn = inbn.has_value();
+    TORCH_CHECK(inbn.has_value() == prebn, "edges in a batch must agree on the input BN");
+    if (prebn) a.inbn = make_bn(*inbn, C);
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
   }
-  a.x = x.data_ptr<float>(); a.zavg = zavg.data_ptr<float>(); a.zmax = zmax.data_ptr<float>();
-  a.stats_avg = ptr_or_null<double>(sa); a.stats_max = ptr_or_null<double>(sm);
-  if (a.stats_avg) TORCH_CHECK(sa->scalar_type() == at::kDouble && sa->numel() >= kRep * 2 * x.size(1), "stats");
-  if (a.stats_max) TORCH_CHECK(sm->scalar_type() == at::kDouble && sm->numel() >= kRep * 2 * x.size(1), "stats");
-  a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = zavg.size(2); a.Wo = zavg.size(3);
-  TORCH_CHECK(a.Ho == (a.H - 1) / S + 1 && zmax.sizes() == zavg.sizes(), "pool shapes");
-  launch_pool_fwd(a, S, cur_stream());
+  launch_dwpw_fwd(bt, K, dil, S, prebn, cur_stream());
+}
+
+// (x, pw, z, stats|None, co_off, off)
+void pw_fwd(std::vector<py::tuple> calls, int64_t S) {
+  check_batch<PwFwdBatch>(calls);
+  PwFwdBatch bt{};
+  bt.n = calls.size();
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    Tensor x = t[0].cast<Tensor>(), pw = t[1].cast<Tensor>(), z = t[2].cast<Tensor>();
+    OptT stats = t[3].cast<OptT>();
+    const int co_off = t[4].cast<int>(), off = t[5].cast<int>();
+    check_f32(x, "x"); check_f32(pw, "pw"); check_f32(z, "z");
+    const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+    const int Cout = pw.size(0), Ho = z.size(2), Wo = z.size(3);
+    TORCH_CHECK(pw.size(1) == Cin && co_off + Cout <= z.size(1) && z.size(0) == N, "pw shapes");
+    TORCH_CHECK((Ho * Wo) % 64 == 0, "Ho*Wo must be a multiple of 64");
+    TORCH_CHECK(Cin <= kMaxC && Cout <= kMaxC, "channels");
+    PwFwdArgs& a = bt.e[i];
+    a.x = x.data_ptr<float>(); a.pw = pw.data_ptr<float>(); a.z = z.data_ptr<float>();
+    a.stats = ptr_or_null<double>(stats);
+    if (a.stats)
+      TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * z.size(1), "stats [kRep][2Ctot]");
+    a.N = N; a.Cin = Cin; a.Cout = Cout; a.CoutTotal = z.size(1); a.co_off = co_off;
+    a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off;
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, Cin); SAME_SHAPE(bt, Cout); SAME_SHAPE(bt, Ho); SAME_SHAPE(bt, Wo);
+  }
+  launch_pw_fwd(bt, cur_stream());
+}
+
+// (x, zavg, zmax, stats_avg|None, stats_max|None, amax|None)
+void pool_fwd(std::vector<py::tuple> calls, int64_t S) {
+  check_batch<PoolFwdBatch>(calls);
+  PoolFwdBatch bt{};
+  bt.n = calls.size();
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    Tensor x = t[0].cast<Tensor>(), zavg = t[1].cast<Tensor>(), zmax = t[2].cast<Tensor>();
+    OptT sa = t[3].cast<OptT>(), sm = t[4].cast<OptT>(), amax = t[5].cast<OptT>();
+    check_f32(x, "x"); check_f32(zavg, "zavg"); check_f32(zmax, "zmax");
+    PoolFwdArgs& a = bt.e[i];
+    if (amax.has_value() && amax->defined()) {
+      TORCH_CHECK(amax->scalar_type() == at::kByte && amax->numel() == zmax.numel(), "amax must be uint8 like zmax");
+      a.amax = amax->data_ptr<uint8_t>();
+    }
+    a.x = x.data_ptr<float>(); a.zavg = zavg.data_ptr<float>(); a.zmax = zmax.data_ptr<float>();
+    a.stats_avg = ptr_or_null<double>(sa); a.stats_max = ptr_or_null<double>(sm);
+    if (a.stats_avg) TORCH_CHECK(sa->scalar_type() == at::kDouble && sa->numel() >= kRep * 2 * x.size(1), "stats");
+    if (a.stats_max) TORCH_CHECK(sm->scalar_type() == at::kDouble && sm->numel() >= kRep * 2 * x.size(1), "stats");
+    a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = zavg.size(2); a.Wo = zavg.size(3);
+    TORCH_CHECK(a.Ho == (a.H - 1) / S + 1 && zmax.sizes() == zavg.sizes(), "pool shapes");
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
+  }
+  launch_pool_fwd(bt, S, cur_stream());
 }
 
 void combine_fwd(std::vector<Tensor> zs, std::vector<py::tuple> bns, std::vector<int64_t> widx, OptT w,
@@ -180,33 +225,48 @@ void combine_fwd(std::vector<Tensor> zs, std::vector<py::tuple> bns, std::vector
   launch_combine_fwd(a, cur_stream());
 }
 
-void combine_bwd_reduce(Tensor dout, std::vector<Tensor> zs, std::vector<py::tuple> bns, OptT xid, Tensor red,
-                        std::vector<int64_t> widx, int64_t id_idx, OptT gw) {
-  check_f32(dout, "dout");
-  TORCH_CHECK(red.scalar_type() == at::kDouble, "red must be f64");
-  CombineBwdArgs a{};
-  a.N = dout.size(0); a.C = dout.size(1); a.HW = dout.size(2) * dout.size(3);
-  a.nops = zs.size();
-  a.rstride = (a.nops + 1) * a.C + 1;
-  TORCH_CHECK(a.nops <= kMaxOps && red.numel() >= (int64_t)kRep * a.rstride, "red size [kRep][(nops+1)C+1]");
-  for (int k = 0; k < a.nops; ++k) {
-    TORCH_CHECK(zs[k].sizes() == dout.sizes(), "z shape");
-    a.z[k] = zs[k].data_ptr<float>();
-    a.bn[k] = make_bn(bns[k], a.C);
-  }
-  a.dout = dout.data_ptr<float>(); a.xid = ptr_or_null<float>(xid); a.red = red.data_ptr<double>();
-  a.gw = ptr_or_null<double>(gw); a.id_idx = id_idx;
-  if (a.gw) {
-    TORCH_CHECK(gw->scalar_type() == at::kDouble && gw->numel() % kRep == 0, "gw must be f64 [kRep][nw]");
-    a.gwstride = gw->numel() / kRep;
-    TORCH_CHECK((int)widx.size() == a.nops, "widx per op");
+// (dout, zs, bns, xid|None, red, widx, id_idx, gw|None)
+void combine_bwd_reduce(std::vector<py::tuple> calls) {
+  check_batch<CombineBwdBatch>(calls);
+  CombineBwdBatch bt{};
+  bt.n = calls.size();
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    Tensor dout = t[0].cast<Tensor>();
+    auto zs = t[1].cast<std::vector<Tensor>>();
+    auto bns = t[2].cast<std::vector<py::tuple>>();
+    OptT xid = t[3].cast<OptT>();
+    Tensor red = t[4].cast<Tensor>();
+    auto widx = t[5].cast<std::vector<int64_t>>();
+    const int id_idx = t[6].cast<int>();
+    OptT gw = t[7].cast<OptT>();
+    check_f32(dout, "dout");
+    TORCH_CHECK(red.scalar_type() == at::kDouble, "red must be f64");
+    CombineBwdArgs& a = bt.e[i];
+    a.N = dout.size(0); a.C = dout.size(1); a.HW = dout.size(2) * dout.size(3);
+    a.nops = zs.size();
+    a.rstride = (a.nops + 1) * a.C + 1;
+    TORCH_CHECK(a.nops <= kMaxOps && red.numel() >= (int64_t)kRep * a.rstride, "red size [kRep][(nops+1)C+1]");
     for (int k = 0; k < a.nops; ++k) {
-      TORCH_CHECK(widx[k] >= 0 && widx[k] < a.gwstride, "widx out of range");
-      a.widx[k] = widx[k];
+      TORCH_CHECK(zs[k].sizes() == dout.sizes(), "z shape");
+      a.z[k] = zs[k].data_ptr<float>();
+      a.bn[k] = make_bn(bns[k], a.C);
     }
-    TORCH_CHECK(id_idx < a.gwstride, "id_idx out of range");
+    a.dout = dout.data_ptr<float>(); a.xid = ptr_or_null<float>(xid); a.red = red.data_ptr<double>();
+    a.gw = ptr_or_null<double>(gw); a.id_idx = id_idx;
+    if (a.gw) {
+      TORCH_CHECK(gw->scalar_type() == at::kDouble && gw->numel() % kRep == 0, "gw must be f64 [kRep][nw]");
+      a.gwstride = gw->numel() / kRep;
+      TORCH_CHECK((int)widx.size() == a.nops, "widx per op");
+      for (int k = 0; k < a.nops; ++k) {
+        TORCH_CHECK(widx[k] >= 0 && widx[k] < a.gwstride, "widx out of range");
+        a.widx[k] = widx[k];
+      }
+      TORCH_CHECK(id_idx < a.gwstride, "id_idx out of range");
+    }
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, HW);
   }
-  launch_combine_bwd_reduce(a, cur_stream());
+  launch_combine_bwd_reduce(bt, cur_stream());
 }
 
 // gW replica r lives gstride floats after replica 0 (gstride == 0: one accumulator)
@@ -218,71 +278,122 @@ void check_grad_sink(const OptT& gW, int64_t numel, int64_t gstride) {
               "gW replicas exceed their buffer");
 }
 
-void pw_bwd(py::tuple gs, Tensor pw, OptT ain, Tensor x, OptT dd, OptT gx, OptT gW, int64_t co_off,
-            int64_t S, int64_t off, int64_t mode, bool need_dx, int64_t gstride) {
-  check_f32(pw, "pw"); check_f32(x, "x");
-  PwBwdArgs a{};
-  const int Cout = pw.size(0), Cin = pw.size(1);
-  Tensor g = gs[0].cast<Tensor>();
-  a.N = g.size(0); a.CoutTotal = g.size(1); a.Ho = g.size(2); a.Wo = g.size(3);
-  a.gs = make_gs(gs, a.CoutTotal);
-  a.Cin = Cin; a.Cout = Cout; a.co_off = co_off; a.S = S; a.off = off; a.mode = mode;
-  a.need_dx = need_dx;
-  a.H = x.size(2); a.W = x.size(3);
-  TORCH_CHECK(Cin * Cout <= 4096, "pw_bwd supports Cin*Cout <= 4096");
-  TORCH_CHECK((a.Ho * a.Wo) % 64 == 0, "Ho*Wo % 64");
-  a.pw = pw.data_ptr<float>(); a.x = x.data_ptr<float>();
-  a.ain = ptr_or_null<float>(ain); a.dd = ptr_or_null<float>(dd); a.gx = ptr_or_null<float>(gx);
-  a.gW = ptr_or_null<float>(gW);
-  if (mode == 0) {
-    TORCH_CHECK(a.ain && (!need_dx || a.dd), "mode 0 needs ain (and dd)");
-  } else {
-    TORCH_CHECK(!need_dx || a.gx, "mode 1 needs gx");
+// (gs, pw, ain|None, x, dd|None, gx|None, gW|None, co_off, off, gstride)
+void pw_bwd(std::vector<py::tuple> calls, int64_t S, int64_t mode, bool need_dx) {
+  check_batch<PwBwdBatch>(calls);
+  PwBwdBatch bt{};
+  bt.n = calls.size();
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    py::tuple gs = t[0].cast<py::tuple>();
+    Tensor pw = t[1].cast<Tensor>();
+    OptT ain = t[2].cast<OptT>();
+    Tensor x = t[3].cast<Tensor>();
+    OptT dd = t[4].cast<OptT>(), gx = t[5].cast<OptT>(), gW = t[6].cast<OptT>();
+    const int co_off = t[7].cast<int>(), off = t[8].cast<int>();
+    const int64_t gstride = t[9].cast<int64_t>();
+    check_f32(pw, "pw"); check_f32(x, "x");
+    PwBwdArgs& a = bt.e[i];
+    const int Cout = pw.size(0), Cin = pw.size(1);
+    Tensor g = gs[0].cast<Tensor>();
+    a.N = g.size(0); a.CoutTotal = g.size(1); a.Ho = g.size(2); a.Wo = g.size(3);
+    a.gs = make_gs(gs, a.CoutTotal);
+    a.Cin = Cin; a.Cout = Cout; a.co_off = co_off; a.S = S; a.off = off; a.mode = mode;
+    a.need_dx = need_dx;
+    a.H = x.size(2); a.W = x.size(3);
+    TORCH_CHECK(Cin * Cout <= 4096, "pw_bwd supports Cin*Cout <= 4096");
+    TORCH_CHECK((a.Ho * a.Wo) % 64 == 0, "Ho*Wo % 64");
+    a.pw = pw.data_ptr<float>(); a.x = x.data_ptr<float>();
+    a.ain = ptr_or_null<float>(ain); a.dd = ptr_or_null<float>(dd); a.gx = ptr_or_null<float>(gx);
+    a.gW = ptr_or_null<float>(gW);
+    if (mode == 0) {
+      TORCH_CHECK(a.ain && (!need_dx || a.dd), "mode 0 needs ain (and dd)");
+    } else {
+      TORCH_CHECK(!need_dx || a.gx, "mode 1 needs gx");
+    }
+    check_grad_sink(gW, (int64_t)Cin * Cout, gstride);
+    a.gstride = gstride;
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, Cin); SAME_SHAPE(bt, Cout); SAME_SHAPE(bt, Ho); SAME_SHAPE(bt, Wo);
   }
-  check_grad_sink(gW, (int64_t)Cin * Cout, gstride);
-  a.gstride = gstride;
-  launch_pw_bwd(a, cur_stream());
+  launch_pw_bwd(bt, cur_stream());
 }
 
-void dw_bwd(Tensor x, c10::optional<py::tuple> inbn, Tensor dw, Tensor dd, Tensor gout, OptT gW, OptT red,
-            int64_t K, int64_t dil, int64_t S, int64_t pad, int64_t gstride) {
-  check_f32(x, "x"); check_f32(dw, "dw"); check_f32(dd, "dd"); check_f32(gout, "gout");
-  DwBwdArgs a{};
-  a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = dd.size(2); a.Wo = dd.size(3);
-  TORCH_CHECK(64 % a.Wo == 0 && a.Ho % (64 / a.Wo) == 0, "tile constraint");
-  TORCH_CHECK(a.H == a.Ho * S && a.W == a.Wo * S, "dw_bwd needs H == Ho*S");
-  TORCH_CHECK(gout.sizes() == x.sizes(), "gout shape");
-  a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.dd = dd.data_ptr<float>();
-  a.gout = gout.data_ptr<float>(); a.gW = ptr_or_null<float>(gW); a.red = ptr_or_null<double>(red);
-  check_grad_sink(gW, (int64_t)a.C * K * K, gstride);
-  a.gstride = gstride;
-  if (a.red) TORCH_CHECK(red->scalar_type() == at::kDouble && red->numel() >= kRep * 2 * a.C, "red [kRep][2C]");
-  a.pad = pad;
-  const int TR = 64 / a.Wo, r = (K - 1) / 2 * dil, h = (r + S - 1) / S, OR = TR + 2 * h;
-  const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (a.Wo - 1) * S + (K - 1) * dil + 1;
-  a.chunk = pick_chunk(a.C, OR * a.Wo + IR * IW, 4 * a.C + (a.gW ? a.C * (int)(K * K) : 0));
-  bool prebn = inbn.has_value();
-  if (prebn) a.inbn = make_bn(*inbn, a.C);
-  launch_dw_bwd(a, K, dil, S, prebn, cur_stream());
+// (x, inbn|None, dw, dd, gout, gW|None, red|None, gstride, overwrite)
+void dw_bwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, int64_t pad) {
+  check_batch<DwBwdBatch>(calls);
+  DwBwdBatch bt{};
+  bt.n = calls.size();
+  bool prebn = false, has_gw = false;
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    Tensor x = t[0].cast<Tensor>();
+    auto inbn = t[1].cast<c10::optional<py::tuple>>();
+    Tensor dw = t[2].cast<Tensor>(), dd = t[3].cast<Tensor>(), gout = t[4].cast<Tensor>();
+    OptT gW = t[5].cast<OptT>(), red = t[6].cast<OptT>();
+    const int64_t gstride = t[7].cast<int64_t>();
+    const bool overwrite = t[8].cast<bool>();
+    check_f32(x, "x"); check_f32(dw, "dw"); check_f32(dd, "dd"); check_f32(gout, "gout");
+    DwBwdArgs& a = bt.e[i];
+    a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = dd.size(2); a.Wo = dd.size(3);
+    TORCH_CHECK(64 % a.Wo == 0 && a.Ho % (64 / a.Wo) == 0, "tile constraint");
+    TORCH_CHECK(a.H == a.Ho * S && a.W == a.Wo * S, "dw_bwd needs H == Ho*S");
+    TORCH_CHECK(gout.sizes() == x.sizes(), "gout shape");
+    TORCH_CHECK(dw.numel() == a.C * K * K && dd.size(1) == a.C, "dw_bwd weight / grad shapes");
+    a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.dd = dd.data_ptr<float>();
+    a.gout = gout.data_ptr<float>(); a.gW = ptr_or_null<float>(gW); a.red = ptr_or_null<double>(red);
+    check_grad_sink(gW, (int64_t)a.C * K * K, gstride);
+    a.gstride = gstride;
+    a.overwrite = overwrite;
+    if (a.red) TORCH_CHECK(red->scalar_type() == at::kDouble && red->numel() >= kRep * 2 * a.C, "red [kRep][2C]");
+    a.pad = pad;
+    if (i == 0) {
+      prebn = inbn.has_value();
+      has_gw = a.gW != nullptr;
+    }
+    TORCH_CHECK(inbn.has_value() == prebn, "edges in a batch must agree on the input BN");
+    TORCH_CHECK((a.gW != nullptr) == has_gw, "edges in a batch must agree on weight-gradient sinks");
+    TORCH_CHECK(!(prebn && overwrite), "overwrite applies to the input-gradient (non-BN) form");
+    const int TR = 64 / a.Wo, r = (K - 1) / 2 * dil, h = (r + S - 1) / S, OR = TR + 2 * h;
+    const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (a.Wo - 1) * S + (K - 1) * dil + 1;
+    a.chunk = pick_chunk(a.C, OR * a.Wo + IR * IW, 4 * a.C + (a.gW ? a.C * (int)(K * K) : 0));
+    if (prebn) a.inbn = make_bn(*inbn, a.C);
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
+  }
+  launch_dw_bwd(bt, K, dil, S, prebn, cur_stream());
 }
 
-void pool_bwd(c10::optional<py::tuple> ga, c10::optional<py::tuple> gm, Tensor x, OptT dout_id, OptT w,
-              int64_t id_idx, Tensor gx, int64_t S, OptT amax) {
-  check_f32(x, "x"); check_f32(gx, "gx");
-  PoolBwdArgs a{};
-  a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3);
-  a.Ho = (a.H - 1) / S + 1; a.Wo = (a.W - 1) / S + 1;
-  TORCH_CHECK(a.Ho * a.Wo <= 8192, "pool_bwd stages one output plane in LDS (Ho*Wo <= 8192)");
-  TORCH_CHECK(gx.sizes() == x.sizes(), "gx shape");
-  TORCH_CHECK(!gm.has_value() || (amax.has_value() && amax->defined() && amax->scalar_type() == at::kByte &&
-                                  amax->numel() == (int64_t)a.N * a.C * a.Ho * a.Wo),
-              "max-pool backward needs the uint8 argmax from pool_fwd");
-  if (amax.has_value() && amax->defined()) a.amax = amax->data_ptr<uint8_t>();
-  if (ga.has_value()) a.ga = make_gs(*ga, a.C);
-  if (gm.has_value()) a.gm = make_gs(*gm, a.C);
-  a.x = x.data_ptr<float>(); a.dout_id = ptr_or_null<float>(dout_id); a.w = ptr_or_null<float>(w);
-  a.id_idx = id_idx; a.gx = gx.data_ptr<float>();
-  launch_pool_bwd(a, S, cur_stream());
+// (ga|None, gm|None, x, dout_id|None, w|None, id_idx, gx, amax|None, overwrite)
+void pool_bwd(std::vector<py::tuple> calls, int64_t S) {
+  check_batch<PoolBwdBatch>(calls);
+  PoolBwdBatch bt{};
+  bt.n = calls.size();
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    auto ga = t[0].cast<c10::optional<py::tuple>>(), gm = t[1].cast<c10::optional<py::tuple>>();
+    Tensor x = t[2].cast<Tensor>();
+    OptT dout_id = t[3].cast<OptT>(), w = t[4].cast<OptT>();
+    const int id_idx = t[5].cast<int>();
+    Tensor gx = t[6].cast<Tensor>();
+    OptT amax = t[7].cast<OptT>();
+    check_f32(x, "x"); check_f32(gx, "gx");
+    PoolBwdArgs& a = bt.e[i];
+    a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3);
+    a.Ho = (a.H - 1) / S + 1; a.Wo = (a.W - 1) / S + 1;
+    TORCH_CHECK(a.Ho * a.Wo <= 8192, "pool_bwd stages one output plane in LDS (Ho*Wo <= 8192)");
+    TORCH_CHECK(gx.sizes() == x.sizes(), "gx shape");
+    TORCH_CHECK(!gm.has_value() || (amax.has_value() && amax->defined() && amax->scalar_type() == at::kByte &&
+                                    amax->numel() == (int64_t)a.N * a.C * a.Ho * a.Wo),
+                "max-pool backward needs the uint8 argmax from pool_fwd");
+    if (amax.has_value() && amax->defined()) a.amax = amax->data_ptr<uint8_t>();
+    if (ga.has_value()) a.ga = make_gs(*ga, a.C);
+    if (gm.has_value()) a.gm = make_gs(*gm, a.C);
+    a.x = x.data_ptr<float>(); a.dout_id = ptr_or_null<float>(dout_id); a.w = ptr_or_null<float>(w);
+    if (a.dout_id) TORCH_CHECK(dout_id->sizes() == x.sizes(), "identity gradient shape");
+    a.id_idx = id_idx; a.gx = gx.data_ptr<float>();
+    a.overwrite = t[8].cast<bool>();
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
+  }
+  launch_pool_bwd(bt, S, cur_stream());
 }
 
 void fold_rows(Tensor buf) {

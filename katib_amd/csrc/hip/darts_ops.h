@@ -78,13 +78,14 @@ struct DwBwdArgs {
   const float* x; BNRef inbn; const float* dw; const float* dd; float* gout; float* gW; double* red;
   int gstride;  // floats between gW replicas (0: single accumulator); red: kRep replicas of [2C]
   int N, C, H, W, Ho, Wo, pad, chunk;
+  int overwrite;  // non-PREBN: gout = masked grad (first writer of this input gradient) instead of +=
 };
 
 struct FoldArgs {  // buf[0][i] = sum_r buf[r][i]; rows 1.. zeroed
   float* buf; int n; int rows;
 };
 
-constexpr int kMaxSeg = 16;
+constexpr int kMaxSeg = 64;
 struct FoldF64Args {  // per segment: p[i] = sum_{r < kRep} p[r*rstride + i]; replicas 1.. zeroed
   double* p[kMaxSeg]; int n[kMaxSeg]; int rstride[kMaxSeg]; int nseg; int total;
 };
@@ -92,17 +93,38 @@ struct FoldF64Args {  // per segment: p[i] = sum_{r < kRep} p[r*rstride + i]; re
 struct PoolBwdArgs {
   GradSrc ga; GradSrc gm; const float* x; const float* dout_id; const float* w; int id_idx; float* gx;
   const unsigned char* amax;
+  int overwrite;  // gx = result instead of +=
   int N, C, H, W, Ho, Wo;
 };
 
-void launch_dwpw_fwd(const DwPwFwdArgs& a, int K, int dil, int S, bool prebn, hipStream_t st);
-void launch_dw_bwd(const DwBwdArgs& a, int K, int dil, int S, bool prebn, hipStream_t st);
-void launch_pw_fwd(const PwFwdArgs& a, hipStream_t st);
-void launch_pool_fwd(const PoolFwdArgs& a, int S, hipStream_t st);
-void launch_pool_bwd(const PoolBwdArgs& a, int S, hipStream_t st);
+// Edge batches: one launch runs the same kernel for up to M edges of a DARTS node that share
+// shapes (blockIdx.y = edge). Passed by value in the kernarg segment (kept <= 4 KB).
+template <typename A, int M>
+struct Batch {
+  A e[M];
+  int n;
+  static constexpr int kCap = M;
+};
+using DwPwFwdBatch = Batch<DwPwFwdArgs, 8>;
+using PwFwdBatch = Batch<PwFwdArgs, 16>;
+using PoolFwdBatch = Batch<PoolFwdArgs, 8>;
+using CombineBwdBatch = Batch<CombineBwdArgs, 4>;
+using PwBwdBatch = Batch<PwBwdArgs, 8>;
+using DwBwdBatch = Batch<DwBwdArgs, 8>;
+using PoolBwdBatch = Batch<PoolBwdArgs, 8>;
+static_assert(sizeof(DwPwFwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096 && sizeof(PoolFwdBatch) <= 4096 &&
+                  sizeof(CombineBwdBatch) <= 4096 && sizeof(PwBwdBatch) <= 4096 && sizeof(DwBwdBatch) <= 4096 &&
+                  sizeof(PoolBwdBatch) <= 4096,
+              "kernel argument batches must fit the 4 KB kernarg budget");
+
+void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st);
+void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st);
+void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st);
+void launch_pool_fwd(const PoolFwdBatch& b, int S, hipStream_t st);
+void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st);
 void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st);
-void launch_combine_bwd_reduce(const CombineBwdArgs& a, hipStream_t st);
-void launch_pw_bwd(const PwBwdArgs& a, hipStream_t st);
+void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st);
+void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st);
 int max_blocks();
 void launch_fold_rows(const FoldArgs& a, hipStream_t st);
 void launch_fold_f64(const FoldF64Args& a, hipStream_t st);

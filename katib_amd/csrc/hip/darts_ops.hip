@@ -104,7 +104,8 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // grid: N * (Ho / TR) blocks, 256 threads. P = TR * Wo == 64 (host-enforced)
 // ------------------------------------------------------------------------------------------------
 template <int K, int DIL, int S, bool PREBN>
-__global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdArgs a) {
+__global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
+  const DwPwFwdArgs& a = bt.e[blockIdx.y];
   constexpr int P = 64;
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int TR = P / Wo;
@@ -225,7 +226,8 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdArgs a) {
 // pw_fwd: z[:, co_off + co] = pw . relu(x) at (oy*S + off, ox*S + off); StdConv / FR half
 // grid: N*Ho*Wo/64 blocks of 64-pixel tiles; Cin, Cout <= 256
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdArgs a) {
+__global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdBatch bt) {
+  const PwFwdArgs& a = bt.e[blockIdx.y];
   constexpr int P = 64;
   const int Cin = a.Cin, Cout = a.Cout, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int HWo = Ho * Wo;
@@ -273,7 +275,8 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdArgs a) {
 // pool_fwd: avg (count_include_pad=False) and max 3x3/pad 1, stride S. One block per (n, c) plane.
 // ------------------------------------------------------------------------------------------------
 template <int S>
-__global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdArgs a) {
+__global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdBatch bt) {
+  const PoolFwdArgs& a = bt.e[blockIdx.y];
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int c = blockIdx.x % C, g0 = blockIdx.x / C, G = gridDim.x / C;
   float sa = 0, sa2 = 0, sm = 0, sm2 = 0;
@@ -371,7 +374,8 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdArgs a) {
 // combine_bwd_reduce: S1[c] = sum dout, S2[k][c] = sum dout * zhat_k, Sid = sum dout * x
 // One block per (n, c) plane.
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdArgs a) {
+__global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdBatch bt) {
+  const CombineBwdArgs& a = bt.e[blockIdx.y];
   const int C = a.C, HW = a.HW;
   const int c = blockIdx.x % C, g0 = blockIdx.x / C, G = gridDim.x / C;
   __shared__ float sMean[kMaxOps], sInv[kMaxOps];
@@ -439,7 +443,8 @@ __device__ __forceinline__ float bn_bwd_val(const GradSrc& gs, size_t i, float m
 // grid: persistent over 64-pixel tiles; weight grads accumulated in registers across tiles.
 // ------------------------------------------------------------------------------------------------
 template <bool MFMA>
-__global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
+__global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
+  const PwBwdArgs& a = bt.e[blockIdx.y];
   constexpr int P = 64, PS = P + 1;  // padded LDS rows: per-channel row reads hit distinct banks
   const int Cin = a.Cin, Cout = a.Cout, Ho = a.Ho, Wo = a.Wo, HWo = Ho * Wo;
   const int ntiles = a.N * HWo / P;
@@ -601,7 +606,8 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
 // else  : input = x, act = relu -> gx += ga * (x > 0).
 // ------------------------------------------------------------------------------------------------
 template <int K, int DIL, int S, bool PREBN>
-__global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
+__global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
+  const DwBwdArgs& a = bt.e[blockIdx.y];
   constexpr int P = 64, KK = K * K;
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int TR = P / Wo;
@@ -721,7 +727,9 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
               }
             }
           } else if (ok) {
-            if (a.x[xi] > 0.f) a.gout[xi] += ga;
+            const float gm = a.x[xi] > 0.f ? ga : 0.f;
+            if (a.overwrite) a.gout[xi] = gm;
+            else if (gm != 0.f) a.gout[xi] += gm;
           }
         }
       }
@@ -738,7 +746,8 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdArgs a) {
 // pool_bwd: gx += avg^T(dz_avg) + max^T(dz_max) + wid * dout (identity skip), per (n,c) plane
 // ------------------------------------------------------------------------------------------------
 template <int S>
-__global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdArgs a) {
+__global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdBatch bt) {
+  const PoolBwdArgs& a = bt.e[blockIdx.y];
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, HWo = Ho * Wo;
   const int nc = blockIdx.x, c = nc % C;
   const size_t ob = (size_t)nc * HWo;
@@ -791,69 +800,79 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdArgs a) {
       }
     }
     if (a.dout_id) g += wid * a.dout_id[(size_t)nc * H * W + q];
-    a.gx[(size_t)nc * H * W + q] += g;
+    if (a.overwrite) a.gx[(size_t)nc * H * W + q] = g;
+    else a.gx[(size_t)nc * H * W + q] += g;
   }
 }
 
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
+static int per_edge_blocks(int tiles, int n) { return std::max(1, std::min(tiles, max_blocks() / std::max(n, 1))); }
+
 template <int K, int DIL, int S>
-static void launch_dwpw_fwd_t(const DwPwFwdArgs& a, bool prebn, hipStream_t st) {
+static void launch_dwpw_fwd_t(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
+  const DwPwFwdArgs& a = b.e[0];
   const int TR = 64 / a.Wo;
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
   size_t lds = sizeof(float) * (a.C * 64 + a.chunk * IR * IW + 4 * a.C);
-  dim3 grid(std::min(a.N * (a.Ho / TR), max_blocks()));
-  if (prebn) hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, a);
-  else hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, a);
+  dim3 grid(per_edge_blocks(a.N * (a.Ho / TR), b.n), b.n);
+  if (prebn) hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, b);
+  else hipLaunchKernelGGL((dwpw_fwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, b);
 }
 
-void launch_dwpw_fwd(const DwPwFwdArgs& a, int K, int dil, int S, bool prebn, hipStream_t st) {
+void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st) {
 #define DISPATCH(KK, DD, SS) \
-  if (K == KK && dil == DD && S == SS) return launch_dwpw_fwd_t<KK, DD, SS>(a, prebn, st);
+  if (K == KK && dil == DD && S == SS) return launch_dwpw_fwd_t<KK, DD, SS>(b, prebn, st);
   DISPATCH(3, 1, 1) DISPATCH(3, 1, 2) DISPATCH(5, 1, 1) DISPATCH(5, 1, 2)
   DISPATCH(3, 2, 1) DISPATCH(3, 2, 2) DISPATCH(5, 2, 1) DISPATCH(5, 2, 2)
 #undef DISPATCH
 }
 
 template <int K, int DIL, int S>
-static void launch_dw_bwd_t(const DwBwdArgs& a, bool prebn, hipStream_t st) {
+static void launch_dw_bwd_t(const DwBwdBatch& b, bool prebn, hipStream_t st) {
+  const DwBwdArgs& a = b.e[0];
   const int TR = 64 / a.Wo;
   const int r = (K - 1) / 2 * DIL, h = (r + S - 1) / S, OR = TR + 2 * h;
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
   size_t lds = sizeof(float) * (a.chunk * OR * a.Wo + a.chunk * IR * IW + 4 * a.C + (a.gW ? a.C * K * K : 0));
-  dim3 grid(std::min(a.N * (a.Ho / TR), max_blocks()));
-  if (prebn) hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, a);
-  else hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, a);
+  dim3 grid(per_edge_blocks(a.N * (a.Ho / TR), b.n), b.n);
+  if (prebn) hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, b);
+  else hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, b);
 }
 
-void launch_dw_bwd(const DwBwdArgs& a, int K, int dil, int S, bool prebn, hipStream_t st) {
+void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st) {
 #define DISPATCH(KK, DD, SS) \
-  if (K == KK && dil == DD && S == SS) return launch_dw_bwd_t<KK, DD, SS>(a, prebn, st);
+  if (K == KK && dil == DD && S == SS) return launch_dw_bwd_t<KK, DD, SS>(b, prebn, st);
   DISPATCH(3, 1, 1) DISPATCH(3, 1, 2) DISPATCH(5, 1, 1) DISPATCH(5, 1, 2)
   DISPATCH(3, 2, 1) DISPATCH(3, 2, 2) DISPATCH(5, 2, 1) DISPATCH(5, 2, 2)
 #undef DISPATCH
 }
 
-void launch_pw_fwd(const PwFwdArgs& a, hipStream_t st) {
+void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st) {
+  const PwFwdArgs& a = b.e[0];
   size_t lds = sizeof(float) * (a.Cin * 64 + 2 * a.Cout);
-  hipLaunchKernelGGL(pw_fwd_kernel, dim3(std::min(a.N * a.Ho * a.Wo / 64, max_blocks())), dim3(256), lds, st, a);
+  dim3 grid(per_edge_blocks(a.N * a.Ho * a.Wo / 64, b.n), b.n);
+  hipLaunchKernelGGL(pw_fwd_kernel, grid, dim3(256), lds, st, b);
 }
 
-static int channel_groups(int N, int C) { return std::max(1, std::min(N, max_blocks() / C)); }
+static int channel_groups(int N, int C, int n) { return std::max(1, std::min(N, max_blocks() / (C * std::max(n, 1)))); }
 
-void launch_pool_fwd(const PoolFwdArgs& a, int S, hipStream_t st) {
-  dim3 grid(a.C * channel_groups(a.N, a.C));
-  if (S == 1) hipLaunchKernelGGL(pool_fwd_kernel<1>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(pool_fwd_kernel<2>, grid, dim3(256), 0, st, a);
+void launch_pool_fwd(const PoolFwdBatch& b, int S, hipStream_t st) {
+  const PoolFwdArgs& a = b.e[0];
+  dim3 grid(a.C * channel_groups(a.N, a.C, b.n), b.n);
+  if (S == 1) hipLaunchKernelGGL(pool_fwd_kernel<1>, grid, dim3(256), 0, st, b);
+  else hipLaunchKernelGGL(pool_fwd_kernel<2>, grid, dim3(256), 0, st, b);
 }
 
-void launch_pool_bwd(const PoolBwdArgs& a, int S, hipStream_t st) {
+void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st) {
+  const PoolBwdArgs& a = b.e[0];
   size_t lds = sizeof(float) * 2 * a.Ho * a.Wo + a.Ho * a.Wo + 16;
-  if (S == 1) hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(a.N * a.C), dim3(256), lds, st, a);
-  else hipLaunchKernelGGL(pool_bwd_kernel<2>, dim3(a.N * a.C), dim3(256), lds, st, a);
+  dim3 grid(a.N * a.C, b.n);
+  if (S == 1) hipLaunchKernelGGL(pool_bwd_kernel<1>, grid, dim3(256), lds, st, b);
+  else hipLaunchKernelGGL(pool_bwd_kernel<2>, grid, dim3(256), lds, st, b);
 }
 
 void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st) {
@@ -862,17 +881,20 @@ void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(combine_fwd_kernel, dim3(blocks), dim3(256), 0, st, a);
 }
 
-void launch_combine_bwd_reduce(const CombineBwdArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(combine_bwd_reduce_kernel, dim3(a.C * channel_groups(a.N, a.C)), dim3(256), 0, st, a);
+void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st) {
+  const CombineBwdArgs& a = b.e[0];
+  hipLaunchKernelGGL(combine_bwd_reduce_kernel, dim3(a.C * channel_groups(a.N, a.C, b.n), b.n), dim3(256), 0, st,
+                     b);
 }
 
-void launch_pw_bwd(const PwBwdArgs& a, hipStream_t st) {
+void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st) {
+  const PwBwdArgs& a = b.e[0];
   int ntiles = a.N * a.Ho * a.Wo / 64;
-  int blocks = std::min(ntiles, max_blocks());
+  dim3 grid(per_edge_blocks(ntiles, b.n), b.n);
   size_t lds = sizeof(float) * (a.Cout * 65 + a.Cin * 65 + 4 * a.Cout + 4);
   const bool mfma = a.Cin % 16 == 0 && a.Cout % 16 == 0 && (a.Cin / 16) * (a.Cout / 16) <= 16;
-  if (mfma) hipLaunchKernelGGL(pw_bwd_kernel<true>, dim3(blocks), dim3(256), lds, st, a);
-  else hipLaunchKernelGGL(pw_bwd_kernel<false>, dim3(blocks), dim3(256), lds, st, a);
+  if (mfma) hipLaunchKernelGGL(pw_bwd_kernel<true>, grid, dim3(256), lds, st, b);
+  else hipLaunchKernelGGL(pw_bwd_kernel<false>, grid, dim3(256), lds, st, b);
 }
 
 

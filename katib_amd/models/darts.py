@@ -14,16 +14,17 @@ MI355X-first structure (not a translation of the module tree):
 * **Flat parameter storage.** All weights live in ONE fp32 buffer ``W`` (and the
   virtual weights in ``W'``); every parameter is a view. Gradients accumulate
   straight into flat gradient buffers (bucket views), so the virtual step, the
-  +/-eps Hessian perturbations, the global-norm clip and SGD are single fused
-  multi-tensor passes (``katib_amd.ops.multi_tensor``) and data parallelism is a
-  single RCCL all-reduce per gradient (``katib_amd.parallel``), not one per tensor.
+  +/-eps Hessian perturbations, the global-norm clip and SGD are whole-buffer ops
+  and data parallelism is a single RCCL all-reduce per gradient
+  (``katib_amd.parallel``), not one per tensor.
 * **Functional network.** ``forward(x, params, alphas)`` is a pure function of a
   parameter table, so the real and the virtual model share all code and the
   Hessian passes run with weights detached (no weight-gradient kernels).
-* **Fused edge kernels.** Each MixedOp edge runs through ``katib_amd.ops.darts``
-  whose HIP path computes the whole op group for an edge with LDS-staged tiles
-  (depthwise + pointwise + BN statistics) and accumulates the softmax-weighted
-  sum into the node buffer; the torch path is the numerics oracle.
+* **Fused, edge-batched kernels.** Each node (all its incoming MixedOp edges) runs
+  through ``katib_amd.ops.hip_darts.mixed_node``: every kernel type is launched once
+  for all edges that share a shape, with LDS-staged tiles (depthwise + pointwise on
+  MFMA + BN statistics) and the softmax-weighted sums accumulated into the node
+  output; the torch path (``katib_amd.ops.darts``) is the numerics oracle.
 * **Graph capture.** The complete search step (5 forward + 5 backward passes,
   optimizer math, all-reduces) is captured once into a HIP graph and replayed:
   at C=4..16 channels the step is launch-bound, so removing per-kernel host
@@ -276,13 +277,9 @@ class DartsNetwork:
             states = [t0, t1]
             ei = 0
             for n in range(L.N):
-                acc = None
-                for j in range(2 + n):
-                    e = cell["edges"][ei]
-                    ei += 1
-                    y = self.mixed_op(states[j], e, P, weights[n][j], bn, training)
-                    acc = y if acc is None else acc + y
-                states.append(acc)
+                edges = cell["edges"][ei:ei + 2 + n]
+                ei += 2 + n
+                states.append(self.mixed_node(states, edges, P, weights[n], bn, training))
             s0, s1 = s1, torch.cat(states[2:], dim=1)
         out = F.adaptive_avg_pool2d(s1, 1).flatten(1)
         return F.linear(out, P["classifier.weight"], P["classifier.bias"])
@@ -304,6 +301,25 @@ class DartsNetwork:
                 return hd.relu_conv_bn(x, w, rm, rv, training, self.momentum, self.eps)
             t = ops.relu_conv1x1(x, w)
         return F.batch_norm(t, rm, rv, None, None, training, self.momentum, self.eps)
+
+    def mixed_node(self, states, edges, P, w, bn, training):
+        """Node = sum over incoming edges of MixedOp (model.py:61-71). On the HIP backend all
+        edges of the node run as one edge-batched autograd Function."""
+        hd = self._hip(states[0], 1)
+        if hd is not None and all(hd.supported(states[e["src"]], e["stride"]) for e in edges):
+            specs, bnl, params = [], [], []
+            for e in edges:
+                spec, pnames, bn_names = self._edge_spec(hd, e)
+                specs.append(spec)
+                bnl.append([bn.get(nm) for nm in bn_names])
+                params.append([P[e["prefix"] + "." + nm] for nm in pnames])
+            return hd.mixed_node([states[e["src"]] for e in edges], [w[e["src"]] for e in edges], specs, bnl,
+                                 params, training, self.momentum, self.eps)
+        acc = None
+        for e in edges:
+            y = self.mixed_op(states[e["src"]], e, P, w[e["src"]], bn, training)
+            acc = y if acc is None else acc + y
+        return acc
 
     def mixed_op(self, x, e, P, w, bn, training):
         """sum_k w_k * op_k(x) (operations.py:164-180)."""

@@ -1,22 +1,26 @@
-"""Autograd wrappers over the HIP DARTS edge kernels (``katib_amd._hipkern``).
+"""Autograd wrappers over the HIP DARTS kernels (``katib_amd._hipkern``).
 
-:func:`mixed_edge` runs one whole MixedOp edge (reference
-``examples/v1beta1/trial-images/darts-cnn-cifar10/operations.py:164-180``) - all
-primitives, their BatchNorms and the softmax-weighted sum - as ~7 forward /
-~12 backward kernel launches (``csrc/hip/darts_ops.hip``):
+:func:`mixed_node` computes one DARTS node - the sum over its incoming edges of the
+MixedOp ``sum_k softmax(alpha)_k * op_k(x_j)`` (reference
+``examples/v1beta1/trial-images/darts-cnn-cifar10/operations.py:164-180`` and
+``model.py:61-71``) - with every kernel launched once for *all* edges of the node that
+share its shape (edge batches, ``blockIdx.y`` = edge):
 
-forward   dwpw_fwd x (sep stage 1, sep stage 2, dil3, dil5), pool_fwd (avg+max),
-          [pw_fwd x2 for the stride-2 skip], combine_fwd (weighted BN sum +
-          running-stat updates)
-backward  combine_bwd_reduce (BN-backward reductions + d softmax-weights),
-          pw_bwd/dw_bwd per conv stage, pool_bwd (+ identity skip)
+forward   dwpw_fwd per (kernel size, dilation, stride) [separable stage 1, dilated],
+          pool_fwd (avg + max + argmax), pw_fwd x2 (stride-2 skip = FactorizedReduce),
+          fold, dwpw_fwd with BN-apply prologue [separable stage 2], fold,
+          combine_fwd per edge accumulating into the node output (+ running-stat updates)
+backward  combine_bwd_reduce (BN-backward sums + d softmax-weights), fold, then pw_bwd /
+          dw_bwd / pool_bwd batches; every input gradient is written (not accumulated) by
+          its first kernel, so no memsets
 
 Cross-workgroup sums go to ``REP`` replicas of each accumulator (workgroup b adds
 into replica b % REP) so that no address sees more than grid/REP atomic adds; a
 ``fold_f64`` launch sums the replicas of BN statistics / BN-backward reductions
-into replica 0 before their consumers run (which then read one value). Weight gradients are accumulated by the kernels
-directly into each weight leaf's ``.grad`` when that is a row-0 view of a buffer
-registered with :func:`register_grad_replicas` (the flat gradient bucket of
+into replica 0 before their consumers run (which then read one value).
+Weight gradients are accumulated by the kernels directly into each weight leaf's
+``.grad`` when that is a row-0 view of a buffer registered with
+:func:`register_grad_replicas` (the flat gradient bucket of
 :class:`katib_amd.models.darts_search.DartsSearch`, folded once per backward pass
 with :func:`fold`), so no AccumulateGrad launches follow; detached weights (the
 Hessian passes) skip weight-gradient work. Callers that drive autograd with
@@ -31,6 +35,7 @@ from __future__ import annotations
 
 import importlib
 import weakref
+from collections import defaultdict
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -42,6 +47,8 @@ except ImportError as e:  # pragma: no cover - machines without the build
 
 F64 = torch.float64
 REP = int(_K.REP)
+_CAP = {"dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 8, "dw_bwd": 8,
+        "pool_bwd": 8}
 _REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
 
 
@@ -71,6 +78,14 @@ def _replica_stride(g: torch.Tensor) -> int:
     return 0
 
 
+def _launch(name: str, calls: List, *args):
+    """Run an edge-batched kernel over ``calls`` in chunks of its batch capacity."""
+    cap = _CAP[name]
+    fn = getattr(_K, name)
+    for i in range(0, len(calls), cap):
+        fn(calls[i:i + cap], *args)
+
+
 class EdgeSpec:
     """Static description of one edge: primitives, stride, parameter names, BN slots.
 
@@ -94,19 +109,13 @@ def _bn(stats: Optional[torch.Tensor], rm, rv, count: int, training: bool, eps: 
     return (None, rm, rv, 1.0 / count, True, eps, 1, 2 * C)
 
 
-def _fold_slots(stats, slot: int, idx, n: int):
-    segs = [(stats[i * slot:(i + 1) * slot], n, n) for i in idx]
-    if segs:
-        _K.fold_f64(segs)
-
-
 class _Sinks:
     """Weight-gradient destinations of one backward call."""
 
     def __init__(self):
         self.temps = []
 
-    def get(self, p: torch.Tensor, key: int):
+    def get(self, p: torch.Tensor, key):
         """(pointer tensor, replica stride): the leaf's registered replicated .grad, else
         a temporary [REP][numel] buffer summed in :meth:`finish`; (None, 0) when the
         weight does not require grad."""
@@ -130,205 +139,301 @@ class _Sinks:
                 grads[key] = s
 
 
-class _MixedEdge(torch.autograd.Function):
+class _Edge:
+    """Per-call state of one edge inside a node."""
+
+    def __init__(self, i, x, w, spec: EdgeSpec, bn, params):
+        self.i, self.x, self.w, self.spec, self.bn = i, x, w, spec, bn
+        self.P = dict(zip(spec.pnames, params))
+        self.S = spec.stride
+        self.refs = []
+        self.zs, self.bns, self.widx = {}, {}, []
+        self.saved = {}
+        self.id_idx, self.xid = -1, None
+        self.upd = []
+        self.id_done = False
+
+
+class _MixedNode(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, spec: EdgeSpec, bn, training, momentum, eps, *params):
-        S = spec.stride
-        x = x.contiguous()
-        N, C, H, W = x.shape
-        Ho, Wo = (H - 1) // S + 1, (W - 1) // S + 1
+    def forward(ctx, meta, *flat):
+        specs, bns, training, momentum, eps, nparams = meta
+        E = len(specs)
+        xs = [t.contiguous() for t in flat[:E]]
+        ws = flat[E:2 * E]
+        params = flat[2 * E:]
+        N, C = xs[0].shape[:2]
+        S0 = specs[0].stride
+        Ho = (xs[0].shape[2] - 1) // S0 + 1
+        Wo = (xs[0].shape[3] - 1) // S0 + 1
         cnt = N * Ho * Wo
-        P = dict(zip(spec.pnames, params))
-        dev = x.device
+        dev = xs[0].device
         slot = REP * 2 * C
-        stats = torch.zeros(max(spec.nbn, 1) * slot, dtype=F64, device=dev) if training else None
+        edges, off = [], 0
+        for i in range(E):
+            edges.append(_Edge(i, xs[i], ws[i], specs[i], bns[i], params[off:off + nparams[i]]))
+            off += nparams[i]
+        nslots = sum(e.spec.nbn for e in edges)
+        stats = torch.zeros(max(nslots, 1) * slot, dtype=F64, device=dev) if training else None
+        base = 0
+        for e in edges:
+            e.slot0 = base
+            e.refs = [_bn(stats[(base + i) * slot:(base + i + 1) * slot] if training else None, e.bn[i][0],
+                          e.bn[i][1], cnt, training, eps, C) for i in range(e.spec.nbn)]
+            base += e.spec.nbn
 
-        def st(i):
-            return stats[i * slot:(i + 1) * slot] if training else None
+        def st(e, i):
+            return stats[(e.slot0 + i) * slot:(e.slot0 + i + 1) * slot] if training else None
 
-        refs = [_bn(st(i), bn[i][0], bn[i][1], cnt, training, eps, C) for i in range(spec.nbn)]
-        zs, bns, widx, upd, saved = {}, {}, [], [], {}
-        id_idx, xid = -1, None
-        stage1, stage2 = [], []  # BN slots produced before / by the separable convs' second stage
-        for k, prim in enumerate(spec.prims):
-            if prim == "none":
-                continue
-            sl = spec.slots.get(prim, ())
-            if prim.startswith("separable_convolution"):
-                K = int(prim[-1])
-                d1 = torch.empty(N, C, Ho, Wo, device=dev)
-                z1 = torch.empty_like(d1)
-                _K.dwpw_fwd(x, P[prim + ".0.dw"], P[prim + ".0.pw"], K, 1, S, K // 2, None, d1, z1, st(sl[0]), True)
-                saved[prim] = [d1, z1]
-                stage1.append(sl[0])
-                stage2.append(sl[1])
-            elif prim.startswith("dilated_convolution"):
-                K = int(prim[-1])
-                d = torch.empty(N, C, Ho, Wo, device=dev)
-                z = torch.empty_like(d)
-                _K.dwpw_fwd(x, P[prim + ".dw"], P[prim + ".pw"], K, 2, S, (K // 2) * 2, None, d, z, st(sl[0]), True)
-                zs[k], bns[k] = z, refs[sl[0]]
-                saved[prim] = (d, z)
-                stage1.append(sl[0])
-            elif prim in ("avg_pooling_3x3", "max_pooling_3x3"):
-                if "pool" not in saved:
-                    za = torch.empty(N, C, Ho, Wo, device=dev)
-                    zm = torch.empty_like(za)
-                    am = torch.empty(N, C, Ho, Wo, dtype=torch.uint8, device=dev)
-                    sa = spec.slots.get("avg_pooling_3x3")
-                    sm = spec.slots.get("max_pooling_3x3")
-                    _K.pool_fwd(x, za, zm, st(sa[0]) if sa else None, st(sm[0]) if sm else None, S, am)
-                    saved["pool"] = (za, zm, am)
-                zs[k] = saved["pool"][0 if prim == "avg_pooling_3x3" else 1]
-                bns[k] = refs[sl[0]]
-                stage1.append(sl[0])
-            elif prim == "skip_connection":
-                if S == 1:
-                    id_idx, xid = k, x
+        def new():
+            return torch.empty(N, C, Ho, Wo, device=dev)
+
+        # ---- stage 1: grouped by (K, dilation, stride, pad)
+        dw_groups = defaultdict(list)
+        pool_groups = defaultdict(list)
+        fr_calls = []
+        stage1, stage2 = [], []
+        for e in edges:
+            for k, prim in enumerate(e.spec.prims):
+                if prim == "none":
                     continue
-                z = torch.empty(N, C, Ho, Wo, device=dev)
-                _K.pw_fwd(x, P[prim + ".conv1"], z, st(sl[0]), 0, 2, 0)
-                _K.pw_fwd(x, P[prim + ".conv2"], z, st(sl[0]), C // 2, 2, 1)
-                zs[k], bns[k] = z, refs[sl[0]]
-                saved[prim] = (z,)
-                stage1.append(sl[0])
-            else:
-                raise ValueError(prim)
-            widx.append(k)
-        if training:
-            _fold_slots(stats, slot, stage1, 2 * C)
-        for k, prim in enumerate(spec.prims):
-            if prim.startswith("separable_convolution"):
-                K = int(prim[-1])
-                sl = spec.slots[prim]
-                d1, z1 = saved[prim]
-                d2, z2 = torch.empty_like(d1), torch.empty_like(d1)
-                _K.dwpw_fwd(z1, P[prim + ".1.dw"], P[prim + ".1.pw"], K, 1, 1, K // 2, refs[sl[0]], d2, z2,
-                            st(sl[1]), True)
-                upd.append(refs[sl[0]])
-                zs[k], bns[k] = z2, refs[sl[1]]
-                saved[prim] = (d1, z1, d2, z2)
-        if training:
-            _fold_slots(stats, slot, stage2, 2 * C)
-        zs = [zs[k] for k in widx]
-        bns = [bns[k] for k in widx]
+                sl = e.spec.slots.get(prim, ())
+                if prim.startswith("separable_convolution"):
+                    K = int(prim[-1])
+                    d1, z1 = new(), new()
+                    dw_groups[(K, 1, e.S, K // 2)].append(
+                        (e.x, e.P[prim + ".0.dw"], e.P[prim + ".0.pw"], None, d1, z1, st(e, sl[0])))
+                    e.saved[prim] = [d1, z1]
+                    stage1.append(e.slot0 + sl[0])
+                    stage2.append(e.slot0 + sl[1])
+                elif prim.startswith("dilated_convolution"):
+                    K = int(prim[-1])
+                    d, z = new(), new()
+                    dw_groups[(K, 2, e.S, (K // 2) * 2)].append(
+                        (e.x, e.P[prim + ".dw"], e.P[prim + ".pw"], None, d, z, st(e, sl[0])))
+                    e.zs[k], e.bns[k] = z, e.refs[sl[0]]
+                    e.saved[prim] = (d, z)
+                    stage1.append(e.slot0 + sl[0])
+                elif prim in ("avg_pooling_3x3", "max_pooling_3x3"):
+                    if "pool" not in e.saved:
+                        za, zm = new(), new()
+                        am = torch.empty(N, C, Ho, Wo, dtype=torch.uint8, device=dev)
+                        sa = e.spec.slots.get("avg_pooling_3x3")
+                        sm = e.spec.slots.get("max_pooling_3x3")
+                        pool_groups[e.S].append((e.x, za, zm, st(e, sa[0]) if sa else None,
+                                                 st(e, sm[0]) if sm else None, am))
+                        e.saved["pool"] = (za, zm, am)
+                    e.zs[k] = e.saved["pool"][0 if prim == "avg_pooling_3x3" else 1]
+                    e.bns[k] = e.refs[sl[0]]
+                    stage1.append(e.slot0 + sl[0])
+                elif prim == "skip_connection":
+                    if e.S == 1:
+                        e.id_idx, e.xid = k, e.x
+                        continue
+                    z = new()
+                    fr_calls.append((e.x, e.P[prim + ".conv1"], z, st(e, sl[0]), 0, 0))
+                    fr_calls.append((e.x, e.P[prim + ".conv2"], z, st(e, sl[0]), C // 2, 1))
+                    e.zs[k], e.bns[k] = z, e.refs[sl[0]]
+                    e.saved[prim] = (z,)
+                    stage1.append(e.slot0 + sl[0])
+                else:
+                    raise ValueError(prim)
+                e.widx.append(k)
+        for (K, dil, S, pad), calls in dw_groups.items():
+            _launch("dwpw_fwd", calls, K, dil, S, pad, True)
+        for S, calls in pool_groups.items():
+            _launch("pool_fwd", calls, S)
+        if fr_calls:
+            _launch("pw_fwd", fr_calls, 2)
+        if training and stage1:
+            _K.fold_f64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage1))])
+        # ---- separable stage 2 (stride 1, input BN-apply prologue)
+        s2_groups = defaultdict(list)
+        for e in edges:
+            for k, prim in enumerate(e.spec.prims):
+                if prim.startswith("separable_convolution"):
+                    K = int(prim[-1])
+                    sl = e.spec.slots[prim]
+                    d1, z1 = e.saved[prim]
+                    d2, z2 = new(), new()
+                    s2_groups[K].append((z1, e.P[prim + ".1.dw"], e.P[prim + ".1.pw"], e.refs[sl[0]], d2, z2,
+                                         st(e, sl[1])))
+                    e.upd.append(e.refs[sl[0]])
+                    e.zs[k], e.bns[k] = z2, e.refs[sl[1]]
+                    e.saved[prim] = (d1, z1, d2, z2)
+        for K, calls in s2_groups.items():
+            _launch("dwpw_fwd", calls, K, 1, 1, K // 2, True)
+        if training and stage2:
+            _K.fold_f64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage2))])
+        # ---- weighted sums into the node output
         out = torch.empty(N, C, Ho, Wo, device=dev)
-        _K.combine_fwd(zs, bns, widx, w, id_idx, xid, None, None, out, momentum, training, False,
-                       upd if training else [])
-        ctx.spec = spec
-        ctx.meta = (saved, zs, bns, widx, id_idx, refs, training)
-        ctx.save_for_backward(x, w, *params)
+        for i, e in enumerate(edges):
+            e.zl = [e.zs[k] for k in e.widx]
+            e.bl = [e.bns[k] for k in e.widx]
+            _K.combine_fwd(e.zl, e.bl, e.widx, e.w, e.id_idx, e.xid, None, None, out, momentum, training, i > 0,
+                           e.upd if training else [])
+        ctx.meta = (edges, training, C)
+        ctx.save_for_backward(*flat)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, w, *params = ctx.saved_tensors
-        spec = ctx.spec
-        saved, zs, bns, widx, id_idx, refs, training = ctx.meta
-        S = spec.stride
-        P = dict(zip(spec.pnames, params))
-        N, C, H, W = x.shape
-        dev = x.device
+        flat = ctx.saved_tensors
+        edges, training, C = ctx.meta
+        E = len(edges)
         dout = dout.contiguous()
-        nops = len(zs)
-        nred = (nops + 1) * C + 1
-        nw = w.numel()
-        buf = torch.zeros(REP * (nred + nw), dtype=F64, device=dev)
-        red, gw_rep = buf[:REP * nred], buf[REP * nred:]
-        _K.combine_bwd_reduce(dout, zs, bns, x if id_idx >= 0 else None, red, widx, id_idx, gw_rep)
-        _K.fold_f64([(red, nred, nred), (gw_rep, nw, nw)])
-        S1 = red[:C]
-        jpos = {k: j for j, k in enumerate(widx)}
-
-        def src(k, z):  # GradSrc of a weighted, BN'd op output
-            j = jpos[k]
-            return (dout, z, S1, red[(1 + j) * C:(2 + j) * C], bns[j], w, k, 1, nred)
-
-        need_x = ctx.needs_input_grad[0]
-        gx = torch.zeros_like(x) if need_x else None
-        scratch = None
+        dev = dout.device
         sinks = _Sinks()
+        pbase, acc = [], 2 * E
+        for e in edges:
+            pbase.append(acc)
+            acc += len(e.spec.pnames)
 
-        def sink(name):
-            return sinks.get(P[name], spec.pidx[name])
+        def sink(e, name):
+            return sinks.get(e.P[name], pbase[e.i] + e.spec.pidx[name])
 
-        # separable convs: both second stages first, one fold of their BN-backward sums, then stage 1
-        seps = [(k, p) for k, p in enumerate(spec.prims) if p.startswith("separable_convolution")]
-        red1 = torch.zeros(max(len(seps), 1) * REP * 2 * C, dtype=F64, device=dev) if training else None
-        stage_grad = {}
-        for i, (k, prim) in enumerate(seps):
-            K = int(prim[-1])
-            d1, z1, d2, z2 = saved[prim]
-            b1 = refs[spec.slots[prim][0]]
-            dd2 = torch.empty_like(d2)
-            gp, gst = sink(prim + ".1.pw")
-            _K.pw_bwd(src(k, z2), P[prim + ".1.pw"], d2, z1, dd2, None, gp, 0, 1, 0, 0, True, gst)
-            g1 = torch.empty_like(z1)
-            r1 = red1[i * REP * 2 * C:(i + 1) * REP * 2 * C] if training else None
-            gp, gst = sink(prim + ".1.dw")
-            _K.dw_bwd(z1, b1, P[prim + ".1.dw"], dd2, g1, gp, r1, K, 1, 1, K // 2, gst)
-            stage_grad[prim] = (g1, r1, b1)
-        if training and seps:
-            _K.fold_f64([(red1[i * REP * 2 * C:(i + 1) * REP * 2 * C], 2 * C, 2 * C) for i in range(len(seps))])
-        pool_done = False
-        for k, prim in enumerate(spec.prims):
-            if prim == "none":
-                continue
-            if prim.startswith("separable_convolution"):
+        # ---- BN-backward sums and d(alpha) for every edge, one fold
+        sizes = []
+        for e in edges:
+            e.nred = (len(e.zl) + 1) * C + 1
+            sizes.append(REP * (e.nred + e.w.numel()))
+        buf = torch.zeros(sum(sizes), dtype=F64, device=dev)
+        o = 0
+        calls, segs = [], []
+        for e, sz in zip(edges, sizes):
+            e.red = buf[o:o + REP * e.nred]
+            e.gw = buf[o + REP * e.nred:o + sz]
+            o += sz
+            calls.append((dout, e.zl, e.bl, e.x if e.id_idx >= 0 else None, e.red, e.widx, e.id_idx, e.gw))
+            segs += [(e.red, e.nred, e.nred), (e.gw, e.w.numel(), e.w.numel())]
+        _launch("combine_bwd_reduce", calls)
+        _K.fold_f64(segs)
+
+        def src(e, k, z):  # GradSrc of a weighted, BN'd op output
+            j = e.widx.index(k)
+            return (dout, z, e.red[:C], e.red[(1 + j) * C:(2 + j) * C], e.bl[j], e.w, k, 1, e.nred)
+
+        gxs = [torch.empty_like(e.x) for e in edges]
+        first = [True] * E  # the first kernel writing gx[e] overwrites it
+
+        def take_first(i):
+            f = first[i]
+            first[i] = False
+            return f
+
+        # ---- separable convs: both second stages, one fold, both first stages
+        seps = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("separable_convolution")]
+        if seps:
+            red1 = torch.zeros(len(seps) * REP * 2 * C, dtype=F64, device=dev) if training else None
+            pw2, dw2 = [], defaultdict(list)
+            for n, (e, k, prim) in enumerate(seps):
                 K = int(prim[-1])
-                pad = K // 2
-                d1, z1, d2, z2 = saved[prim]
-                g1, r1, b1 = stage_grad[prim]
+                d1, z1, d2, z2 = e.saved[prim]
+                dd2 = torch.empty_like(d2)
+                g, gst = sink(e, prim + ".1.pw")
+                pw2.append((src(e, k, z2), e.P[prim + ".1.pw"], d2, z1, dd2, None, g, 0, 0, gst))
+                g1 = torch.empty_like(z1)
+                r1 = red1[n * REP * 2 * C:(n + 1) * REP * 2 * C] if training else None
+                g, gst = sink(e, prim + ".1.dw")
+                dw2[K].append((z1, e.refs[e.spec.slots[prim][0]], e.P[prim + ".1.dw"], dd2, g1, g, r1, gst, False))
+                e.saved[prim + "/g1"] = (g1, r1)
+            _launch("pw_bwd", pw2, 1, 0, True)
+            for K, calls in dw2.items():
+                _launch("dw_bwd", calls, K, 1, 1, K // 2)
+            if training:
+                _K.fold_f64([(red1[n * REP * 2 * C:(n + 1) * REP * 2 * C], 2 * C, 2 * C) for n in range(len(seps))])
+            pw1, dw1 = [], defaultdict(list)
+            for e, k, prim in seps:
+                K = int(prim[-1])
+                d1, z1, d2, z2 = e.saved[prim]
+                g1, r1 = e.saved[prim + "/g1"]
+                b1 = e.refs[e.spec.slots[prim][0]]
                 gs1 = (g1, z1, r1[:C] if training else None, r1[C:2 * C] if training else None, b1, None, 0, 1, 2 * C)
                 dd1 = torch.empty_like(d1)
-                gp, gst = sink(prim + ".0.pw")
-                _K.pw_bwd(gs1, P[prim + ".0.pw"], d1, x, dd1, None, gp, 0, 1, 0, 0, True, gst)
-                if not need_x and scratch is None:
-                    scratch = torch.empty_like(x)
-                gp, gst = sink(prim + ".0.dw")
-                _K.dw_bwd(x, None, P[prim + ".0.dw"], dd1, gx if need_x else scratch, gp, None, K, 1, S, pad, gst)
-            elif prim.startswith("dilated_convolution"):
+                g, gst = sink(e, prim + ".0.pw")
+                pw1.append((gs1, e.P[prim + ".0.pw"], d1, e.x, dd1, None, g, 0, 0, gst))
+                g, gst = sink(e, prim + ".0.dw")
+                dw1[(K, e.S)].append((e.x, None, e.P[prim + ".0.dw"], dd1, gxs[e.i], g, None, gst, take_first(e.i)))
+            _launch("pw_bwd", pw1, 1, 0, True)
+            for (K, S), calls in dw1.items():
+                _launch("dw_bwd", calls, K, 1, S, K // 2)
+        # ---- dilated convs
+        dils = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("dilated_convolution")]
+        if dils:
+            pwd, dwd = [], defaultdict(list)
+            for e, k, prim in dils:
                 K = int(prim[-1])
-                d, z = saved[prim]
+                d, z = e.saved[prim]
                 dd = torch.empty_like(d)
-                gp, gst = sink(prim + ".pw")
-                _K.pw_bwd(src(k, z), P[prim + ".pw"], d, x, dd, None, gp, 0, 1, 0, 0, True, gst)
-                if not need_x and scratch is None:
-                    scratch = torch.empty_like(x)
-                gp, gst = sink(prim + ".dw")
-                _K.dw_bwd(x, None, P[prim + ".dw"], dd, gx if need_x else scratch, gp, None, K, 2, S, (K // 2) * 2,
-                          gst)
-            elif prim in ("avg_pooling_3x3", "max_pooling_3x3"):
-                if pool_done or not need_x:
-                    continue
-                pool_done = True
-                za, zm, am = saved["pool"]
-                ga = gm = None
-                for kk, pp in enumerate(spec.prims):
-                    if pp == "avg_pooling_3x3":
-                        ga = src(kk, za)
-                    elif pp == "max_pooling_3x3":
-                        gm = src(kk, zm)
-                _K.pool_bwd(ga, gm, x, dout if id_idx >= 0 else None, w, id_idx, gx, S, am)
-            elif prim == "skip_connection" and S != 1:
-                (z,) = saved[prim]
-                gs = src(k, z)
-                gp, gst = sink(prim + ".conv1")
-                _K.pw_bwd(gs, P[prim + ".conv1"], None, x, None, gx, gp, 0, 2, 0, 1, need_x, gst)
-                gp, gst = sink(prim + ".conv2")
-                _K.pw_bwd(gs, P[prim + ".conv2"], None, x, None, gx, gp, C // 2, 2, 1, 1, need_x, gst)
-        if need_x and id_idx >= 0 and not pool_done:
-            gx.add_(dout * w[id_idx])
-        grads = [None] * len(params)
+                g, gst = sink(e, prim + ".pw")
+                pwd.append((src(e, k, z), e.P[prim + ".pw"], d, e.x, dd, None, g, 0, 0, gst))
+                g, gst = sink(e, prim + ".dw")
+                dwd[(K, e.S)].append((e.x, None, e.P[prim + ".dw"], dd, gxs[e.i], g, None, gst, take_first(e.i)))
+            _launch("pw_bwd", pwd, 1, 0, True)
+            for (K, S), calls in dwd.items():
+                _launch("dw_bwd", calls, K, 2, S, (K // 2) * 2)
+        # ---- pools (+ the identity skip of stride-1 edges)
+        pools = defaultdict(list)
+        for e in edges:
+            if "pool" not in e.saved:
+                continue
+            za, zm, am = e.saved["pool"]
+            ga = gm = None
+            for k, p in enumerate(e.spec.prims):
+                if p == "avg_pooling_3x3":
+                    ga = src(e, k, za)
+                elif p == "max_pooling_3x3":
+                    gm = src(e, k, zm)
+            pools[e.S].append((ga, gm, e.x, dout if e.id_idx >= 0 else None, e.w, e.id_idx, gxs[e.i], am,
+                               take_first(e.i)))
+            e.id_done = True
+        for S, calls in pools.items():
+            _launch("pool_bwd", calls, S)
+        for e in edges:
+            if e.id_idx >= 0 and not e.id_done:
+                if take_first(e.i):
+                    torch.mul(dout, e.w[e.id_idx], out=gxs[e.i])
+                else:
+                    gxs[e.i].add_(dout * e.w[e.id_idx])
+        # ---- stride-2 skip (FactorizedReduce): scattered adds, so its gx must exist already
+        frc = []
+        for e in edges:
+            if "skip_connection" in e.saved:
+                if take_first(e.i):
+                    gxs[e.i].zero_()
+                k = e.spec.prims.index("skip_connection")
+                (z,) = e.saved["skip_connection"]
+                gs = src(e, k, z)
+                g, gst = sink(e, "skip_connection.conv1")
+                frc.append((gs, e.P["skip_connection.conv1"], None, e.x, None, gxs[e.i], g, 0, 0, gst))
+                g, gst = sink(e, "skip_connection.conv2")
+                frc.append((gs, e.P["skip_connection.conv2"], None, e.x, None, gxs[e.i], g, C // 2, 1, gst))
+        if frc:
+            _launch("pw_bwd", frc, 2, 1, True)
+        for i in range(E):
+            if first[i]:  # an edge whose only primitive is "none"
+                gxs[i].zero_()
+        grads = [None] * len(flat)
+        for i, e in enumerate(edges):
+            grads[i] = gxs[i] if ctx.needs_input_grad[1 + i] else None
+            grads[E + i] = e.gw[:e.w.numel()].to(e.w.dtype) if ctx.needs_input_grad[1 + E + i] else None
         sinks.finish(grads)
-        gw_out = gw_rep[:nw].to(w.dtype) if ctx.needs_input_grad[1] else None
-        return (gx, gw_out, None, None, None, None, None, *grads)
+        return (None, *grads)
+
+
+def mixed_node(xs: Sequence[torch.Tensor], ws: Sequence[torch.Tensor], specs: Sequence[EdgeSpec],
+               bns: Sequence[List[Tuple[torch.Tensor, torch.Tensor]]], params: Sequence[Sequence[torch.Tensor]],
+               training: bool, momentum: float = 0.1, eps: float = 1e-5):
+    """sum over edges e of sum_k ws[e]_k * op_k(xs[e]); ``params[e]`` ordered as ``specs[e].pnames``."""
+    meta = (list(specs), list(bns), training, momentum, eps, [len(p) for p in params])
+    flat = list(xs) + list(ws) + [p for ps in params for p in ps]
+    return _MixedNode.apply(meta, *flat)
 
 
 def mixed_edge(x, w, spec: EdgeSpec, bn: List[Tuple[torch.Tensor, torch.Tensor]], params: Sequence[torch.Tensor],
                training: bool, momentum: float = 0.1, eps: float = 1e-5):
-    """sum_k w_k * op_k(x) for one edge; ``params`` ordered as ``spec.pnames``."""
-    return _MixedEdge.apply(x, w, spec, bn, training, momentum, eps, *params)
+    """sum_k w_k * op_k(x) for one edge (a node with a single incoming edge)."""
+    return mixed_node([x], [w], [spec], [bn], [params], training, momentum, eps)
 
 
 # --------------------------------------------------------------------------------- preprocess
@@ -347,10 +452,9 @@ class _StdConvBN(torch.autograd.Function):
         stats = torch.zeros(REP * 2 * Cout, dtype=F64, device=x.device) if training else None
         z = torch.empty(N, Cout, Ho, Wo, device=x.device)
         if fr:
-            _K.pw_fwd(x, w1, z, stats, 0, 2, 0)
-            _K.pw_fwd(x, w2, z, stats, Cout // 2, 2, 1)
+            _K.pw_fwd([(x, w1, z, stats, 0, 0), (x, w2, z, stats, Cout // 2, 1)], 2)
         else:
-            _K.pw_fwd(x, w1, z, stats, 0, 1, 0)
+            _K.pw_fwd([(x, w1, z, stats, 0, 0)], 1)
         if training:
             _K.fold_f64([(stats, 2 * Cout, 2 * Cout)])
         bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
@@ -369,7 +473,7 @@ class _StdConvBN(torch.autograd.Function):
         nred = 2 * Cout + 1
         red = torch.zeros(REP * nred, dtype=F64, device=x.device)
         if training:
-            _K.combine_bwd_reduce(dout, [z], [bn], None, red, [0], -1, None)
+            _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
             _K.fold_f64([(red, nred, nred)])
         gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0, 1, nred)
         need_x = ctx.needs_input_grad[0]
@@ -379,10 +483,10 @@ class _StdConvBN(torch.autograd.Function):
         g1, s1 = sinks.get(w1, 1)
         if fr:
             g2, s2 = sinks.get(w2, 2)
-            _K.pw_bwd(gs, w1, None, x, None, gx, g1, 0, 2, 0, 1, need_x, s1)
-            _K.pw_bwd(gs, w2, None, x, None, gx, g2, Cout // 2, 2, 1, 1, need_x, s2)
+            _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1), (gs, w2, None, x, None, gx, g2, Cout // 2, 1, s2)],
+                      2, 1, need_x)
         else:
-            _K.pw_bwd(gs, w1, None, x, None, gx, g1, 0, 1, 0, 1, need_x, s1)
+            _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1)], 1, 1, need_x)
         sinks.finish(grads)
         return gx, None, None, None, None, None, grads[1], grads[2]
 

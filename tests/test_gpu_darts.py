@@ -154,3 +154,50 @@ def test_search_step_matches_torch(capture):
     assert abs(lt[1] - lh[1]) < 1e-3 * max(1.0, abs(lt[1]))
     _close(Wh, Wt, "W", rtol=1e-3, atol=1e-4)
     _close(Ah, At, "alpha", rtol=5e-2, atol=5e-5)
+
+
+@pytest.mark.parametrize("C,cell_idx,node", [(4, 0, 1), (8, 1, 1), (16, 0, 2), (8, 1, 2)])
+def test_mixed_node_matches_torch(C, cell_idx, node):
+    """All edges of a node in one edge-batched Function (mixed strides in reduction cells)."""
+    from katib_amd.models.darts import DartsNetwork
+    from katib_amd.ops import darts as dops
+
+    layout, W, dev, BNState = _setup(C, N=3)
+    cell = layout.cells[cell_idx]
+    edges = [e for e in cell["edges"] if e["node"] == node]
+    Cc = cell["C"]
+    gen = torch.Generator(device=dev).manual_seed(9)
+    H = 32
+    states = []
+    for j in range(2 + node):
+        h = H if (j < 2 or not cell["reduction"]) else H // 2
+        states.append(torch.randn(8, Cc, h, h, device=dev, generator=gen))
+    w = torch.softmax(torch.randn(2 + node, len(layout.prims), device=dev, generator=gen), -1)
+    Ho = H // 2 if cell["reduction"] else H
+    R = torch.randn(8, Cc, Ho, Ho, device=dev, generator=gen)
+    res = []
+    for backend in ("torch", "hip"):
+        dops.set_backend(backend)
+        net = DartsNetwork(layout)
+        Wl = W.clone()
+        gW = torch.zeros_like(Wl)
+        P, G = layout.views(Wl), layout.views(gW)
+        for k, v in P.items():
+            v.requires_grad_(True)
+            v.grad = G[k]
+        bn = BNState(layout, dev)
+        xs = [s.clone().requires_grad_(True) for s in states]
+        wl = w.clone().requires_grad_(True)
+        out = net.mixed_node(xs, edges, P, wl, bn, True)
+        (out * R).sum().backward(inputs=xs + [wl] + list(P.values()))
+        torch.cuda.synchronize()
+        res.append((out.detach(), [x.grad for x in xs], wl.grad, gW, bn.mean.clone(), bn.var.clone()))
+    dops.set_backend("torch")
+    (o_t, gx_t, gw_t, gW_t, m_t, v_t), (o_h, gx_h, gw_h, gW_h, m_h, v_h) = res
+    _close(o_h, o_t, "out", rtol=1e-3, atol=1e-4)
+    for i, (a, b) in enumerate(zip(gx_h, gx_t)):
+        _close(a, b, "dx[%d]" % i, rtol=1e-3, atol=1e-4)
+    _close(gw_h, gw_t, "dalpha", rtol=1e-3, atol=1e-4)
+    _close(gW_h, gW_t, "dW", rtol=1e-3, atol=1e-4)
+    _close(m_h, m_t, "running_mean", rtol=1e-3, atol=1e-5)
+    _close(v_h, v_t, "running_var", rtol=1e-3, atol=1e-5)
