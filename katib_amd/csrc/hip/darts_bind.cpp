@@ -198,31 +198,46 @@ void pool_fwd(std::vector<py::tuple> calls, int64_t S) {
   launch_pool_fwd(bt, S, cur_stream());
 }
 
-void combine_fwd(std::vector<Tensor> zs, std::vector<py::tuple> bns, std::vector<int64_t> widx, OptT w,
-                 int64_t id_idx, OptT xid, OptT gamma, OptT beta, Tensor out, double momentum, bool update_running,
-                 bool accumulate, std::vector<py::tuple> upd) {
+// calls: per edge (zs, bns, widx, w|None, id_idx, xid|None, upd); all edges summed into `out`
+void combine_fwd(std::vector<py::tuple> calls, OptT gamma, OptT beta, Tensor out, double momentum,
+                 bool update_running, bool accumulate) {
   check_f32(out, "out");
-  TORCH_CHECK(zs.size() == bns.size() && zs.size() == widx.size() && (int)zs.size() <= kMaxOps, "ops");
-  CombineFwdArgs a{};
-  a.N = out.size(0); a.C = out.size(1); a.HW = out.size(2) * out.size(3);
-  TORCH_CHECK(a.C <= kMaxC, "C too large");
-  a.nops = zs.size();
-  for (size_t k = 0; k < zs.size(); ++k) {
-    check_f32(zs[k], "z");
-    TORCH_CHECK(zs[k].sizes() == out.sizes(), "combine input shape");
-    a.z[k] = zs[k].data_ptr<float>();
-    a.bn[k] = make_bn(bns[k], a.C);
-    a.widx[k] = widx[k];
+  check_batch<CombineFwdBatch>(calls);
+  CombineFwdBatch bt{};
+  bt.n = calls.size();
+  const int C = out.size(1);
+  TORCH_CHECK(C <= kMaxC, "C too large");
+  TORCH_CHECK((int64_t)2 * bt.n * kMaxOps * C * 4 <= 65536, "combine LDS budget exceeded");
+  for (int e = 0; e < bt.n; ++e) {
+    const py::tuple& t = calls[e];
+    auto zs = t[0].cast<std::vector<Tensor>>();
+    auto bns = t[1].cast<std::vector<py::tuple>>();
+    auto widx = t[2].cast<std::vector<int64_t>>();
+    OptT w = t[3].cast<OptT>();
+    const int id_idx = t[4].cast<int>();
+    OptT xid = t[5].cast<OptT>();
+    auto upd = t[6].cast<std::vector<py::tuple>>();
+    TORCH_CHECK(zs.size() == bns.size() && zs.size() == widx.size() && (int)zs.size() <= kMaxOps, "ops");
+    CombineFwdArgs& a = bt.e[e];
+    a.N = out.size(0); a.C = C; a.HW = out.size(2) * out.size(3);
+    a.nops = zs.size();
+    for (size_t k = 0; k < zs.size(); ++k) {
+      check_f32(zs[k], "z");
+      TORCH_CHECK(zs[k].sizes() == out.sizes(), "combine input shape");
+      a.z[k] = zs[k].data_ptr<float>();
+      a.bn[k] = make_bn(bns[k], C);
+      a.widx[k] = widx[k];
+    }
+    TORCH_CHECK((int)upd.size() <= kMaxOps, "too many update-only BN layers");
+    a.nupd = upd.size();
+    for (size_t k = 0; k < upd.size(); ++k) a.upd[k] = make_bn(upd[k], C);
+    a.w = ptr_or_null<float>(w); a.id_idx = id_idx; a.xid = ptr_or_null<float>(xid);
+    if (a.xid) TORCH_CHECK(xid->sizes() == out.sizes(), "identity shape");
+    a.gamma = ptr_or_null<float>(gamma); a.beta = ptr_or_null<float>(beta);
+    a.out = out.data_ptr<float>(); a.momentum = momentum; a.update_running = update_running;
+    a.accumulate = accumulate;
   }
-  TORCH_CHECK((int)upd.size() <= kMaxOps, "too many update-only BN layers");
-  a.nupd = upd.size();
-  for (size_t k = 0; k < upd.size(); ++k) a.upd[k] = make_bn(upd[k], a.C);
-  a.w = ptr_or_null<float>(w); a.id_idx = id_idx; a.xid = ptr_or_null<float>(xid);
-  if (a.xid) TORCH_CHECK(xid->sizes() == out.sizes(), "identity shape");
-  a.gamma = ptr_or_null<float>(gamma); a.beta = ptr_or_null<float>(beta);
-  a.out = out.data_ptr<float>(); a.momentum = momentum; a.update_running = update_running;
-  a.accumulate = accumulate;
-  launch_combine_fwd(a, cur_stream());
+  launch_combine_fwd(bt, cur_stream());
 }
 
 // (dout, zs, bns, xid|None, red, widx, id_idx, gw|None)

@@ -106,13 +106,14 @@ struct Batch {
   static constexpr int kCap = M;
 };
 using DwPwFwdBatch = Batch<DwPwFwdArgs, 8>;
+using CombineFwdBatch = Batch<CombineFwdArgs, 3>;
 using PwFwdBatch = Batch<PwFwdArgs, 16>;
 using PoolFwdBatch = Batch<PoolFwdArgs, 8>;
 using CombineBwdBatch = Batch<CombineBwdArgs, 4>;
 using PwBwdBatch = Batch<PwBwdArgs, 8>;
 using DwBwdBatch = Batch<DwBwdArgs, 8>;
 using PoolBwdBatch = Batch<PoolBwdArgs, 8>;
-static_assert(sizeof(DwPwFwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096 && sizeof(PoolFwdBatch) <= 4096 &&
+static_assert(sizeof(DwPwFwdBatch) <= 4096 && sizeof(CombineFwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096 && sizeof(PoolFwdBatch) <= 4096 &&
                   sizeof(CombineBwdBatch) <= 4096 && sizeof(PwBwdBatch) <= 4096 && sizeof(DwBwdBatch) <= 4096 &&
                   sizeof(PoolBwdBatch) <= 4096,
               "kernel argument batches must fit the 4 KB kernarg budget");
@@ -122,7 +123,7 @@ void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipSt
 void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st);
 void launch_pool_fwd(const PoolFwdBatch& b, int S, hipStream_t st);
 void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st);
-void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st);
+void launch_combine_fwd(const CombineFwdBatch& b, hipStream_t st);
 void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st);
 void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st);
 int max_blocks();

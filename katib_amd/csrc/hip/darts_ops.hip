@@ -40,7 +40,7 @@ static int g_max_blocks = 0;
 int max_blocks() {
   if (g_max_blocks <= 0) {
     const char* e = getenv("KATIB_HIP_MAX_BLOCKS");
-    g_max_blocks = e ? std::max(1, atoi(e)) : 1024;
+    g_max_blocks = e ? std::max(1, atoi(e)) : 2048;
   }
   return g_max_blocks;
 }
@@ -336,37 +336,56 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdBatch bt) {
 // ------------------------------------------------------------------------------------------------
 // combine_fwd: out = sum_k w[k] * BN_k(z_k) + wid * x  (elementwise), running stats in block 0
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdArgs a) {
-  const int C = a.C, HW = a.HW;
-  const size_t total = (size_t)a.N * C * HW;
-  __shared__ float sMean[kMaxOps][kMaxC], sInv[kMaxOps][kMaxC], sW[kMaxOps + 1];
-  for (int i = threadIdx.x; i < a.nops * C; i += 256) {
-    int k = i / C, c = i % C;
-    bn_coeffs(a.bn[k], c, sMean[k][c], sInv[k][c]);
-  }
-  if (threadIdx.x < a.nops) sW[threadIdx.x] = a.w ? a.w[a.widx[threadIdx.x]] : 1.f;
-  if (threadIdx.x == 0) sW[kMaxOps] = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
-  __syncthreads();
-  if (blockIdx.x == 0 && a.update_running) {
-    for (int i = threadIdx.x; i < (a.nops + a.nupd) * C; i += 256) {
+__global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
+  // All edges of a node in one pass: out = sum_e [ sum_k w_e[k] * BN_ek(z_ek) + w_e[id] * x_e ].
+  const CombineFwdArgs& a0 = bt.e[0];
+  const int C = a0.C, HW = a0.HW, ne = bt.n;
+  const size_t total = (size_t)a0.N * C * HW;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sMean = smem;                                 // [ne][kMaxOps][C]
+  float* sInv = sMean + ne * kMaxOps * C;              // [ne][kMaxOps][C]
+  float* sW = sInv + ne * kMaxOps * C;                 // [ne][kMaxOps + 1]
+  for (int e = 0; e < ne; ++e) {
+    const CombineFwdArgs& a = bt.e[e];
+    for (int i = threadIdx.x; i < a.nops * C; i += 256) {
       int k = i / C, c = i % C;
-      const BNRef& b = k < a.nops ? a.bn[k] : a.upd[k - a.nops];
-      if (!b.rmean || b.eval) continue;
-      double m, v;
-      bn_moments(b, c, m, v);
-      double cnt = 1.0 / (double)b.inv_count;
-      double vu = cnt > 1 ? v * cnt / (cnt - 1) : v;
-      b.rmean[c] = (1.f - a.momentum) * b.rmean[c] + a.momentum * (float)m;
-      b.rvar[c] = (1.f - a.momentum) * b.rvar[c] + a.momentum * (float)vu;
+      bn_coeffs(a.bn[k], c, sMean[(e * kMaxOps + k) * C + c], sInv[(e * kMaxOps + k) * C + c]);
+    }
+    if (threadIdx.x < a.nops) sW[e * (kMaxOps + 1) + threadIdx.x] = a.w ? a.w[a.widx[threadIdx.x]] : 1.f;
+    if (threadIdx.x == 0) sW[e * (kMaxOps + 1) + kMaxOps] = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    for (int e = 0; e < ne; ++e) {
+      const CombineFwdArgs& a = bt.e[e];
+      if (!a.update_running) continue;
+      for (int i = threadIdx.x; i < (a.nops + a.nupd) * C; i += 256) {
+        int k = i / C, c = i % C;
+        const BNRef& b = k < a.nops ? a.bn[k] : a.upd[k - a.nops];
+        if (!b.rmean || b.eval) continue;
+        double m, v;
+        bn_moments(b, c, m, v);
+        double cnt = 1.0 / (double)b.inv_count;
+        double vu = cnt > 1 ? v * cnt / (cnt - 1) : v;
+        b.rmean[c] = (1.f - a.momentum) * b.rmean[c] + a.momentum * (float)m;
+        b.rvar[c] = (1.f - a.momentum) * b.rvar[c] + a.momentum * (float)vu;
+      }
     }
   }
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
     int c = (int)((i / HW) % C);
     float acc = 0.f;
-    for (int k = 0; k < a.nops; ++k) acc += sW[k] * (a.z[k][i] - sMean[k][c]) * sInv[k][c];
-    if (a.xid) acc += sW[kMaxOps] * a.xid[i];
-    if (a.gamma) acc = acc * a.gamma[c] + a.beta[c];
-    a.out[i] = a.accumulate ? a.out[i] + acc : acc;
+    for (int e = 0; e < ne; ++e) {
+      const CombineFwdArgs& a = bt.e[e];
+      const float* sw = sW + e * (kMaxOps + 1);
+      for (int k = 0; k < a.nops; ++k) {
+        const int j = (e * kMaxOps + k) * C + c;
+        acc += sw[k] * (a.z[k][i] - sMean[j]) * sInv[j];
+      }
+      if (a.xid) acc += sw[kMaxOps] * a.xid[i];
+    }
+    if (a0.gamma) acc = acc * a0.gamma[c] + a0.beta[c];
+    a0.out[i] = a0.accumulate ? a0.out[i] + acc : acc;
   }
 }
 
@@ -676,9 +695,14 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
         }
       }
       // input grads for own input rows: the tap geometry depends only on the pixel q, so it
-      // is computed once per pixel (branch-free masks) and reused for every channel
-      for (int q0 = 0; q0 < nq; q0 += 256) {
-        const int q = q0 + tid;
+      // is computed once per pixel (branch-free masks) and reused for every channel. A tile
+      // owns nq = 64*S*S input pixels: at stride 1 the block's 4 waves take 4 channel groups
+      // of the same 64 pixels (wave-uniform channel -> scalar weight loads, wave-level sums).
+      const int qspan = (nq < 256 && 256 % nq == 0) ? nq : 256;
+      const int G = 256 / qspan;
+      for (int q0 = 0; q0 < nq; q0 += qspan) {
+        const int q = q0 + tid % qspan;
+        const int cg = __builtin_amdgcn_readfirstlane(tid / qspan);
         const int rr = q / W, ix = q - rr * W;
         const int iy = oy0 * S + rr;
         const bool ok = q < nq && iy < H;
@@ -697,7 +721,7 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
           ocol[k] = u ? ox : 0;
           mcol[k] = u ? 1.f : 0.f;
         }
-        for (int cc = 0; cc < cn; ++cc) {
+        for (int cc = cg; cc < cn; cc += G) {
           const int c = c0 + cc;
           const float* wk = a.dw + c * KK;  // wave-uniform -> scalar loads
           const float* dd = sDD + cc * OR * Wo;
@@ -875,10 +899,12 @@ void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st) {
   else hipLaunchKernelGGL(pool_bwd_kernel<2>, grid, dim3(256), lds, st, b);
 }
 
-void launch_combine_fwd(const CombineFwdArgs& a, hipStream_t st) {
+void launch_combine_fwd(const CombineFwdBatch& b, hipStream_t st) {
+  const CombineFwdArgs& a = b.e[0];
   size_t total = (size_t)a.N * a.C * a.HW;
   int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
-  hipLaunchKernelGGL(combine_fwd_kernel, dim3(blocks), dim3(256), 0, st, a);
+  size_t lds = sizeof(float) * (2 * b.n * kMaxOps * a.C + b.n * (kMaxOps + 1));
+  hipLaunchKernelGGL(combine_fwd_kernel, dim3(blocks), dim3(256), lds, st, b);
 }
 
 void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st) {

@@ -9,7 +9,7 @@ share its shape (edge batches, ``blockIdx.y`` = edge):
 forward   dwpw_fwd per (kernel size, dilation, stride) [separable stage 1, dilated],
           pool_fwd (avg + max + argmax), pw_fwd x2 (stride-2 skip = FactorizedReduce),
           fold, dwpw_fwd with BN-apply prologue [separable stage 2], fold,
-          combine_fwd per edge accumulating into the node output (+ running-stat updates)
+          combine_fwd summing every edge's weighted BN outputs into the node (+ running stats)
 backward  combine_bwd_reduce (BN-backward sums + d softmax-weights), fold, then pw_bwd /
           dw_bwd / pool_bwd batches; every input gradient is written (not accumulated) by
           its first kernel, so no memsets
@@ -47,8 +47,8 @@ except ImportError as e:  # pragma: no cover - machines without the build
 
 F64 = torch.float64
 REP = int(_K.REP)
-_CAP = {"dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 8, "dw_bwd": 8,
-        "pool_bwd": 8}
+_CAP = {"combine_fwd": 3, "dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 8,
+        "dw_bwd": 8, "pool_bwd": 8}
 _REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
 
 
@@ -267,11 +267,14 @@ class _MixedNode(torch.autograd.Function):
             _K.fold_f64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage2))])
         # ---- weighted sums into the node output
         out = torch.empty(N, C, Ho, Wo, device=dev)
-        for i, e in enumerate(edges):
+        ccalls = []
+        for e in edges:
             e.zl = [e.zs[k] for k in e.widx]
             e.bl = [e.bns[k] for k in e.widx]
-            _K.combine_fwd(e.zl, e.bl, e.widx, e.w, e.id_idx, e.xid, None, None, out, momentum, training, i > 0,
-                           e.upd if training else [])
+            ccalls.append((e.zl, e.bl, e.widx, e.w, e.id_idx, e.xid, e.upd if training else []))
+        cap = _CAP["combine_fwd"]
+        for i in range(0, E, cap):
+            _K.combine_fwd(ccalls[i:i + cap], None, None, out, momentum, training, i > 0)
         ctx.meta = (edges, training, C)
         ctx.save_for_backward(*flat)
         return out
@@ -459,7 +462,7 @@ class _StdConvBN(torch.autograd.Function):
             _K.fold_f64([(stats, 2 * Cout, 2 * Cout)])
         bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
         out = torch.empty_like(z)
-        _K.combine_fwd([z], [bn], [0], None, -1, None, None, None, out, momentum, training, False, [])
+        _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], None, None, out, momentum, training, False)
         ctx.meta = (bn, fr, Cout, training)
         ctx.save_for_backward(x, z, w1, *([w2] if fr else []))
         return out
