@@ -11,8 +11,10 @@ autocast with fp32 master weights, fused AdamW (``foreach``), flash attention
 through ``scaled_dot_product_attention``, synthetic Markov-chain tokens resident in
 HBM, train step captured as a HIP graph.
 
-Checkpoints: ``model.pt`` + ``optim.pt`` (``torch.save``; loaded with
-``weights_only=True``) in ``$KATIB_TRIAL_CHECKPOINT_DIR`` (or ``--checkpoint-dir``).
+Checkpoints: the parent's state is fetched GPU-to-GPU from the warm worker that
+trained it (:mod:`katib_amd.parallel.p2p_ckpt`, peer copy over xGMI); ``model.pt`` +
+``optim.pt`` (``torch.save``, loaded with ``weights_only=True``) in
+``$KATIB_TRIAL_CHECKPOINT_DIR`` (or ``--checkpoint-dir``) are the durable fallback.
 
 Prints ``step=<n> loss=<l>`` while training and ``Validation-loss=<l>
 Validation-accuracy=<token accuracy>`` at the end.
@@ -23,12 +25,14 @@ from __future__ import annotations
 import argparse
 import math
 import os
+import time
 from dataclasses import dataclass
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..parallel import p2p_ckpt
 from .common import CapturedStep, Timer, device, markov_tokens, report
 
 
@@ -116,6 +120,8 @@ def parse_args(argv):
     p.add_argument("--checkpoint-dir", default="")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--capture", type=int, default=1)
+    p.add_argument("--p2p", type=int, default=1, help="hand checkpoints GPU-to-GPU (parallel.p2p_ckpt)")
+    p.add_argument("--save-files", type=int, default=1, help="also write model.pt/optim.pt (durable copy)")
     return p.parse_args(argv)
 
 
@@ -137,11 +143,22 @@ def main(argv=None):
                             fused=cuda, foreach=not cuda, capturable=cuda)
     start_step = 0
     ck = _ckpt_dir(args)
-    if ck and os.path.exists(os.path.join(ck, "model.pt")):
+    source = "init"
+    t_load = time.time()
+    st = p2p_ckpt.fetch(ck, dev) if (ck and cuda and args.p2p) else None  # parent's weights, GPU to GPU
+    if st is not None:
+        model.load_state_dict(st["model"])
+        opt.load_state_dict(st["optim"])
+        start_step = int(st["step"])
+        source = "p2p"
+    elif ck and os.path.exists(os.path.join(ck, "model.pt")):
         model.load_state_dict(torch.load(os.path.join(ck, "model.pt"), map_location=dev, weights_only=True))
         st = torch.load(os.path.join(ck, "optim.pt"), map_location=dev, weights_only=True)
         opt.load_state_dict(st["optim"])
         start_step = int(st["step"])
+        source = "file"
+    if source != "init":
+        report(checkpoint_source=source, checkpoint_load_seconds=time.time() - t_load)
     for g in opt.param_groups:  # the trial's (possibly perturbed) hyperparameters
         g["lr"] = args.lr
         g["weight_decay"] = args.weight_decay
@@ -201,8 +218,12 @@ def main(argv=None):
             n += yb.numel()
     if ck:
         os.makedirs(ck, exist_ok=True)
-        torch.save(model.state_dict(), os.path.join(ck, "model.pt"))
-        torch.save({"optim": opt.state_dict(), "step": start_step + args.steps}, os.path.join(ck, "optim.pt"))
+        end_step = start_step + args.steps
+        if cuda and args.p2p:
+            p2p_ckpt.publish({"model": model.state_dict(), "optim": opt.state_dict(), "step": end_step}, ck)
+        if args.save_files:
+            torch.save(model.state_dict(), os.path.join(ck, "model.pt"))
+            torch.save({"optim": opt.state_dict(), "step": end_step}, os.path.join(ck, "optim.pt"))
     tokens_per_s = args.steps * B * T / max(elapsed, 1e-9)
     report(**{"Validation-loss": tot / n, "Validation-accuracy": correct / n, "tokens_per_s": tokens_per_s})
     return tot / n
