@@ -262,4 +262,4 @@ class PbtService(SuggestionService):
             [j[0] for j in jobs], trial_names=[j[2] for j in jobs], labels=[j[1] for j in jobs]))
 
     def checkpoint_dir(self, trial_name: str) -> str:
-        return os.path.join(self.job_queue.suggestion_dir, trial_name) if self.job_queue else ""
+        return os.path.join(self.job_queue.suggestion_dir, trial_name) if self.job_queue is not None else ""

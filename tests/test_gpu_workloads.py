@@ -33,7 +33,9 @@ def test_pbt_gpt2_p2p_handoff(tmp_path):
         e.spec.max_trial_count, e.spec.parallel_trial_count, e.spec.max_failed_trial_count = 12, 5, 2
         m.create_experiment(e)
         done = m.run_until_complete(e.metadata.name, timeout=900)
-        assert EC.is_succeeded(done), done.status.conditions
+        msgs = [t.status.conditions[-1].message[-1500:] for t in m.list_trials(e.metadata.name)
+                if t.status.conditions[-1].type == "Failed"]
+        assert EC.is_succeeded(done), msgs
         logs = "".join(open(p).read() for p in glob.glob(str(tmp_path / "state" / "trials" / "*" / "*" / "metrics.log")))
         assert "checkpoint_source=p2p" in logs  # children loaded their parent's weights GPU-to-GPU
     finally:

@@ -63,6 +63,11 @@ def test_gpt2_pbt_example(manager):
     assert EC.is_succeeded(done), done.status.conditions
     parents = [t.metadata.labels.get("pbt.suggestion.katib.kubeflow.org/parent") for t in trials]
     assert any(parents)  # later generations continue from a parent checkpoint
+    import glob
+
+    # suggestion_trial_dir is remapped to each member's own directory under the state dir
+    members = glob.glob(os.path.join(manager.state_dir, "pbt", e.metadata.name, "*", "model.pt"))
+    assert len(members) >= 5
 
 
 def test_enas_child_example(manager):
