@@ -137,6 +137,7 @@ def main():
                        "global_batch": bs * comm.world_size, "seq_len": None,
                        "parallelism": "dp%d" % comm.world_size, "epochs": cfg["epochs"],
                        "steps_per_epoch": steps_per_epoch, "ops": args.ops, "hip_graph": bool(search.capture),
+                       "allreduce": ("xgmi-oneshot" if comm.xgmi is not None else "rccl") if comm.distributed else None,
                        "second_order": True},
             "ms_valid_batch": round(ms_valid, 4),
             "train_images_per_s": round(bs * comm.world_size * 1000.0 / ms_step, 1),

@@ -19,8 +19,9 @@ train/valid batches and the four gradient vectors are averaged with one RCCL
 all-reduce each over flat buffers. BN statistics stay per-rank (like DDP).
 
 With ``capture=True`` every segment between collectives is captured once as a
-HIP graph (``torch.cuda.CUDAGraph``) and replayed; at world size 1 the whole
-step is a single graph. All scalars (lr, eps, Adam step) live on the device so
+HIP graph (``torch.cuda.CUDAGraph``) and replayed; at world size 1, or when the
+all-reduces run as the one-shot xGMI kernel (``parallel/xgmi.py``, capturable),
+the whole step is a single graph. All scalars (lr, eps, Adam step) live on the device so
 the replay needs no host synchronisation.
 """
 
@@ -57,6 +58,8 @@ class DartsSearch:
         self.layout = layout
         self.device = torch.device(device)
         self.comm = comm or Comm(device=self.device)
+        if self.device.type == "cuda":
+            self.comm.enable_xgmi()  # collective; RCCL stays the fallback
         self.s = dict(DEFAULTS)
         if settings:
             self.s.update({k: float(v) for k, v in settings.items() if k in DEFAULTS})
@@ -229,13 +232,18 @@ class DartsSearch:
 
     def _build_graphs(self):
         segs = self._segments()
-        # merge segments with no collective in between (all of them at world size 1)
+        # merge segments with no host-side collective in between: all of them at world size 1
+        # or when the all-reduces run as the (capturable) one-shot xGMI kernel
+        whole = self.comm.graph_capturable([t for _, colls in segs for t in colls])
         groups, cur = [], []
         for fn, colls in segs:
-            cur.append(fn)
-            if colls and self.comm.distributed:
-                groups.append((cur, colls))
-                cur = []
+            if whole:
+                cur.append(lambda fn=fn, colls=colls: (fn(), [self.comm.allreduce_mean_(t) for t in colls]))
+            else:
+                cur.append(fn)
+                if colls and self.comm.distributed:
+                    groups.append((cur, colls))
+                    cur = []
         if cur:
             groups.append((cur, []))
         # warm up on a side stream (required before capture), then capture

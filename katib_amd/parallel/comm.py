@@ -23,6 +23,7 @@ class Comm:
         self.rank, self.world_size, self.local_rank = rank, world_size, local_rank
         self.backend = backend
         self.device = device or torch.device("cpu")
+        self.xgmi = None  # one-shot xGMI all-reduce (parallel/xgmi.py), see enable_xgmi()
 
     @staticmethod
     def from_env(device_type: Optional[str] = None) -> "Comm":
@@ -53,30 +54,58 @@ class Comm:
     def distributed(self) -> bool:
         return self.world_size > 1
 
+    def enable_xgmi(self) -> bool:
+        """Collective: set up the one-shot xGMI all-reduce for small float32 messages
+        (falls back to RCCL when unavailable, disabled or failing its self-test)."""
+        if self.xgmi is None and self.world_size > 1 and self.backend == "nccl":
+            from . import xgmi
+
+            self.xgmi = xgmi.create(self)
+        return self.xgmi is not None
+
+    def graph_capturable(self, tensors) -> bool:
+        """True when all-reducing ``tensors`` can be captured inside a HIP graph."""
+        return self.world_size == 1 or (self.xgmi is not None and all(self.xgmi.fits(t) for t in tensors))
+
+    def _coll(self, fn, t: torch.Tensor, *a, **kw) -> torch.Tensor:
+        """Run a torch.distributed collective; gloo gets a host copy of device tensors."""
+        if self.backend == "gloo" and t.is_cuda:
+            h = t.cpu()
+            fn(h, *a, **kw)
+            t.copy_(h)
+        else:
+            fn(t, *a, **kw)
+        return t
+
     def allreduce_mean_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world_size > 1:
-            if self.backend == "nccl":
+            if self.xgmi is not None and self.xgmi.fits(t):
+                self.xgmi.allreduce_(t, average=True)
+            elif self.backend == "nccl":
                 dist.all_reduce(t, op=dist.ReduceOp.AVG)
             else:
-                dist.all_reduce(t)
+                self._coll(dist.all_reduce, t)
                 t.div_(self.world_size)
         return t
 
     def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world_size > 1:
-            dist.all_reduce(t)
+            if self.xgmi is not None and self.xgmi.fits(t):
+                self.xgmi.allreduce_(t)
+            else:
+                self._coll(dist.all_reduce, t)
         return t
 
     def allreduce_max(self, x: float) -> float:
         if self.world_size <= 1:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=self.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        self._coll(dist.all_reduce, t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world_size > 1:
-            dist.broadcast(t, src)
+            self._coll(dist.broadcast, t, src)
         return t
 
     def barrier(self):
