@@ -1,0 +1,377 @@
+// Implicit-GEMM convolutions for gfx950: bf16 operands, fp32 accumulation on
+// v_mfma_f32_16x16x32_bf16, NHWC activations, [K][R][S][C] filters.
+//
+// The CIFAR ResNet-18 trial (BASELINE config 3) spends >90 % of its time in MIOpen's
+// naive fallback kernels for several bf16 NHWC shapes on this stack (profiles/
+// resnet18_*), and the ENAS child networks need the same k x k / stride / dilation
+// family (reference op_library.py:22-155). Three kernels cover training:
+//
+//  fwd   y[m][k]  = sum_(r,s,c) x[pix(m,r,s)][c] * w[k][r][s][c]     M = N*OH*OW, N = K
+//  dgrad dx[m][c] = sum_(r,s,k) dy[pix'(m,r,s)][k] * wt[c][r][s][k]   M = N*H*W,   N = C
+//  wgrad dw[k][(r,s,c)] = sum_p dy[p][k] * x[pix(p,r,s)][c]          split over p, fp32 atomics
+//
+// fwd/dgrad: both operands are reduction-contiguous (16-byte chunks of 8 channels), so
+// every thread gathers fixed rows x fixed 8-channel chunk per stage straight into
+// registers (zero for padding / stride holes), writes them to a double-buffered LDS
+// image with 16-B padded rows (conflict-free ds_read_b128 fragment reads) and the
+// 4 waves (2 x 2) run 2 MFMA k-steps per 64-deep stage. Block -> tile order is XCD
+// aware: the tiles that share an im2col row block sit on one XCD (one L2).
+// wgrad: the reduction runs over pixels, which are strided in both operands, so the
+// LDS images stay in natural [pixel][channel] layout and the MFMA fragments are read
+// with the gfx950 transposing ds_read_b64_tr_b16.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+
+#include "conv_igemm.h"
+
+namespace katib_hip {
+namespace conv {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: HIP's uint4 class (unions) defeats SROA -> scratch
+typedef __hip_bfloat16 bf16;
+
+constexpr int kBK = 64;       // reduction depth per LDS stage
+constexpr int kPad = 8;       // bf16 row padding (16 B)
+constexpr int kThreads = 256;  // 4 waves as 2 x 2
+
+__device__ inline int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// ---------------------------------------------------------------- fwd / dgrad
+template <int MODE, int BM, int BN>
+__global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16* __restrict__ src,
+                                                         const bf16* __restrict__ wmat, bf16* __restrict__ y,
+                                                         float* __restrict__ y32, int M, int N, int Kd) {
+  constexpr int WM = BM / 2, WN = BN / 2, RM = WM / 16, RN = WN / 16;
+  constexpr int LD = kBK + kPad;
+  constexpr int AR = BM / 32, BR = BN / 32;  // rows per thread per stage
+  __shared__ __align__(16) bf16 smem[2 * (BM + BN) * LD];
+  bf16* As = smem;
+  bf16* Bs = smem + 2 * BM * LD;
+
+  const int tilesN = (N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / tilesN) * BM, n0 = (wg % tilesN) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int kc = tid & 7, trow = tid >> 3;
+
+  // per-thread gathered rows: image base pixel and the (h, w) origin of the window
+  int a_base[AR], a_h[AR], a_w[AR];
+  bool a_ok[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + trow + 32 * i;
+    a_ok[i] = m < M;
+    const int mm = a_ok[i] ? m : 0;
+    if (MODE == 0) {
+      const int hw = g.OH * g.OW, n = mm / hw, rem = mm - n * hw, oh = rem / g.OW, ow = rem - oh * g.OW;
+      a_base[i] = n * g.H * g.W;
+      a_h[i] = oh * g.sh - g.ph;
+      a_w[i] = ow * g.sw - g.pw;
+    } else {
+      const int hw = g.H * g.W, n = mm / hw, rem = mm - n * hw, ih = rem / g.W, iw = rem - ih * g.W;
+      a_base[i] = n * g.OH * g.OW;
+      a_h[i] = ih + g.ph;
+      a_w[i] = iw + g.pw;
+    }
+  }
+  const bf16* b_row[BR];
+  bool b_ok[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + trow + 32 * i;
+    b_ok[i] = n < N;
+    b_row[i] = wmat + (int64_t)(b_ok[i] ? n : 0) * Kd;
+  }
+
+  u32x4 ra[AR], rb[BR];
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  auto gload = [&](int kt) {
+    const int kk = kt * kBK + kc * 8;
+    const bool kin = kk < Kd;
+    const int CH = MODE == 0 ? g.C : g.K;
+    const int rs = kk / CH, ch = kk - rs * CH, r = rs / g.S, s = rs - r * g.S;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      u32x4 v = zero;
+      if (kin && a_ok[i]) {
+        if (MODE == 0) {
+          const int ih = a_h[i] + r * g.dh, iw = a_w[i] + s * g.dw;
+          if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+            v = *reinterpret_cast<const u32x4*>(src + (int64_t)(a_base[i] + ih * g.W + iw) * g.C + ch);
+        } else {
+          int oh = a_h[i] - r * g.dh, ow = a_w[i] - s * g.dw;
+          bool ok = oh >= 0 && ow >= 0;
+          if (ok && g.sh > 1) {
+            ok = (oh % g.sh) == 0;
+            oh /= g.sh;
+          }
+          if (ok && g.sw > 1) {
+            ok = (ow % g.sw) == 0;
+            ow /= g.sw;
+          }
+          if (ok && oh < g.OH && ow < g.OW)
+            v = *reinterpret_cast<const u32x4*>(src + (int64_t)(a_base[i] + oh * g.OW + ow) * g.K + ch);
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) rb[i] = (kin && b_ok[i]) ? *reinterpret_cast<const u32x4*>(b_row[i] + kk) : zero;
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      *reinterpret_cast<u32x4*>(As + (buf * BM + trow + 32 * i) * LD + kc * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<u32x4*>(Bs + (buf * BN + trow + 32 * i) * LD + kc * 8) = rb[i];
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int a = 0; a < RM; ++a)
+#pragma unroll
+    for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (Kd + kBK - 1) / kBK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+#pragma unroll
+    for (int ks = 0; ks < kBK / 32; ++ks) {
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int a = 0; a < RM; ++a)
+        af[a] = __builtin_bit_cast(
+            bf16x8, *reinterpret_cast<const u32x4*>(As + (buf * BM + wr * WM + a * 16 + fr) * LD + ks * 32 + fk));
+#pragma unroll
+      for (int b = 0; b < RN; ++b)
+        bfg[b] = __builtin_bit_cast(
+            bf16x8, *reinterpret_cast<const u32x4*>(Bs + (buf * BN + wc * WN + b * 16 + fr) * LD + ks * 32 + fk));
+#pragma unroll
+      for (int a = 0; a < RM; ++a)
+#pragma unroll
+        for (int b = 0; b < RN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfg[b], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D of 16x16x32 -> col = lane & 15, row = 4 * (lane >> 4) + j
+#pragma unroll
+  for (int a = 0; a < RM; ++a)
+#pragma unroll
+    for (int b = 0; b < RN; ++b) {
+      const int col = n0 + wc * WN + b * 16 + fr;
+      if (col >= N) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m0 + wr * WM + a * 16 + 4 * (lane >> 4) + j;
+        if (row >= M) continue;
+        if (y32)
+          y32[(int64_t)row * N + col] = acc[a][b][j];
+        else
+          y[(int64_t)row * N + col] = __float2bfloat16(acc[a][b][j]);
+      }
+    }
+}
+
+// ---------------------------------------------------------------- wgrad
+template <int BMW, int BNW>
+__global__ __launch_bounds__(kThreads) void wgrad_kernel(ConvGeom g, const bf16* __restrict__ x,
+                                                         const bf16* __restrict__ dy, float* __restrict__ dw, int P,
+                                                         int Kd, int chunk) {
+  constexpr int BP = 64;  // pixels per LDS stage (2 MFMA k-steps)
+  constexpr int WM = BMW / 2, WN = BNW / 2, RM = WM / 16, RN = WN / 16;
+  constexpr int LDA = BMW + kPad, LDB = BNW + kPad;
+  constexpr int AC = BP * BMW / 8 / kThreads, BC = BP * BNW / 8 / kThreads;  // 16-B chunks per thread
+  __shared__ __align__(16) bf16 smem[2 * BP * (LDA + LDB)];
+  bf16* As = smem;
+  bf16* Bs = smem + 2 * BP * LDA;
+
+  const int K = g.K;
+  const int tilesN = (Kd + BNW - 1) / BNW;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / tilesN) * BMW, n0 = (wg % tilesN) * BNW;
+  const int p_begin = blockIdx.y * chunk, p_end = min(P, p_begin + chunk);
+  if (p_begin >= p_end) return;  // uniform per block
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int hw = g.OH * g.OW;
+
+  // fixed per-thread chunk columns: A (dy) chunk -> (pixel row, 8 output channels)
+  int a_prow[AC], a_col[AC];
+#pragma unroll
+  for (int i = 0; i < AC; ++i) {
+    const int id = tid + kThreads * i;
+    a_prow[i] = id / (BMW / 8);
+    a_col[i] = m0 + (id % (BMW / 8)) * 8;
+  }
+  // B (im2col x) chunk -> (pixel row, 8 channels at one (r, s))
+  int b_prow[BC], b_col[BC], b_r[BC], b_s[BC], b_c[BC];
+#pragma unroll
+  for (int i = 0; i < BC; ++i) {
+    const int id = tid + kThreads * i;
+    b_prow[i] = id / (BNW / 8);
+    const int col = n0 + (id % (BNW / 8)) * 8;
+    b_col[i] = col;
+    const int rs = col / g.C;
+    b_c[i] = col - rs * g.C;
+    b_r[i] = rs / g.S;
+    b_s[i] = rs - b_r[i] * g.S;
+  }
+  u32x4 ra[AC], rb[BC];
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  auto gload = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < AC; ++i) {
+      const int p = p0 + a_prow[i];
+      ra[i] = (p < p_end && a_col[i] < K) ? *reinterpret_cast<const u32x4*>(dy + (int64_t)p * K + a_col[i]) : zero;
+    }
+#pragma unroll
+    for (int i = 0; i < BC; ++i) {
+      const int p = p0 + b_prow[i];
+      u32x4 v = zero;
+      if (p < p_end && b_col[i] < Kd) {
+        const int n = p / hw, rem = p - n * hw, oh = rem / g.OW, ow = rem - oh * g.OW;
+        const int ih = oh * g.sh - g.ph + b_r[i] * g.dh, iw = ow * g.sw - g.pw + b_s[i] * g.dw;
+        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+          v = *reinterpret_cast<const u32x4*>(x + ((int64_t)(n * g.H + ih) * g.W + iw) * g.C + b_c[i]);
+      }
+      rb[i] = v;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AC; ++i)
+      *reinterpret_cast<u32x4*>(As + (buf * BP + a_prow[i]) * LDA + (a_col[i] - m0)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BC; ++i)
+      *reinterpret_cast<u32x4*>(Bs + (buf * BP + b_prow[i]) * LDB + (b_col[i] - n0)) = rb[i];
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int a = 0; a < RM; ++a)
+#pragma unroll
+    for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed fragment reads: lane 16g + 4q + pp addresses row (8g + q [+4]) cols (c0 + 4pp)
+  const int tg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  gload(p_begin);
+  sstore(0);
+  __syncthreads();
+  int buf = 0;
+  for (int p0 = p_begin; p0 < p_end; p0 += BP) {
+    const bool more = p0 + BP < p_end;
+    if (more) gload(p0 + BP);
+#pragma unroll
+    for (int ks = 0; ks < BP / 32; ++ks) {
+      const int prow = buf * BP + ks * 32 + 8 * tg + tq;
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int a = 0; a < RM; ++a) {
+        const bf16* p1 = As + prow * LDA + wr * WM + a * 16 + 4 * tp;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1));
+        const s16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1 + 4 * LDA));
+        af[a] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int b = 0; b < RN; ++b) {
+        const bf16* p1 = Bs + prow * LDB + wc * WN + b * 16 + 4 * tp;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1));
+        const s16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1 + 4 * LDB));
+        bfg[b] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int a = 0; a < RM; ++a)
+#pragma unroll
+        for (int b = 0; b < RN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfg[b], acc[a][b], 0, 0, 0);
+    }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  const int fr = lane & 15;
+#pragma unroll
+  for (int a = 0; a < RM; ++a)
+#pragma unroll
+    for (int b = 0; b < RN; ++b) {
+      const int col = n0 + wc * WN + b * 16 + fr;
+      if (col >= Kd) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m0 + wr * WM + a * 16 + 4 * (lane >> 4) + j;
+        if (row < K) unsafeAtomicAdd(dw + (int64_t)row * Kd + col, acc[a][b][j]);
+      }
+    }
+}
+
+template <int MODE, int BM, int BN>
+hipError_t launch_igemm(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, float* y32, int M, int N, int Kd,
+                        hipStream_t st) {
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN>), dim3(grid), dim3(kThreads), 0, st, g, src, wm, y, y32, M, N, Kd);
+  return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t dispatch(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, float* y32, int M, int N, int Kd,
+                    hipStream_t st) {
+  const bool wide = N > 64;
+  const int tiles128 = ((M + 127) / 128) * ((N + (wide ? 127 : 63)) / (wide ? 128 : 64));
+  const bool tall = tiles128 >= 512;  // else halve BM to fill the 256 CUs
+  if (wide) return tall ? launch_igemm<MODE, 128, 128>(g, src, wm, y, y32, M, N, Kd, st)
+                        : launch_igemm<MODE, 64, 128>(g, src, wm, y, y32, M, N, Kd, st);
+  return tall ? launch_igemm<MODE, 128, 64>(g, src, wm, y, y32, M, N, Kd, st)
+              : launch_igemm<MODE, 64, 64>(g, src, wm, y, y32, M, N, Kd, st);
+}
+
+}  // namespace
+
+hipError_t launch_fwd(const ConvGeom& g, const bf16* x, const bf16* w, bf16* y, float* out_f32, hipStream_t st) {
+  return dispatch<0>(g, x, w, y, out_f32, g.N * g.OH * g.OW, g.K, g.R * g.S * g.C, st);
+}
+
+hipError_t launch_dgrad(const ConvGeom& g, const bf16* dy, const bf16* wt, bf16* dx, hipStream_t st) {
+  return dispatch<1>(g, dy, wt, dx, nullptr, g.N * g.H * g.W, g.C, g.R * g.S * g.K, st);
+}
+
+hipError_t launch_wgrad(const ConvGeom& g, const bf16* x, const bf16* dy, float* dw32, hipStream_t st) {
+  const int P = g.N * g.OH * g.OW, Kd = g.R * g.S * g.C;
+  const bool wideM = g.K > 64, wideN = Kd > 64;
+  const int tiles = ((g.K + (wideM ? 127 : 63)) / (wideM ? 128 : 64)) * ((Kd + (wideN ? 127 : 63)) / (wideN ? 128 : 64));
+  constexpr int BP = 64;
+  int splits = (2048 + tiles - 1) / tiles;
+  const int max_splits = (P + 4 * BP - 1) / (4 * BP);  // >= 4 stages per block
+  splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
+  if (splits < 1) splits = 1;
+  int chunk = (P + splits - 1) / splits;
+  chunk = (chunk + BP - 1) / BP * BP;
+  splits = (P + chunk - 1) / chunk;
+  dim3 grid(tiles, splits);
+  if (wideM && wideN)
+    hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk);
+  else if (wideM)
+    hipLaunchKernelGGL((wgrad_kernel<128, 64>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk);
+  else if (wideN)
+    hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk);
+  return hipGetLastError();
+}
+
+}  // namespace conv
+}  // namespace katib_hip

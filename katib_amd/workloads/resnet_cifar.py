@@ -2,9 +2,11 @@
 
 ``--epochs`` is the HyperBand resource. The network is the CIFAR ResNet-18 variant
 (3x3 stem, no max-pool, [2, 2, 2, 2] basic blocks, 64-512 channels). MI355X
-specifics: channels-last activations, bf16 autocast (fp32 master weights, MFMA
-convolutions through MIOpen), device-resident synthetic data, and the whole train
-step (forward, loss, backward, SGD+Nesterov momentum) captured as one HIP graph.
+specifics: channels-last activations, bf16 autocast (fp32 master weights), every
+convolution on the hand-written implicit-GEMM MFMA kernels (``ops/conv.py``,
+``--conv torch`` switches back to MIOpen), device-resident synthetic data, and the
+whole train step (forward, loss, backward, SGD+Nesterov momentum) captured as one
+HIP graph.
 
 Per epoch it prints ``epoch=<e> loss=<l> Validation-accuracy=<a>``; the median-stop
 rule compares the objective after ``start_step`` reports.
@@ -18,7 +20,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import conv as hconv
 from .common import CapturedStep, Timer, device, pattern_images, report
+
+Conv = hconv.Conv2d  # HIP implicit GEMM on GPU, stock nn.Conv2d on CPU
 
 
 def parse_args(argv):
@@ -34,19 +39,20 @@ def parse_args(argv):
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--capture", type=int, default=1)
     p.add_argument("--max-steps", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
+    p.add_argument("--conv", default="hip", choices=["hip", "torch"], help="convolution backend on GPU")
     return p.parse_args(argv)
 
 
 class BasicBlock(nn.Module):
     def __init__(self, cin, cout, stride):
         super().__init__()
-        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.conv1 = Conv(cin, cout, 3, stride, 1, bias=False)
         self.bn1 = nn.BatchNorm2d(cout)
-        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.conv2 = Conv(cout, cout, 3, 1, 1, bias=False)
         self.bn2 = nn.BatchNorm2d(cout)
         self.short = None
         if stride != 1 or cin != cout:
-            self.short = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+            self.short = nn.Sequential(Conv(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x):
         out = F.relu(self.bn1(self.conv1(x)))
@@ -58,7 +64,7 @@ class ResNet18(nn.Module):
     def __init__(self, width=64, classes=10):
         super().__init__()
         w = width
-        self.stem = nn.Sequential(nn.Conv2d(3, w, 3, 1, 1, bias=False), nn.BatchNorm2d(w), nn.ReLU())
+        self.stem = nn.Sequential(Conv(3, w, 3, 1, 1, bias=False), nn.BatchNorm2d(w), nn.ReLU())
         layers, cin = [], w
         for i, cout in enumerate((w, 2 * w, 4 * w, 8 * w)):
             stride = 1 if i == 0 else 2
@@ -73,7 +79,9 @@ class ResNet18(nn.Module):
 
 
 def main(argv=None):
+    global Conv
     args = parse_args(argv if argv is not None else [])
+    Conv = hconv.Conv2d if args.conv == "hip" else nn.Conv2d
     dev = device()
     torch.manual_seed(args.seed)
     cuda = dev.type == "cuda"
