@@ -23,8 +23,10 @@ ConvGeom make_geom(const std::vector<int64_t>& v) {
   }
   TORCH_CHECK(g.N > 0 && g.H > 0 && g.W > 0 && g.C > 0 && g.K > 0 && g.R > 0 && g.S > 0, "empty geometry");
   TORCH_CHECK(g.sh > 0 && g.sw > 0 && g.dh > 0 && g.dw > 0, "stride / dilation must be positive");
-  TORCH_CHECK(g.OH == (g.H + 2 * g.ph - g.dh * (g.R - 1) - 1) / g.sh + 1 &&
-                  g.OW == (g.W + 2 * g.pw - g.dw * (g.S - 1) - 1) / g.sw + 1 && g.OH > 0 && g.OW > 0,
+  // (ph, pw) is the top/left padding; the bottom/right padding is implied by (OH, OW), which
+  // allows TF-style asymmetric 'same' padding. Every gather is bounds-checked in the kernels.
+  TORCH_CHECK(g.OH > 0 && g.OW > 0 && g.ph < g.dh * g.R && g.pw < g.dw * g.S &&
+                  (int64_t)(g.OH - 1) * g.sh <= (int64_t)g.H + g.ph && (int64_t)(g.OW - 1) * g.sw <= (int64_t)g.W + g.pw,
               "output size inconsistent with the geometry");
   TORCH_CHECK((int64_t)g.N * g.H * g.W * g.C < (1ll << 31) && (int64_t)g.N * g.OH * g.OW * g.K < (1ll << 31),
               "tensor too large for 32-bit pixel indexing");

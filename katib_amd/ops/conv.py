@@ -51,15 +51,18 @@ def _pad_c(t: torch.Tensor, c8: int) -> torch.Tensor:
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, padding, dilation):
+    def forward(ctx, x, w, stride, padding, dilation, out_hw):
         k = kernels()
         N, C, H, W = x.shape
         K, _, R, S = w.shape
         sh, sw = stride
         ph, pw = padding
         dh, dw = dilation
-        OH = (H + 2 * ph - dh * (R - 1) - 1) // sh + 1
-        OW = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+        if out_hw is None:
+            OH = (H + 2 * ph - dh * (R - 1) - 1) // sh + 1
+            OW = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+        else:  # asymmetric ('same') padding: (ph, pw) top/left, the rest implied by the output size
+            OH, OW = out_hw
         C8 = (C + 7) // 8 * 8
         xn = _pad_c(_nhwc(x.to(torch.bfloat16)), C8)
         wk = _pad_c(w.detach().permute(0, 2, 3, 1).to(torch.bfloat16), C8).contiguous()  # [K][R][S][C8]
@@ -88,14 +91,16 @@ class _ConvFn(torch.autograd.Function):
             dw32 = torch.zeros((K, R * S * C8), device=gy.device, dtype=torch.float32)
             k.conv_wgrad(xn, gyn, dw32, ctx.geom)
             gw = dw32.view(K, R, S, C8)[..., :ctx.C].permute(0, 3, 1, 2).to(ctx.wdtype)
-        return gx, gw, None, None, None
+        return gx, gw, None, None, None, None
 
 
-def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, padding=0, dilation=1) -> torch.Tensor:
-    """bf16 NHWC implicit-GEMM convolution (groups=1) with an fp32 weight master."""
+def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, padding=0, dilation=1,
+           out_hw=None) -> torch.Tensor:
+    """bf16 NHWC implicit-GEMM convolution (groups=1) with an fp32 weight master.
+    ``out_hw`` overrides the output size for asymmetric padding (``padding`` = top/left)."""
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)  # like autocast; keeps the Function's input grad bf16
-    y = _ConvFn.apply(x, w, _pair(stride), _pair(padding), _pair(dilation))
+    y = _ConvFn.apply(x, w, _pair(stride), _pair(padding), _pair(dilation), out_hw)
     if bias is not None:
         y = y + bias.to(y.dtype).view(1, -1, 1, 1)
     return y
@@ -103,6 +108,18 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, padding=0, dil
 
 def supported(x: torch.Tensor, w: torch.Tensor, groups: int = 1) -> bool:
     return x.is_cuda and groups == 1 and w.shape[0] % 8 == 0 and x.dim() == 4
+
+
+def same_conv2d(x, w, bias, stride: int):
+    """TF/Keras ``padding='same'`` (bottom/right-heavy when the total padding is odd)."""
+    k = w.shape[2]
+    outs, tops = [], []
+    for size in x.shape[2:]:
+        out = -(-size // stride)
+        total = max((out - 1) * stride + k - size, 0)
+        outs.append(out)
+        tops.append(total // 2)
+    return conv2d(x, w, bias, stride, tuple(tops), 1, tuple(outs))
 
 
 class Conv2d(nn.Conv2d):

@@ -12,7 +12,9 @@ pooling, Dropout(0.4) and a dense softmax classifier, trained with Adam(1e-3) on
 batches of 128, printing ``Training-Accuracy``, ``Training-Loss``,
 ``Validation-Accuracy``, ``Validation-Loss`` per epoch.
 
-MI355X specifics: NCHW channels-last bf16 convolutions on MFMA (MIOpen), the train step
+MI355X specifics: channels-last bf16 convolutions on the hand-written implicit-GEMM
+MFMA kernels (``ops/conv.py``; TF 'same' padding handled inside the kernel's gather,
+depthwise convolutions stay on MIOpen), the train step
 captured as a HIP graph, synthetic CIFAR-10-shaped data in HBM, and data parallelism
 over the trial's GPUs (``WORLD_SIZE`` ranks, RCCL all-reduce of the flat gradient)
 in place of ``tf.distribute.MirroredStrategy``.
@@ -29,6 +31,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import conv as hconv
 from .common import CapturedStep, Timer, device, pattern_images, report
 
 
@@ -47,6 +50,9 @@ class _SameConv(nn.Module):
         self.conv = nn.Conv2d(cin, cout, k, s, 0, groups=groups, bias=bias)
 
     def forward(self, x):
+        c = self.conv
+        if hconv.supported(x, c.weight, c.groups):  # HIP implicit-GEMM (MFMA) path
+            return hconv.same_conv2d(x, c.weight, c.bias, self.s)
         t, b, _ = _same_pad(x.shape[2], self.k, self.s)
         l, r, _ = _same_pad(x.shape[3], self.k, self.s)
         return self.conv(F.pad(x, (l, r, t, b)))
@@ -68,7 +74,7 @@ class Op(nn.Module):
         elif self.kind == "separable_convolution":
             f, k, s, dm = geti("num_filter", 64), geti("filter_size", 3), geti("stride", 1), geti("depth_multiplier", 1)
             self.body = nn.Sequential(_SameConv(cin, cin * dm, k, s, groups=cin, bias=False),
-                                      nn.Conv2d(cin * dm, f, 1), nn.BatchNorm2d(f, eps=1e-3, momentum=0.01))
+                                      hconv.Conv2d(cin * dm, f, 1), nn.BatchNorm2d(f, eps=1e-3, momentum=0.01))
             self.cout, self.hw = f, -(-hw // s)
         elif self.kind == "depthwise_convolution":
             k, s, dm = geti("filter_size", 3), geti("stride", 1), geti("depth_multiplier", 1)

@@ -69,3 +69,31 @@ def test_conv_module_dropin():
     y = mod(x.contiguous(memory_format=torch.channels_last))
     yr = ref(x.float())
     assert _rel(y, yr) < 1e-2
+
+
+@pytest.mark.parametrize("k,s,size", [(3, 2, 32), (5, 2, 15), (7, 1, 8), (3, 2, 7), (5, 1, 16)])
+def test_same_conv_asymmetric_padding(k, s, size):
+    """TF 'same' padding (bottom/right-heavy) through the kernel's gather, as the ENAS child uses it."""
+    from katib_amd.ops import conv as hc
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(2, 16, size, size, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(24, 16, k, k, device=dev, generator=g) * 0.05).to(torch.bfloat16).float()
+    b = torch.randn(24, device=dev, generator=g)
+    out = -(-size // s)
+    total = max((out - 1) * s + k - size, 0)
+    t = total // 2
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(F.pad(xr, (t, total - t, t, total - t)), wr, b, stride=s)
+    xh = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wh = w.clone().requires_grad_(True)
+    yh = hc.same_conv2d(xh, wh, b, s)
+    assert yh.shape == yr.shape
+    gy = torch.randn(yr.shape, device=dev, generator=g).to(torch.bfloat16)
+    yr.backward(gy.float())
+    yh.backward(gy)
+    assert _rel(yh, yr) < 1e-2
+    assert _rel(xh.grad, xr.grad) < 1e-2
+    assert _rel(wh.grad, wr.grad) < 2e-3
