@@ -443,9 +443,10 @@ void fold_f64(std::vector<py::tuple> segs) {
 
 void register_xgmi(py::module& m);  // xgmi_bind.cpp
 void register_conv(py::module& m);  // conv_bind.cpp
+void register_transformer(py::module& m);  // transformer_bind.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, xGMI all-reduce)";
+  m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, transformer, xGMI all-reduce)";
   m.def("dwpw_fwd", &dwpw_fwd);
   m.def("pw_fwd", &pw_fwd);
   m.def("pool_fwd", &pool_fwd);
@@ -461,4 +462,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("max_blocks", &max_blocks);
   register_xgmi(m);
   register_conv(m);
+  register_transformer(m);
 }

@@ -1,0 +1,207 @@
+// torch bindings of the GPT-2 trial kernels (transformer.hip). Every entry point checks
+// dtype, contiguity, device, alignment and the element counts the kernel and its grid
+// assume before launching on the current HIP stream (graph-capturable: no host syncs).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "transformer.h"
+
+namespace py = pybind11;
+using at::Tensor;
+namespace T_ = katib_hip::tfm;
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void chk(const Tensor& t, at::ScalarType dt, int64_t numel, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt && t.is_contiguous(), name, " must be a contiguous ",
+              c10::toString(dt), " GPU tensor");
+  TORCH_CHECK(t.numel() == numel, name, " has ", t.numel(), " elements, expected ", numel);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+T_::bf16* bp(const Tensor& t) { return reinterpret_cast<T_::bf16*>(t.data_ptr()); }
+void ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e)); }
+
+void ln_fwd(const Tensor& x32, const c10::optional<Tensor>& r, const c10::optional<Tensor>& xo, const Tensor& gamma,
+            const Tensor& beta, const Tensor& y, const Tensor& mean, const Tensor& rstd, double eps) {
+  TORCH_CHECK(x32.dim() == 2, "x32 must be [M, D]");
+  const int64_t M = x32.size(0), D = x32.size(1);
+  TORCH_CHECK(D % 256 == 0 && D / 256 >= 1 && D / 256 <= 8 && D / 256 != 7, "ln_fwd: D must be 256*{1..6,8}");
+  chk(x32, at::kFloat, M * D, "x32");
+  chk(gamma, at::kBFloat16, D, "gamma");
+  chk(beta, at::kBFloat16, D, "beta");
+  chk(y, at::kBFloat16, M * D, "y");
+  chk(mean, at::kFloat, M, "mean");
+  chk(rstd, at::kFloat, M, "rstd");
+  const T_::bf16* rp = nullptr;
+  float* xop = nullptr;
+  if (r.has_value()) {
+    TORCH_CHECK(xo.has_value(), "ln_fwd: residual add needs xo");
+    chk(*r, at::kBFloat16, M * D, "r");
+    chk(*xo, at::kFloat, M * D, "xo");
+    rp = bp(*r);
+    xop = xo->data_ptr<float>();
+  }
+  ok(T_::ln_fwd(x32.data_ptr<float>(), rp, xop, bp(gamma), bp(beta), bp(y), mean.data_ptr<float>(),
+                rstd.data_ptr<float>(), (int)M, (int)D, (float)eps, stream()),
+     "ln_fwd");
+}
+
+int64_t ln_bwd_blocks(int64_t M) { return T_::ln_bwd_blocks((int)M); }
+
+void ln_bwd(const Tensor& dy, const Tensor& xin, const Tensor& mean, const Tensor& rstd, const Tensor& gamma,
+            const c10::optional<Tensor>& dres, const Tensor& dx, const c10::optional<Tensor>& dr,
+            const Tensor& part_g, const Tensor& part_b) {
+  TORCH_CHECK(xin.dim() == 2, "xin must be [M, D]");
+  const int64_t M = xin.size(0), D = xin.size(1);
+  TORCH_CHECK(D % 256 == 0 && D / 256 >= 1 && D / 256 <= 8 && D / 256 != 7, "ln_bwd: D must be 256*{1..6,8}");
+  chk(dy, at::kBFloat16, M * D, "dy");
+  chk(xin, at::kFloat, M * D, "xin");
+  chk(mean, at::kFloat, M, "mean");
+  chk(rstd, at::kFloat, M, "rstd");
+  chk(gamma, at::kBFloat16, D, "gamma");
+  chk(dx, at::kFloat, M * D, "dx");
+  const int64_t nb = T_::ln_bwd_blocks((int)M);
+  chk(part_g, at::kFloat, nb * D, "part_g");
+  chk(part_b, at::kFloat, nb * D, "part_b");
+  const float* dresp = nullptr;
+  if (dres.has_value()) {
+    chk(*dres, at::kFloat, M * D, "dres");
+    dresp = dres->data_ptr<float>();
+  }
+  T_::bf16* drp = nullptr;
+  if (dr.has_value()) {
+    chk(*dr, at::kBFloat16, M * D, "dr");
+    drp = bp(*dr);
+  }
+  ok(T_::ln_bwd(bp(dy), xin.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), bp(gamma), dresp,
+                dx.data_ptr<float>(), drp, part_g.data_ptr<float>(), part_b.data_ptr<float>(), (int)M, (int)D,
+                stream()),
+     "ln_bwd");
+}
+
+void ln_reduce(const Tensor& part_g, const Tensor& part_b, const Tensor& dgamma, const Tensor& dbeta) {
+  const int64_t D = dgamma.numel();
+  TORCH_CHECK(D > 0 && part_g.numel() % D == 0, "ln_reduce: partials must be [nblk, D]");
+  const int64_t nb = part_g.numel() / D;
+  chk(part_g, at::kFloat, nb * D, "part_g");
+  chk(part_b, at::kFloat, nb * D, "part_b");
+  chk(dgamma, at::kBFloat16, D, "dgamma");
+  chk(dbeta, at::kBFloat16, D, "dbeta");
+  ok(T_::ln_reduce_params(part_g.data_ptr<float>(), part_b.data_ptr<float>(), (int)nb, (int)D, bp(dgamma), bp(dbeta),
+                          stream()),
+     "ln_reduce");
+}
+
+void gelu_fwd(const Tensor& u, const Tensor& g) {
+  TORCH_CHECK(u.numel() % 8 == 0, "gelu: numel must be a multiple of 8");
+  chk(u, at::kBFloat16, u.numel(), "u");
+  chk(g, at::kBFloat16, u.numel(), "g");
+  ok(T_::gelu_fwd(bp(u), bp(g), u.numel(), stream()), "gelu_fwd");
+}
+
+void gelu_bwd(const Tensor& u, const Tensor& dy, const Tensor& du) {
+  TORCH_CHECK(u.numel() % 8 == 0, "gelu: numel must be a multiple of 8");
+  chk(u, at::kBFloat16, u.numel(), "u");
+  chk(dy, at::kBFloat16, u.numel(), "dy");
+  chk(du, at::kBFloat16, u.numel(), "du");
+  ok(T_::gelu_bwd(bp(u), bp(dy), bp(du), u.numel(), stream()), "gelu_bwd");
+}
+
+void xent_fwd(const Tensor& logits, const Tensor& tgt, const Tensor& loss, const Tensor& lse, int64_t V) {
+  TORCH_CHECK(logits.dim() == 2, "logits must be [N, Vp]");
+  const int64_t N = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(Vp % 8 == 0 && V > 0 && V <= Vp, "xent: Vp % 8 == 0 and 0 < V <= Vp");
+  chk(logits, at::kBFloat16, N * Vp, "logits");
+  TORCH_CHECK(tgt.is_cuda() && tgt.scalar_type() == at::kLong && tgt.is_contiguous() && tgt.numel() == N, "tgt");
+  chk(loss, at::kFloat, N, "loss");
+  chk(lse, at::kFloat, N, "lse");
+  ok(T_::xent_fwd(bp(logits), tgt.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), (int)N, (int)V,
+                  (int)Vp, stream()),
+     "xent_fwd");
+}
+
+void xent_bwd(const Tensor& logits, const Tensor& tgt, const Tensor& lse, const Tensor& gscale, double inv_n,
+              int64_t V) {
+  TORCH_CHECK(logits.dim() == 2, "logits must be [N, Vp]");
+  const int64_t N = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(Vp % 8 == 0 && V > 0 && V <= Vp, "xent: Vp % 8 == 0 and 0 < V <= Vp");
+  chk(logits, at::kBFloat16, N * Vp, "logits");
+  TORCH_CHECK(tgt.is_cuda() && tgt.scalar_type() == at::kLong && tgt.is_contiguous() && tgt.numel() == N, "tgt");
+  chk(lse, at::kFloat, N, "lse");
+  TORCH_CHECK(gscale.is_cuda() && gscale.scalar_type() == at::kFloat && gscale.numel() == 1, "gscale");
+  ok(T_::xent_bwd(bp(logits), tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), gscale.data_ptr<float>(), (float)inv_n,
+                  (int)N, (int)V, (int)Vp, stream()),
+     "xent_bwd");
+}
+
+void grad_sumsq(const Tensor& g, const Tensor& sumsq) {
+  TORCH_CHECK(g.numel() % 8 == 0, "grad_sumsq: numel must be a multiple of 8");
+  chk(g, at::kBFloat16, g.numel(), "g");
+  TORCH_CHECK(sumsq.is_cuda() && sumsq.scalar_type() == at::kFloat && sumsq.numel() == 1, "sumsq");
+  ok(T_::grad_sumsq(bp(g), g.numel(), sumsq.data_ptr<float>(), stream()), "grad_sumsq");
+}
+
+void adamw(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& w16, const Tensor& lr,
+           const Tensor& step, double b1, double b2, double eps, double wd, const Tensor& sumsq, double max_norm) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(n % 8 == 0, "adamw: flat buffers must be padded to a multiple of 8");
+  chk(p, at::kFloat, n, "p");
+  chk(g, at::kBFloat16, n, "g");
+  chk(m, at::kFloat, n, "m");
+  chk(v, at::kFloat, n, "v");
+  chk(w16, at::kBFloat16, n, "w16");
+  for (const Tensor* s : {&lr, &step, &sumsq})
+    TORCH_CHECK(s->is_cuda() && s->scalar_type() == at::kFloat && s->numel() == 1, "adamw scalars must be fp32[1]");
+  ok(T_::adamw(p.data_ptr<float>(), bp(g), m.data_ptr<float>(), v.data_ptr<float>(), bp(w16), n, lr.data_ptr<float>(),
+               step.data_ptr<float>(), (float)b1, (float)b2, (float)eps, (float)wd, sumsq.data_ptr<float>(),
+               (float)max_norm, stream()),
+     "adamw");
+}
+
+void check_attn(int64_t B, int64_t Tn, int64_t H) {
+  TORCH_CHECK(B > 0 && H > 0 && Tn > 0 && Tn % 128 == 0, "attention: T must be a positive multiple of 128");
+  TORCH_CHECK(B * Tn * 3 * H * 64 < (1ll << 31), "attention: tensor too large for 32-bit row indexing");
+}
+
+void attn_fwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, int64_t B, int64_t Tn, int64_t H,
+              double sm_scale) {
+  check_attn(B, Tn, H);
+  chk(qkv, at::kBFloat16, B * Tn * 3 * H * 64, "qkv");
+  chk(o, at::kBFloat16, B * Tn * H * 64, "o");
+  chk(lse, at::kFloat, B * H * Tn, "lse");
+  ok(T_::attn_fwd(bp(qkv), bp(o), lse.data_ptr<float>(), (int)B, (int)Tn, (int)H, (float)sm_scale, stream()),
+     "attn_fwd");
+}
+
+void attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& dout, const Tensor& lse, const Tensor& delta,
+              const Tensor& dqkv, int64_t B, int64_t Tn, int64_t H, double sm_scale) {
+  check_attn(B, Tn, H);
+  chk(qkv, at::kBFloat16, B * Tn * 3 * H * 64, "qkv");
+  chk(o, at::kBFloat16, B * Tn * H * 64, "o");
+  chk(dout, at::kBFloat16, B * Tn * H * 64, "dout");
+  chk(lse, at::kFloat, B * H * Tn, "lse");
+  chk(delta, at::kFloat, B * H * Tn, "delta");
+  chk(dqkv, at::kBFloat16, B * Tn * 3 * H * 64, "dqkv");
+  ok(T_::attn_bwd(bp(qkv), bp(o), bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bp(dqkv), (int)B,
+                  (int)Tn, (int)H, (float)sm_scale, stream()),
+     "attn_bwd");
+}
+
+}  // namespace
+
+void register_transformer(py::module& m) {
+  m.def("ln_fwd", &ln_fwd, "residual add + LayerNorm forward (fp32 stream, bf16 out)");
+  m.def("ln_bwd", &ln_bwd, "LayerNorm backward (+ residual grad), per-block dgamma/dbeta partials");
+  m.def("ln_bwd_blocks", &ln_bwd_blocks);
+  m.def("ln_reduce", &ln_reduce, "sum LayerNorm parameter-gradient partials into bf16 grads");
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("xent_fwd", &xent_fwd, "vocabulary cross-entropy forward (per-row loss and lse)");
+  m.def("xent_bwd", &xent_bwd, "cross-entropy backward, in place over the logits");
+  m.def("grad_sumsq", &grad_sumsq);
+  m.def("adamw", &adamw, "flat AdamW with global-norm clip, writes bf16 shadow weights");
+  m.def("attn_fwd", &attn_fwd, "causal flash attention forward, head dim 64 (MFMA)");
+  m.def("attn_bwd", &attn_bwd, "causal flash attention backward (delta, dK/dV, dQ)");
+}

@@ -1,0 +1,237 @@
+"""GPT-2 as a flat-buffer functional network with a hand-written backward.
+
+The PBT trial of BASELINE config 5 trains GPT-2 small (124M parameters). Instead of
+autograd over ``nn.Module`` parameters (per-parameter gradient tensors, an extra
+accumulate kernel per parameter, autocast re-casting every weight each forward), the
+whole model lives in five flat buffers:
+
+* ``p32``  fp32 master weights          * ``m``, ``v``  AdamW moments (fp32)
+* ``w16``  bf16 shadow weights the GEMMs read (written by the AdamW kernel)
+* ``g16``  bf16 gradients, every slice written exactly once per step by the backward
+
+so one optimizer launch (global-norm clip + AdamW + bf16 cast) updates every parameter,
+a checkpoint is five contiguous buffers (``state_dict``/``load_state_dict`` keep the
+``nn.Module`` names of :class:`katib_amd.workloads.gpt2_pbt.GPT`), and the whole step
+(forward, backward, optimizer) is one HIP-graph replay. Plain GEMMs go to hipBLASLt
+(``torch.addmm``/``torch.mm`` with ``out=`` straight into the gradient slices); LayerNorm,
+GELU, attention, cross-entropy and AdamW are the kernels of :mod:`katib_amd.ops.transformer`.
+
+The residual stream is fp32 ([B*T, d]); its gradient is one fp32 buffer updated in
+place through the whole backward. The tied LM head uses a vocabulary padded to a
+multiple of 64 (50257 -> 50304) so logits rows are 16-byte aligned; pad rows of the
+embedding stay zero and the cross-entropy kernels ignore the pad columns.
+
+The reference's own trial images delegate all of this to framework autograd (e.g.
+``examples/v1beta1/trial-images/pytorch-mnist/mnist.py:32-48``); GPT-2 is new scope from
+BASELINE.json config 5.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Tuple
+
+import torch
+import torch.nn.functional as F
+
+
+def _pad8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+@dataclass
+class Spec:
+    name: str
+    shape: Tuple[int, ...]
+    init: str  # normal | normal_proj | zeros | ones
+    off: int = 0
+    store_shape: Tuple[int, ...] = ()
+
+    @property
+    def numel(self) -> int:
+        n = 1
+        for s in self.store_shape or self.shape:
+            n *= s
+        return n
+
+
+class GPT2Flat:
+    def __init__(self, cfg, device, ops, dtype=torch.bfloat16, seed: int = 0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.ops = ops
+        self.dtype = dtype
+        self.V = cfg.vocab
+        self.Vp = (cfg.vocab + 63) // 64 * 64
+        d = cfg.d
+        specs: List[Spec] = [Spec("wte.weight", (cfg.vocab, d), "normal", store_shape=(self.Vp, d)),
+                             Spec("wpe.weight", (cfg.ctx, d), "normal")]
+        for i in range(cfg.n_layer):
+            pre = "blocks.%d." % i
+            specs += [Spec(pre + "ln1.weight", (d,), "ones"), Spec(pre + "ln1.bias", (d,), "zeros"),
+                      Spec(pre + "qkv.weight", (3 * d, d), "normal"), Spec(pre + "qkv.bias", (3 * d,), "zeros"),
+                      Spec(pre + "proj.weight", (d, d), "normal_proj"), Spec(pre + "proj.bias", (d,), "zeros"),
+                      Spec(pre + "ln2.weight", (d,), "ones"), Spec(pre + "ln2.bias", (d,), "zeros"),
+                      Spec(pre + "fc.weight", (4 * d, d), "normal"), Spec(pre + "fc.bias", (4 * d,), "zeros"),
+                      Spec(pre + "fc2.weight", (d, 4 * d), "normal_proj"), Spec(pre + "fc2.bias", (d,), "zeros")]
+        specs += [Spec("ln_f.weight", (d,), "ones"), Spec("ln_f.bias", (d,), "zeros")]
+        off = 0
+        for s in specs:
+            s.off = off
+            off += _pad8(s.numel)
+        self.specs = {s.name: s for s in specs}
+        self.order = [s.name for s in specs]
+        self.P = off
+        dev = self.device
+        self.p32 = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.w16 = torch.zeros(off, device=dev, dtype=dtype)
+        self.g16 = torch.zeros(off, device=dev, dtype=dtype)
+        self.m = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.v = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
+        self.lr_t = torch.full((1,), 3e-4, device=dev, dtype=torch.float32)
+        self.sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
+        self.gscale = torch.ones(1, device=dev, dtype=torch.float32)
+        self.p = {n: self._view(self.p32, n) for n in self.order}
+        self.w = {n: self._view(self.w16, n) for n in self.order}
+        self.g = {n: self._view(self.g16, n) for n in self.order}
+        self._init(seed)
+
+    # ---------------------------------------------------------------- parameters
+    def _view(self, buf, name):
+        s = self.specs[name]
+        return buf[s.off:s.off + s.numel].view(s.store_shape or s.shape)
+
+    def _init(self, seed):
+        gen = torch.Generator(device="cpu").manual_seed(seed)
+        std_proj = 0.02 / math.sqrt(2 * self.cfg.n_layer)
+        for n in self.order:
+            s = self.specs[n]
+            if s.init == "ones":
+                t = torch.ones(s.shape)
+            elif s.init == "zeros":
+                t = torch.zeros(s.shape)
+            else:
+                t = torch.randn(s.shape, generator=gen) * (0.02 if s.init == "normal" else std_proj)
+            self.p[n][:s.shape[0]].copy_(t)
+        self.w16.copy_(self.p32)
+
+    def n_params(self) -> int:
+        return sum(math.prod(self.specs[n].shape) for n in self.order if n != "wpe.weight")
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {n: self.p[n][:self.specs[n].shape[0]] for n in self.order}
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]):
+        for n in self.order:
+            s = self.specs[n]
+            t = sd[n]
+            if tuple(t.shape) != s.shape:
+                raise ValueError("%s: checkpoint shape %s != model shape %s" % (n, tuple(t.shape), s.shape))
+            self.p[n][:s.shape[0]].copy_(t)
+        self.w16.copy_(self.p32)
+
+    def optim_state(self) -> Dict[str, torch.Tensor]:
+        return {"exp_avg": self.m, "exp_avg_sq": self.v, "step": self.step_t}
+
+    def load_optim_state(self, st: Dict[str, torch.Tensor]):
+        self.m.copy_(st["exp_avg"])
+        self.v.copy_(st["exp_avg_sq"])
+        self.step_t.copy_(st["step"].reshape(1))
+
+    # ---------------------------------------------------------------- forward
+    def _lin(self, x, name):
+        return torch.addmm(self.w[name + ".bias"], x, self.w[name + ".weight"].t())
+
+    def _embed(self, idx):
+        B, T = idx.shape
+        x = F.embedding(idx.reshape(-1), self.w["wte.weight"]).float()
+        return (x.view(B, T, -1) + self.w["wpe.weight"][:T].float()).view(B * T, -1)
+
+    def forward(self, idx, save: bool = False):
+        """Logits [B*T, Vp] (pad columns are zero-weight rows; ignore them)."""
+        c, ops = self.cfg, self.ops
+        B, T = idx.shape
+        H = c.n_head
+        resid = self._embed(idx)
+        pending = None
+        acts = []
+        for i in range(c.n_layer):
+            pre = "blocks.%d." % i
+            sa, h1, mu1, rs1 = ops.ln_fwd(resid, pending, self.w[pre + "ln1.weight"], self.w[pre + "ln1.bias"])
+            qkv = self._lin(h1, pre + "qkv")
+            o, lse = ops.attn_fwd(qkv, B, T, H, c.d // H)
+            a = self._lin(o, pre + "proj")
+            sb, h2, mu2, rs2 = ops.ln_fwd(sa, a, self.w[pre + "ln2.weight"], self.w[pre + "ln2.bias"])
+            u = self._lin(h2, pre + "fc")
+            gl = ops.gelu_fwd(u)
+            pending = self._lin(gl, pre + "fc2")
+            resid = sb
+            if save:
+                acts.append((sa, h1, mu1, rs1, qkv, o, lse, sb, h2, mu2, rs2, u, gl))
+        sf, hf, muf, rsf = ops.ln_fwd(resid, pending, self.w["ln_f.weight"], self.w["ln_f.bias"])
+        logits = torch.mm(hf, self.w["wte.weight"].t())
+        if save:
+            self._saved = (acts, sf, hf, muf, rsf)
+        return logits
+
+    # ---------------------------------------------------------------- training step
+    def forward_backward(self, idx, tgt):
+        """Mean next-token cross-entropy; fills every slice of ``g16``."""
+        c, ops = self.cfg, self.ops
+        B, T = idx.shape
+        M, H, d = B * T, c.n_head, c.d
+        tgt = tgt.reshape(-1)
+        logits = self.forward(idx, save=True)
+        acts, sf, hf, muf, rsf = self._saved
+        self._saved = None
+        loss_rows, lse_ce = ops.xent_fwd(logits, tgt, self.V)
+        loss = loss_rows.mean()
+        dlog = ops.xent_bwd(logits, tgt, lse_ce, self.gscale, self.V)
+        g = self.g
+        torch.mm(dlog.t(), hf, out=g["wte.weight"])  # tied LM head (pad rows get 0)
+        dh = torch.mm(dlog, self.w["wte.weight"])
+        del dlog, logits
+        G = torch.empty((M, d), device=self.device, dtype=torch.float32)  # residual-stream gradient
+        dr = torch.empty((M, d), device=self.device, dtype=self.dtype)
+        ops.ln_bwd(dh, sf, muf, rsf, self.w["ln_f.weight"], G, dr, g["ln_f.weight"], g["ln_f.bias"],
+                   accumulate=False)
+        for i in reversed(range(c.n_layer)):
+            pre = "blocks.%d." % i
+            sa, h1, mu1, rs1, qkv, o, lse, sb, h2, mu2, rs2, u, gl = acts.pop()
+            # MLP: dr is the gradient of fc2's output
+            torch.mm(dr.t(), gl, out=g[pre + "fc2.weight"])
+            torch.sum(dr, 0, out=g[pre + "fc2.bias"])
+            du = ops.gelu_bwd(u, torch.mm(dr, self.w[pre + "fc2.weight"]))
+            torch.mm(du.t(), h2, out=g[pre + "fc.weight"])
+            torch.sum(du, 0, out=g[pre + "fc.bias"])
+            dh2 = torch.mm(du, self.w[pre + "fc.weight"])
+            del du
+            ops.ln_bwd(dh2, sb, mu2, rs2, self.w[pre + "ln2.weight"], G, dr, g[pre + "ln2.weight"],
+                       g[pre + "ln2.bias"])
+            # attention: dr is now the gradient of proj's output
+            torch.mm(dr.t(), o, out=g[pre + "proj.weight"])
+            torch.sum(dr, 0, out=g[pre + "proj.bias"])
+            do = torch.mm(dr, self.w[pre + "proj.weight"])
+            dqkv = ops.attn_bwd(qkv, o, do, lse, B, T, H, d // H)
+            torch.mm(dqkv.t(), h1, out=g[pre + "qkv.weight"])
+            torch.sum(dqkv, 0, out=g[pre + "qkv.bias"])
+            dh1 = torch.mm(dqkv, self.w[pre + "qkv.weight"])
+            del dqkv
+            ops.ln_bwd(dh1, sa, mu1, rs1, self.w[pre + "ln1.weight"], G, dr if i > 0 else None,
+                       g[pre + "ln1.weight"], g[pre + "ln1.bias"])
+        # embeddings: G is the gradient of wte[idx] + wpe[:T]
+        Gb = G.to(self.dtype)
+        g["wte.weight"].index_add_(0, idx.reshape(-1), Gb)
+        gw = g["wpe.weight"]
+        torch.sum(Gb.view(B, T, d), 0, out=gw[:T])
+        if T < gw.shape[0]:
+            gw[T:].zero_()
+        return loss
+
+    def optimizer_step(self, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, max_norm=1.0):
+        """AdamW on the flat buffers; ``lr_t`` (device scalar) is the learning rate."""
+        self.step_t.add_(1.0)
+        self.ops.adamw(self.p32, self.g16, self.m, self.v, self.w16, self.lr_t, self.step_t, beta1, beta2, eps,
+                       weight_decay, max_norm, self.sumsq)

@@ -1,0 +1,210 @@
+"""Transformer ops for the GPT-2 trial: two interchangeable backends.
+
+* :class:`HipOps`   - the hand-written gfx950 kernels of ``csrc/hip/transformer.hip``
+  (fused residual-add LayerNorm, tanh GELU, vocabulary cross-entropy with the gradient
+  written in place, flat AdamW with global-norm clipping that emits the bf16 shadow
+  weights, causal flash attention forward/backward on MFMA). bf16 activations, fp32
+  residual stream and statistics.
+* :class:`TorchOps` - plain PyTorch implementations of exactly the same contracts
+  (any dtype, any device); the numerical oracle for the HIP kernels and the CPU path.
+
+Contracts (``M`` rows, ``D`` features, ``Vp`` padded vocabulary of which ``V`` are real):
+
+``ln_fwd(x32, r, gamma, beta) -> (xin, y, mean, rstd)``
+    ``xin = x32 + r`` (fp32; ``x32`` itself when ``r`` is None), ``y = LN(xin)``.
+``ln_bwd(dy, xin, mean, rstd, gamma, G, dr, dgamma, dbeta)``
+    ``G += LN'(dy)`` in place (``G`` fp32 residual-stream gradient; ``G`` is *set* when
+    ``accumulate=False``), ``dr[:] = G`` cast to the activation dtype when ``dr`` is given,
+    ``dgamma/dbeta`` written.
+``attn_fwd(qkv, B, T, H) -> (o, lse)``
+    causal softmax attention with head dim 64; ``qkv`` is ``[B*T, 3*H*64]`` (q | k | v, heads
+    contiguous), ``o`` is ``[B*T, H*64]``, ``lse`` ``[B, H, T]`` = log2-sum-exp2 of the
+    scaled scores (in log2 units).
+``xent_fwd(logits, tgt, V) -> (loss_rows, lse)``; ``xent_bwd(logits, tgt, lse, gscale, V)``
+    writes ``(softmax - onehot) * gscale / N`` over ``logits`` in place.
+"""
+
+from __future__ import annotations
+
+import importlib
+import math
+
+import torch
+import torch.nn.functional as F
+
+LOG2E = 1.4426950408889634
+
+
+def _kern():
+    try:
+        return importlib.import_module("katib_amd._hipkern")
+    except ImportError as e:
+        raise ImportError("katib_amd._hipkern is not built (run __graft_entry__.build()): %s" % e)
+
+
+class TorchOps:
+    name = "torch"
+
+    def __init__(self, eps: float = 1e-5):
+        self.eps = eps
+
+    # ---------------------------------------------------------------- LayerNorm
+    def ln_fwd(self, x32, r, gamma, beta):
+        xin = x32 if r is None else x32 + r.float()
+        mean = xin.mean(-1)
+        var = ((xin - mean[:, None]) ** 2).mean(-1)
+        rstd = torch.rsqrt(var + self.eps)
+        y = ((xin - mean[:, None]) * rstd[:, None] * gamma.float() + beta.float()).to(gamma.dtype)
+        return xin, y, mean, rstd
+
+    def ln_bwd(self, dy, xin, mean, rstd, gamma, G, dr, dgamma, dbeta, accumulate=True):
+        D = xin.shape[-1]
+        g = dy.float()
+        xh = (xin - mean[:, None]) * rstd[:, None]
+        dxh = g * gamma.float()
+        dx = rstd[:, None] * (dxh - dxh.sum(-1, keepdim=True) / D - xh * (dxh * xh).sum(-1, keepdim=True) / D)
+        if accumulate:
+            G.add_(dx)
+        else:
+            G.copy_(dx)
+        if dr is not None:
+            dr.copy_(G)
+        dgamma.copy_((g * xh).sum(0))
+        dbeta.copy_(g.sum(0))
+
+    # ---------------------------------------------------------------- GELU
+    def gelu_fwd(self, u):
+        return F.gelu(u.float(), approximate="tanh").to(u.dtype)
+
+    def gelu_bwd(self, u, dy):
+        x = u.float()
+        k0, k1 = math.sqrt(2.0 / math.pi), 0.044715
+        t = torch.tanh(k0 * (x + k1 * x ** 3))
+        d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+        return (dy.float() * d).to(u.dtype)
+
+    # ---------------------------------------------------------------- attention
+    def attn_fwd(self, qkv, B, T, H, hd=64):
+        q, k, v = qkv.float().view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+        s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
+        mask = torch.ones(T, T, dtype=torch.bool, device=qkv.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+        lse = torch.logsumexp(s, -1)
+        o = torch.softmax(s, -1) @ v
+        return o.permute(0, 2, 1, 3).reshape(B * T, H * hd).to(qkv.dtype), lse * LOG2E
+
+    def attn_bwd(self, qkv, o, dout, lse, B, T, H, hd=64):
+        with torch.enable_grad():
+            x = qkv.detach().float().requires_grad_(True)
+            q, k, v = x.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+            s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
+            mask = torch.ones(T, T, dtype=torch.bool, device=qkv.device).triu(1)
+            p = torch.softmax(s.masked_fill(mask, float("-inf")), -1)
+            out = (p @ v).permute(0, 2, 1, 3).reshape(B * T, H * hd)
+            (g,) = torch.autograd.grad(out, x, dout.float())
+        return g.to(qkv.dtype)
+
+    # ---------------------------------------------------------------- cross-entropy
+    def xent_fwd(self, logits, tgt, V):
+        x = logits[:, :V].float()
+        lse = torch.logsumexp(x, -1)
+        return lse - x.gather(1, tgt[:, None])[:, 0], lse
+
+    def xent_bwd(self, logits, tgt, lse, gscale, V):
+        N = logits.shape[0]
+        p = torch.exp(logits[:, :V].float() - lse[:, None])
+        p[torch.arange(N, device=logits.device), tgt] -= 1.0
+        logits[:, :V] = (p * (gscale.float() / N)).to(logits.dtype)
+        logits[:, V:] = 0
+        return logits
+
+    # ---------------------------------------------------------------- optimizer
+    def adamw(self, p, g, m, v, w16, lr, step, b1, b2, eps, wd, max_norm, sumsq):
+        gf = g.float()
+        sumsq.copy_((gf * gf).sum().reshape(1))
+        if max_norm > 0:
+            gf = gf * torch.clamp(max_norm / (sumsq.sqrt() + 1e-6), max=1.0)
+        t = step.float()
+        bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+        m.mul_(b1).add_(gf, alpha=1 - b1)
+        v.mul_(b2).addcmul_(gf, gf, value=1 - b2)
+        p.mul_(1 - lr * wd)
+        p.sub_(lr / bc1 * m / (v.sqrt() / bc2.sqrt() + eps))
+        w16.copy_(p)
+
+
+class HipOps:
+    """The gfx950 kernels. Raises at construction if the extension is missing."""
+
+    name = "hip"
+
+    def __init__(self, eps: float = 1e-5):
+        self.k = _kern()
+        self.eps = eps
+        self._ones = {}
+
+    def ln_fwd(self, x32, r, gamma, beta):
+        M, D = x32.shape
+        xin = x32 if r is None else torch.empty_like(x32)
+        y = torch.empty((M, D), device=x32.device, dtype=torch.bfloat16)
+        mean = torch.empty(M, device=x32.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        self.k.ln_fwd(x32, r, None if r is None else xin, gamma, beta, y, mean, rstd, self.eps)
+        return xin, y, mean, rstd
+
+    def ln_bwd(self, dy, xin, mean, rstd, gamma, G, dr, dgamma, dbeta, accumulate=True):
+        M, D = xin.shape
+        nb = self.k.ln_bwd_blocks(M)
+        part = torch.empty((2, nb, D), device=xin.device, dtype=torch.float32)
+        self.k.ln_bwd(dy, xin, mean, rstd, gamma, G if accumulate else None, G, dr, part[0], part[1])
+        self.k.ln_reduce(part[0], part[1], dgamma, dbeta)
+
+    def gelu_fwd(self, u):
+        g = torch.empty_like(u)
+        self.k.gelu_fwd(u, g)
+        return g
+
+    def gelu_bwd(self, u, dy):
+        du = torch.empty_like(u)
+        self.k.gelu_bwd(u, dy, du)
+        return du
+
+    def attn_fwd(self, qkv, B, T, H, hd=64):
+        assert hd == 64
+        o = torch.empty((B * T, H * hd), device=qkv.device, dtype=torch.bfloat16)
+        lse = torch.empty((B, H, T), device=qkv.device, dtype=torch.float32)
+        self.k.attn_fwd(qkv, o, lse, B, T, H, 1.0 / math.sqrt(hd))
+        return o, lse
+
+    def attn_bwd(self, qkv, o, dout, lse, B, T, H, hd=64):
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty_like(lse)
+        self.k.attn_bwd(qkv, o, dout, lse, delta, dqkv, B, T, H, 1.0 / math.sqrt(hd))
+        return dqkv
+
+    def xent_fwd(self, logits, tgt, V):
+        N = logits.shape[0]
+        loss = torch.empty(N, device=logits.device, dtype=torch.float32)
+        lse = torch.empty_like(loss)
+        self.k.xent_fwd(logits, tgt, loss, lse, V)
+        return loss, lse
+
+    def xent_bwd(self, logits, tgt, lse, gscale, V):
+        self.k.xent_bwd(logits, tgt, lse, gscale, 1.0 / logits.shape[0], V)
+        return logits
+
+    def adamw(self, p, g, m, v, w16, lr, step, b1, b2, eps, wd, max_norm, sumsq):
+        sumsq.zero_()
+        self.k.grad_sumsq(g, sumsq)
+        self.k.adamw(p, g, m, v, w16, lr, step, b1, b2, eps, wd, sumsq, max_norm)
+
+
+def get_ops(name: str = "auto", device=None):
+    """``hip`` (fails loudly without the extension), ``torch``, or ``auto`` (hip on a GPU)."""
+    if name == "auto":
+        name = "hip" if (device is not None and torch.device(device).type == "cuda") else "torch"
+    if name == "hip":
+        return HipOps()
+    if name == "torch":
+        return TorchOps()
+    raise ValueError("unknown transformer ops backend %r" % name)

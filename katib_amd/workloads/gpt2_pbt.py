@@ -6,10 +6,15 @@ prepares the trial's checkpoint directory from the parent's, reference
 the trial's hyperparameters, evaluates, and writes its own checkpoint back.
 
 Model: GPT-2 small (12 layers, d=768, 12 heads, context 1024, vocab 50257, tied
-embeddings, GELU MLP, pre-LayerNorm) - 124M parameters. MI355X specifics: bf16
-autocast with fp32 master weights, fused AdamW (``foreach``), flash attention
-through ``scaled_dot_product_attention``, synthetic Markov-chain tokens resident in
-HBM, train step captured as a HIP graph.
+embeddings, GELU MLP, pre-LayerNorm) - 124M parameters. On MI355X (``--impl flat``,
+the default on a GPU) the model is :class:`katib_amd.models.gpt2.GPT2Flat`: flat fp32
+master / bf16 shadow / bf16 gradient buffers, a hand-written backward, the gfx950
+kernels of ``csrc/hip/transformer.hip`` (flash attention, fused residual LayerNorm,
+GELU, vocabulary cross-entropy, one-launch AdamW with global-norm clipping) around
+hipBLASLt GEMMs, the whole step (forward, backward, optimizer) replayed as one HIP
+graph. ``--impl module`` is the plain ``nn.Module`` + autocast + ``torch.optim.AdamW``
+path (the CPU default and the numerical oracle). Data: synthetic Markov-chain tokens
+resident in HBM.
 
 Checkpoints: the parent's state is fetched GPU-to-GPU from the warm worker that
 trained it (:mod:`katib_amd.parallel.p2p_ckpt`, peer copy over xGMI); ``model.pt`` +
@@ -32,6 +37,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..models.gpt2 import GPT2Flat
+from ..ops.transformer import get_ops
 from ..parallel import p2p_ckpt
 from .common import CapturedStep, Timer, device, markov_tokens, report
 
@@ -122,11 +129,28 @@ def parse_args(argv):
     p.add_argument("--capture", type=int, default=1)
     p.add_argument("--p2p", type=int, default=1, help="hand checkpoints GPU-to-GPU (parallel.p2p_ckpt)")
     p.add_argument("--save-files", type=int, default=1, help="also write model.pt/optim.pt (durable copy)")
+    p.add_argument("--impl", default="auto", choices=["auto", "flat", "module"],
+                   help="flat: flat-buffer model on the HIP kernels (GPU default); module: nn.Module + autograd")
+    p.add_argument("--ops", default="auto", choices=["auto", "hip", "torch"], help="kernel backend of --impl flat")
     return p.parse_args(argv)
 
 
 def _ckpt_dir(args):
     return args.checkpoint_dir or os.environ.get("KATIB_TRIAL_CHECKPOINT_DIR", "")
+
+
+def _load_state(model, opt, st, flat: bool) -> bool:
+    """Load a {"model", "optim", "step"} checkpoint into either implementation; the
+    optimizer moments carry over only between like implementations."""
+    model.load_state_dict(st["model"])
+    o = st.get("optim")
+    if flat and isinstance(o, dict) and "exp_avg" in o:
+        model.load_optim_state(o)
+        return True
+    if not flat and isinstance(o, dict) and "state" in o:
+        opt.load_state_dict(o)
+        return True
+    return False
 
 
 def main(argv=None):
@@ -138,36 +162,32 @@ def main(argv=None):
     T = args.seq_len or cfg.ctx
     toks = markov_tokens(args.num_tokens, vocab=cfg.vocab, seed=99, dev=dev)
     n_train = int(len(toks) * 0.9)
-    model = GPT(cfg).to(dev)
-    opt = torch.optim.AdamW(model.parameters(), lr=args.lr, betas=(0.9, 0.95), weight_decay=args.weight_decay,
-                            fused=cuda, foreach=not cuda, capturable=cuda)
+    flat = (args.impl == "flat") or (args.impl == "auto" and cuda)
+    if flat:
+        ops = get_ops(args.ops if args.ops != "auto" else ("hip" if cuda else "torch"), dev)
+        model = GPT2Flat(cfg, dev, ops, dtype=torch.bfloat16 if cuda else torch.float32, seed=args.seed)
+        opt = None
+    else:
+        model = GPT(cfg).to(dev)
+        opt = torch.optim.AdamW(model.parameters(), lr=args.lr, betas=(0.9, 0.95), weight_decay=args.weight_decay,
+                                fused=cuda, foreach=not cuda, capturable=cuda)
     start_step = 0
     ck = _ckpt_dir(args)
     source = "init"
     t_load = time.time()
     st = p2p_ckpt.fetch(ck, dev) if (ck and cuda and args.p2p) else None  # parent's weights, GPU to GPU
     if st is not None:
-        model.load_state_dict(st["model"])
-        opt.load_state_dict(st["optim"])
-        start_step = int(st["step"])
         source = "p2p"
     elif ck and os.path.exists(os.path.join(ck, "model.pt")):
-        model.load_state_dict(torch.load(os.path.join(ck, "model.pt"), map_location=dev, weights_only=True))
-        st = torch.load(os.path.join(ck, "optim.pt"), map_location=dev, weights_only=True)
-        opt.load_state_dict(st["optim"])
-        start_step = int(st["step"])
+        ost = torch.load(os.path.join(ck, "optim.pt"), map_location=dev, weights_only=True)
+        st = {"model": torch.load(os.path.join(ck, "model.pt"), map_location=dev, weights_only=True),
+              "optim": ost["optim"], "step": ost["step"]}
         source = "file"
-    if source != "init":
-        report(checkpoint_source=source, checkpoint_load_seconds=time.time() - t_load)
-    for g in opt.param_groups:  # the trial's (possibly perturbed) hyperparameters
-        g["lr"] = args.lr
-        g["weight_decay"] = args.weight_decay
-    lr_t = torch.tensor(args.lr, device=dev) if cuda else args.lr
-    if cuda:
-        for g in opt.param_groups:
-            g["lr"] = lr_t
-    for p_ in model.parameters():
-        p_.grad = torch.zeros_like(p_)
+    if st is not None:
+        moments = _load_state(model, opt, st, flat)
+        start_step = int(st["step"])
+        report(checkpoint_source=source, checkpoint_load_seconds=time.time() - t_load,
+               checkpoint_optimizer_state=int(moments))
     B = args.batch_size
     offs = torch.zeros(B, dtype=torch.long, device=dev)
     ar = torch.arange(T + 1, device=dev)
@@ -177,53 +197,78 @@ def main(argv=None):
         w = toks[(o[:, None] + ar[None, :])]
         return w[:, :-1], w[:, 1:]
 
-    def train_step():
-        xb, yb = batch(offs)
-        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda):
-            logits = model(xb)
-        loss = F.cross_entropy(logits.float().view(-1, cfg.vocab), yb.reshape(-1))
-        opt.zero_grad(set_to_none=False)
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        opt.step()
-        loss_buf.copy_(loss.detach())
-        return loss_buf
+    if flat:
+        def train_step():
+            xb, yb = batch(offs)
+            loss = model.forward_backward(xb, yb)
+            model.optimizer_step(weight_decay=args.weight_decay, max_norm=1.0)
+            loss_buf.copy_(loss.detach())
+            return loss_buf
+
+        def set_lr(v):
+            model.lr_t.fill_(v)
+    else:
+        for g in opt.param_groups:  # the trial's (possibly perturbed) hyperparameters
+            g["lr"] = args.lr
+            g["weight_decay"] = args.weight_decay
+        lr_t = torch.tensor(args.lr, device=dev) if cuda else args.lr
+        if cuda:
+            for g in opt.param_groups:
+                g["lr"] = lr_t
+        for p_ in model.parameters():
+            p_.grad = torch.zeros_like(p_)
+
+        def train_step():
+            xb, yb = batch(offs)
+            with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda):
+                logits = model(xb)
+            loss = F.cross_entropy(logits.float().view(-1, cfg.vocab), yb.reshape(-1))
+            opt.zero_grad(set_to_none=False)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step()
+            loss_buf.copy_(loss.detach())
+            return loss_buf
+
+        def set_lr(v):
+            if cuda:
+                lr_t.fill_(v)
+            else:
+                for g in opt.param_groups:
+                    g["lr"] = v
 
     step = CapturedStep(train_step, enabled=bool(args.capture))
     gen = torch.Generator(device=dev).manual_seed(args.seed * 1000 + start_step)
     timer = Timer()
     for i in range(args.steps):
         s = start_step + i
-        warm = min(1.0, (s + 1) / max(args.warmup, 1))
-        if cuda:
-            lr_t.fill_(args.lr * warm)
-        else:
-            for g in opt.param_groups:
-                g["lr"] = args.lr * warm
+        set_lr(args.lr * min(1.0, (s + 1) / max(args.warmup, 1)))
         offs.copy_(torch.randint(0, n_train - T - 1, (B,), device=dev, generator=gen))
         step()
         if (i + 1) % 10 == 0 or i == args.steps - 1:
             report(step=s + 1, loss=float(loss_buf))
     elapsed = timer.elapsed()
-    model.eval()
+    if not flat:
+        model.eval()
     tot, correct, n = 0.0, 0.0, 0
-    with torch.no_grad(), torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda):
+    with torch.no_grad(), torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda and not flat):
         eg = torch.Generator(device=dev).manual_seed(7)
         for _ in range(args.eval_batches):
             o = torch.randint(n_train, len(toks) - T - 1, (B,), device=dev, generator=eg)
             xb, yb = batch(o)
-            logits = model(xb).float()
+            logits = (model.forward(xb)[:, :cfg.vocab] if flat else model(xb)).float()
             tot += float(F.cross_entropy(logits.view(-1, cfg.vocab), yb.reshape(-1), reduction="sum"))
-            correct += float((logits.argmax(-1) == yb).sum())
+            correct += float((logits.view(-1, cfg.vocab).argmax(-1) == yb.reshape(-1)).sum())
             n += yb.numel()
     if ck:
         os.makedirs(ck, exist_ok=True)
         end_step = start_step + args.steps
+        optim_state = model.optim_state() if flat else opt.state_dict()
         if cuda and args.p2p:
-            p2p_ckpt.publish({"model": model.state_dict(), "optim": opt.state_dict(), "step": end_step}, ck)
+            p2p_ckpt.publish({"model": model.state_dict(), "optim": optim_state, "step": end_step}, ck)
         if args.save_files:
             torch.save(model.state_dict(), os.path.join(ck, "model.pt"))
-            torch.save({"optim": opt.state_dict(), "step": end_step}, os.path.join(ck, "optim.pt"))
+            torch.save({"optim": optim_state, "step": end_step}, os.path.join(ck, "optim.pt"))
     tokens_per_s = args.steps * B * T / max(elapsed, 1e-9)
     report(**{"Validation-loss": tot / n, "Validation-accuracy": correct / n, "tokens_per_s": tokens_per_s})
     return tot / n
