@@ -43,6 +43,12 @@ hipError_t adamw(float* p, const bf16* g, float* m, float* v, bf16* w16, int64_t
                  const float* step, float beta1, float beta2, float eps, float wd, const float* sumsq,
                  float max_norm, hipStream_t st);
 
+// out[c] = bf16(sum_r part[r][c]) (split-K / partial-sum reduction), n % 4 == 0.
+hipError_t reduce_rows(const float* part, int R, int64_t n, bf16* out, hipStream_t st);
+// out[c] = bf16(sum_r x[r][c]) for x [M, N] bf16 (N % 8 == 0); part: fp32 [colsum_chunks(M, N)][N] scratch.
+int colsum_chunks(int M, int N);
+hipError_t colsum(const bf16* x, int M, int N, float* part, bf16* out, hipStream_t st);
+
 // Causal flash attention, head dim 64. qkv [B, T, 3, H, 64] bf16; o [B, T, H, 64] bf16;
 // lse [B, H, T] fp32 in the log2 domain of the scaled scores. T % 128 == 0.
 hipError_t attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, float sm_scale, hipStream_t st);

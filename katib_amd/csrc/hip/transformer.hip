@@ -379,6 +379,47 @@ __global__ __launch_bounds__(256) void adamw_k(float* __restrict__ p, const u16*
   }
 }
 
+// ============================================================== column sums / split-K partial reduction
+// out[c] = bf16(sum_r part[r][c]); n % 4 == 0
+__global__ __launch_bounds__(256) void reduce_rows_k(const float* __restrict__ part, int R, int64_t n,
+                                                     u16* __restrict__ out) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    f32x4 s = reinterpret_cast<const f32x4*>(part)[i];
+#pragma unroll 8
+    for (int r = 1; r < R; ++r) s += reinterpret_cast<const f32x4*>(part + (int64_t)r * n)[i];
+    reinterpret_cast<u32x2*>(out)[i] = u32x2{pack2(s[0], s[1]), pack2(s[2], s[3])};
+  }
+}
+
+// part[chunk][c] = sum over the chunk's rows of x[r][c]; block = 16 column vectors (8 bf16) x 16 row groups
+__global__ __launch_bounds__(256) void colsum_k(const u16* __restrict__ x, int M, int N, int rows,
+                                                float* __restrict__ part) {
+  __shared__ f32x4 red[16][16][2];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int cv = blockIdx.x * 16 + tx;
+  const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = a;
+  if (cv * 8 < N) {
+#pragma unroll 4
+    for (int r = r0 + ty; r < r1; r += 16) {
+      const u32x4 q = *reinterpret_cast<const u32x4*>(x + (int64_t)r * N + cv * 8);
+      a += f32x4{lo2f(q[0]), hi2f(q[0]), lo2f(q[1]), hi2f(q[1])};
+      b += f32x4{lo2f(q[2]), hi2f(q[2]), lo2f(q[3]), hi2f(q[3])};
+    }
+  }
+  red[ty][tx][0] = a;
+  red[ty][tx][1] = b;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int c = threadIdx.x & 15, h = threadIdx.x >> 4;
+    f32x4 s = red[0][c][h];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) s += red[k][c][h];
+    if ((blockIdx.x * 16 + c) * 8 < N) reinterpret_cast<f32x4*>(part + (int64_t)blockIdx.y * N + (blockIdx.x * 16 + c) * 8)[h] = s;
+  }
+}
+
 // ============================================================== flash attention (head dim 64)
 constexpr int HD = 64;
 constexpr int LDK = HD + 8;  // LDS row pitch in bf16 (144 B: 16-B padded rows)
@@ -904,6 +945,26 @@ hipError_t adamw(float* p, const bf16* g, float* m, float* v, bf16* w16, int64_t
   hipLaunchKernelGGL(adamw_k, dim3(grid_for(n, 4)), dim3(256), 0, st, p, reinterpret_cast<const u16*>(g), m, v,
                      reinterpret_cast<u16*>(w16), n / 4, lr, step, beta1, beta2, eps, wd, sumsq, max_norm);
   return hipGetLastError();
+}
+
+hipError_t reduce_rows(const float* part, int R, int64_t n, bf16* out, hipStream_t st) {
+  hipLaunchKernelGGL(reduce_rows_k, dim3(grid_for(n, 4)), dim3(256), 0, st, part, R, n, reinterpret_cast<u16*>(out));
+  return hipGetLastError();
+}
+
+int colsum_chunks(int M, int N) {
+  const int cb = (N / 8 + 15) / 16;
+  int R = 1024 / cb;
+  R = R < 1 ? 1 : (R > 64 ? 64 : R);
+  const int max_r = (M + 15) / 16;  // >= 16 rows per chunk
+  return R > max_r ? max_r : R;
+}
+
+hipError_t colsum(const bf16* x, int M, int N, float* part, bf16* out, hipStream_t st) {
+  const int R = colsum_chunks(M, N), rows = (M + R - 1) / R;
+  hipLaunchKernelGGL(colsum_k, dim3((N / 8 + 15) / 16, R), dim3(256), 0, st, reinterpret_cast<const u16*>(x), M, N,
+                     rows, part);
+  return reduce_rows(part, R, N, out, st);
 }
 
 hipError_t attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, float sm_scale, hipStream_t st) {

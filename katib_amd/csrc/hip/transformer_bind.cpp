@@ -160,6 +160,24 @@ void adamw(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v, c
      "adamw");
 }
 
+void reduce_rows(const Tensor& part, const Tensor& out) {
+  const int64_t n = out.numel();
+  TORCH_CHECK(n > 0 && n % 4 == 0 && part.numel() % n == 0, "reduce_rows: part must be [R, n], n % 4 == 0");
+  chk(part, at::kFloat, part.numel(), "part");
+  chk(out, at::kBFloat16, n, "out");
+  ok(T_::reduce_rows(part.data_ptr<float>(), (int)(part.numel() / n), n, bp(out), stream()), "reduce_rows");
+}
+
+void colsum(const Tensor& x, const Tensor& out) {
+  TORCH_CHECK(x.dim() == 2, "colsum: x must be [M, N]");
+  const int64_t M = x.size(0), N = x.size(1);
+  TORCH_CHECK(N % 8 == 0 && M > 0 && M < (1ll << 31), "colsum: N % 8 == 0");
+  chk(x, at::kBFloat16, M * N, "x");
+  chk(out, at::kBFloat16, N, "out");
+  auto part = at::empty({T_::colsum_chunks((int)M, (int)N), N}, x.options().dtype(at::kFloat));
+  ok(T_::colsum(bp(x), (int)M, (int)N, part.data_ptr<float>(), bp(out), stream()), "colsum");
+}
+
 void check_attn(int64_t B, int64_t Tn, int64_t H) {
   TORCH_CHECK(B > 0 && H > 0 && Tn > 0 && Tn % 128 == 0, "attention: T must be a positive multiple of 128");
   TORCH_CHECK(B * Tn * 3 * H * 64 < (1ll << 31), "attention: tensor too large for 32-bit row indexing");
@@ -202,6 +220,8 @@ void register_transformer(py::module& m) {
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward, in place over the logits");
   m.def("grad_sumsq", &grad_sumsq);
   m.def("adamw", &adamw, "flat AdamW with global-norm clip, writes bf16 shadow weights");
+  m.def("reduce_rows", &reduce_rows, "bf16 out = sum of fp32 partial rows (split-K reduction)");
+  m.def("colsum", &colsum, "bf16 column sums of a [M, N] bf16 matrix (bias gradients)");
   m.def("attn_fwd", &attn_fwd, "causal flash attention forward, head dim 64 (MFMA)");
   m.def("attn_bwd", &attn_bwd, "causal flash attention backward (delta, dK/dV, dQ)");
 }

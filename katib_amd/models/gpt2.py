@@ -201,22 +201,22 @@ class GPT2Flat:
             pre = "blocks.%d." % i
             sa, h1, mu1, rs1, qkv, o, lse, sb, h2, mu2, rs2, u, gl = acts.pop()
             # MLP: dr is the gradient of fc2's output
-            torch.mm(dr.t(), gl, out=g[pre + "fc2.weight"])
-            torch.sum(dr, 0, out=g[pre + "fc2.bias"])
+            ops.wgrad(dr, gl, g[pre + "fc2.weight"])
+            ops.colsum(dr, g[pre + "fc2.bias"])
             du = ops.gelu_bwd(u, torch.mm(dr, self.w[pre + "fc2.weight"]))
-            torch.mm(du.t(), h2, out=g[pre + "fc.weight"])
-            torch.sum(du, 0, out=g[pre + "fc.bias"])
+            ops.wgrad(du, h2, g[pre + "fc.weight"])
+            ops.colsum(du, g[pre + "fc.bias"])
             dh2 = torch.mm(du, self.w[pre + "fc.weight"])
             del du
             ops.ln_bwd(dh2, sb, mu2, rs2, self.w[pre + "ln2.weight"], G, dr, g[pre + "ln2.weight"],
                        g[pre + "ln2.bias"])
             # attention: dr is now the gradient of proj's output
-            torch.mm(dr.t(), o, out=g[pre + "proj.weight"])
-            torch.sum(dr, 0, out=g[pre + "proj.bias"])
+            ops.wgrad(dr, o, g[pre + "proj.weight"])
+            ops.colsum(dr, g[pre + "proj.bias"])
             do = torch.mm(dr, self.w[pre + "proj.weight"])
             dqkv = ops.attn_bwd(qkv, o, do, lse, B, T, H, d // H)
-            torch.mm(dqkv.t(), h1, out=g[pre + "qkv.weight"])
-            torch.sum(dqkv, 0, out=g[pre + "qkv.bias"])
+            ops.wgrad(dqkv, h1, g[pre + "qkv.weight"])
+            ops.colsum(dqkv, g[pre + "qkv.bias"])
             dh1 = torch.mm(dqkv, self.w[pre + "qkv.weight"])
             del dqkv
             ops.ln_bwd(dh1, sa, mu1, rs1, self.w[pre + "ln1.weight"], G, dr if i > 0 else None,

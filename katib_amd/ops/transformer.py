@@ -118,6 +118,13 @@ class TorchOps:
         logits[:, V:] = 0
         return logits
 
+    # ---------------------------------------------------------------- GEMM helpers
+    def colsum(self, x, out):
+        torch.sum(x, 0, out=out)
+
+    def wgrad(self, dy, x, out):
+        torch.mm(dy.t(), x, out=out)
+
     # ---------------------------------------------------------------- optimizer
     def adamw(self, p, g, m, v, w16, lr, step, b1, b2, eps, wd, max_norm, sumsq):
         gf = g.float()
@@ -141,7 +148,7 @@ class HipOps:
     def __init__(self, eps: float = 1e-5):
         self.k = _kern()
         self.eps = eps
-        self._ones = {}
+        self._bmm_f32 = True
 
     def ln_fwd(self, x32, r, gamma, beta):
         M, D = x32.shape
@@ -192,6 +199,32 @@ class HipOps:
     def xent_bwd(self, logits, tgt, lse, gscale, V):
         self.k.xent_bwd(logits, tgt, lse, gscale, 1.0 / logits.shape[0], V)
         return logits
+
+    def colsum(self, x, out):
+        """Bias gradient: bf16 column sums of [M, N] (two-stage, fp32 partials)."""
+        self.k.colsum(x, out)
+
+    def wgrad(self, dy, x, out):
+        """``out = dy^T x`` ([N, K] from [M, N], [M, K]). The reduction over M = B*T tokens is
+        long and the output small (768 x 768 = 36 tiles of 128^2 for the attention
+        projection), so split it S ways into a batched GEMM with fp32 output and add the
+        slabs with one kernel: >= 512 output tiles fill the 256 CUs."""
+        M, N = dy.shape
+        K = x.shape[1]
+        tiles = -(-N // 128) * -(-K // 128)
+        S = 1
+        while tiles * S < 512 and M % (2 * S) == 0 and M // (2 * S) >= 1024:
+            S *= 2
+        if S == 1 or not self._bmm_f32:
+            torch.mm(dy.t(), x, out=out)
+            return
+        try:
+            part = torch.bmm(dy.view(S, M // S, N).transpose(1, 2), x.view(S, M // S, K), out_dtype=torch.float32)
+        except (RuntimeError, TypeError, NotImplementedError):
+            self._bmm_f32 = False  # this stack's bmm has no fp32-output bf16 path
+            torch.mm(dy.t(), x, out=out)
+            return
+        self.k.reduce_rows(part.view(S, N * K), out.view(-1))
 
     def adamw(self, p, g, m, v, w16, lr, step, b1, b2, eps, wd, max_norm, sumsq):
         sumsq.zero_()

@@ -240,14 +240,19 @@ def main(argv=None):
     step = CapturedStep(train_step, enabled=bool(args.capture))
     gen = torch.Generator(device=dev).manual_seed(args.seed * 1000 + start_step)
     timer = Timer()
+    steady = min(5, args.steps // 3)  # steps before this one include graph capture
+    t_steady, elapsed = None, 0.0
     for i in range(args.steps):
         s = start_step + i
+        if i == steady:
+            t_steady = Timer()
         set_lr(args.lr * min(1.0, (s + 1) / max(args.warmup, 1)))
         offs.copy_(torch.randint(0, n_train - T - 1, (B,), device=dev, generator=gen))
         step()
         if (i + 1) % 10 == 0 or i == args.steps - 1:
             report(step=s + 1, loss=float(loss_buf))
     elapsed = timer.elapsed()
+    steady_s = t_steady.elapsed() if t_steady is not None else elapsed
     if not flat:
         model.eval()
     tot, correct, n = 0.0, 0.0, 0
@@ -269,7 +274,8 @@ def main(argv=None):
         if args.save_files:
             torch.save(model.state_dict(), os.path.join(ck, "model.pt"))
             torch.save({"optim": optim_state, "step": end_step}, os.path.join(ck, "optim.pt"))
-    tokens_per_s = args.steps * B * T / max(elapsed, 1e-9)
+    tokens_per_s = (args.steps - steady) * B * T / max(steady_s, 1e-9) if t_steady is not None else \
+        args.steps * B * T / max(elapsed, 1e-9)
     report(**{"Validation-loss": tot / n, "Validation-accuracy": correct / n, "tokens_per_s": tokens_per_s})
     return tot / n
 

@@ -178,3 +178,18 @@ def test_gpt2_trial_captured_flat(tmp_path):
     assert v_flat < math.log(1000) - 0.3 and v_mod < math.log(1000) - 0.3
     assert abs(v_flat - v_mod) < 0.15, (v_flat, v_mod)
     assert v_cont < math.log(1000) - 1.0  # continued from the flat checkpoint (5 steps from scratch: ~6.8)
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (16384, 3072, 768), (4096, 768, 3072), (300, 64, 40)])
+def test_wgrad_and_colsum(ops, M, N, K):
+    hip, _ = ops
+    g = _gen()
+    dy = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    out = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+    hip.wgrad(dy, x, out)
+    ref = dy.float().t() @ x.float()
+    assert _rel(out, ref) < 1e-2
+    b = torch.empty(N, device=DEV, dtype=torch.bfloat16)
+    hip.colsum(dy, b)
+    assert _rel(b, dy.float().sum(0)) < 1e-2
