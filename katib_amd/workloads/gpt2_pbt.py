@@ -245,6 +245,8 @@ def main(argv=None):
     for i in range(args.steps):
         s = start_step + i
         if i == steady:
+            if cuda:
+                torch.cuda.synchronize()
             t_steady = Timer()
         set_lr(args.lr * min(1.0, (s + 1) / max(args.warmup, 1)))
         offs.copy_(torch.randint(0, n_train - T - 1, (B,), device=dev, generator=gen))
