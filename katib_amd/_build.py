@@ -51,6 +51,32 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_selftest(sanitize: str = "address,undefined", out_dir: str = "", verbose: bool = False) -> str:
+    """Standalone native self-test executable (csrc/native/tests/native_selftest.cpp) linked
+    with the runtime sources, optionally under ``-fsanitize=<sanitize>`` (host code only:
+    ``address,undefined`` or ``thread``); sanitizer runtimes are linked statically so the
+    binary runs without any preloading."""
+    srcs = [s for s in sorted(glob.glob(os.path.join(NATIVE_SRC, "*.cpp"))) if not s.endswith("bindings.cpp")]
+    srcs.append(os.path.join(NATIVE_SRC, "tests", "native_selftest.cpp"))
+    deps = srcs + sorted(glob.glob(os.path.join(NATIVE_SRC, "*.hpp")))
+    tag = sanitize.replace(",", "_") if sanitize else "plain"
+    out_dir = out_dir or os.path.join(NATIVE_SRC, "build")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "native_selftest_" + tag)
+    if not _newer(out, deps):
+        return out
+    cmd = ["g++", "-O1", "-g", "-std=c++17", "-Wall", "-Wno-unused-result", f"-I{NATIVE_SRC}"]
+    if sanitize:
+        cmd += [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
+        cmd += ["-static-libtsan"] if "thread" in sanitize else ["-static-libasan", "-static-libubsan"]
+    cmd += srcs + ["-o", out + ".tmp", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def hip_target() -> str:
     return os.path.join(PKG_DIR, "_hipkern" + EXT_SUFFIX)
 

@@ -109,6 +109,10 @@ def cmd_run(a):
                 cols = ["trial", "status"] + [p.name for p in done.spec.parameters or []] + \
                     [done.spec.objective.objective_metric_name]
                 _print_table(rows, cols)
+        if a.trace:
+            m.tracer.export(a.trace)
+            for r_ in results:
+                r_["trace_phase_latencies_s"] = m.tracer.phase_latencies()
     finally:
         m.shutdown()
     print(json.dumps(results if len(results) != 1 else results[0], indent=None if a.json else 2))
@@ -309,6 +313,7 @@ def build_parser():
     r.add_argument("--namespace", default="default")
     r.add_argument("--timeout", type=float, default=24 * 3600)
     r.add_argument("--json", action="store_true")
+    r.add_argument("--trace", default=None, help="write the trial/suggestion timeline (Chrome trace JSON)")
     r.set_defaults(fn=cmd_run)
 
     s = sub.add_parser("serve", help="run the scheduler daemon with its HTTP API")

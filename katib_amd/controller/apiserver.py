@@ -91,6 +91,10 @@ class ApiServer:
             return 200, "text/plain", b"ok"
         if path == "/metrics":
             return 200, "text/plain; version=0.0.4", m.metrics.expose().encode()
+        if path == "/katib/trace":  # Chrome/Perfetto timeline of trials and suggestion calls
+            return _json(m.tracer.chrome_trace())
+        if path == "/katib/trace/latencies":
+            return _json(m.tracer.phase_latencies())
         if path == "/katib/observation_logs":
             logs = m.get_observation_log(_q(query, "trialName"), _q(query, "metricName", ""),
                                          _q(query, "startTime", ""), _q(query, "endTime", ""))

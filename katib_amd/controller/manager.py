@@ -44,6 +44,7 @@ from ..api.models import (V1beta1AlgorithmSetting, V1beta1EarlyStoppingRule, V1b
 from ..api.validation import ValidationError, is_restartable, validate_experiment
 from ..rpc import api_pb2 as api
 from ..utils.prometheus import Registry
+from ..utils.tracing import Tracer
 from . import gjson
 from .config import KatibConfig
 from .converters import comparison_from_pb, convert_experiment, convert_trials
@@ -132,6 +133,7 @@ class Manager:
         self._t0 = time.time()
         self._completed = 0
         self.fault_injector: Optional[Callable[[str, Key], bool]] = None
+        self.tracer = Tracer()  # trial / suggestion timeline (utils/tracing.py)
         self._install_default_templates()
 
     # ============================================================== public API (apiserver)
@@ -575,6 +577,7 @@ class Manager:
             self.trials[tkey] = trial
             self.metrics.inc("katib_trial_created_total", namespace=key[0])
             TC.mark_created(trial, C.TRIAL_CREATED_REASON, "Trial is created")
+            self.tracer.instant("trial.created", trial=tkey[1], experiment=exp.metadata.name)
             self.runs[tkey] = TrialRun()
         if done and not assignments:
             st = exp.status
@@ -665,7 +668,9 @@ class Manager:
                                         trials=convert_trials(trials), current_request_number=need,
                                         total_request_number=sug.spec.requests)
         try:
-            reply = svc.GetSuggestions(req)
+            with self.tracer.span("suggestion.GetSuggestions", experiment=exp.metadata.name,
+                                  algorithm=exp.spec.algorithm.algorithm_name, current_request_number=need):
+                reply = svc.GetSuggestions(req)
         except AlgorithmError as e:
             SC.mark_failed(sug, C.SUGGESTION_FAILED_REASON, e.message)
             return False
@@ -894,6 +899,8 @@ class Manager:
         run.phase = "Launching"
         run.started = time.time()
         trial.status.start_time = trial.status.start_time or now()
+        self.tracer.begin(name, "trial", track=("gpu" + ",".join(str(d) for d in run.devices)) if run.devices
+                          else "cpu", trial=name, experiment=exp_name, attempt=run.attempt)
         if self.fault_injector is not None and self.fault_injector("launch", tkey):
             raise RuntimeError("fault injected at launch")
         for rep in plan.replicas:
@@ -1072,6 +1079,10 @@ class Manager:
         trial = self.trials[tkey]
         run.phase, run.reason, run.message = phase, reason, message
         run.finished = time.time()
+        first = self._first_metric_time(tkey[1])
+        if first is not None:
+            self.tracer.instant("trial.first_metric", trial=tkey[1], at=first)
+        self.tracer.end(tkey[1], phase=phase, reason=reason)
         kind = run.plan.kind if run.plan else C.JOB_KIND_JOB
         status = job_status(kind, phase, reason, message)
         succeeded = gjson.matches(status, trial.spec.success_condition or "")
@@ -1109,6 +1120,18 @@ class Manager:
         if not trial.spec.retain_run:
             # the Job is deleted once the trial completed (trial_controller.go:297-306)
             self._event(trial, "Normal", C.JOB_DELETED_REASON, "Job %s has been deleted" % trial.metadata.name)
+
+    def _first_metric_time(self, trial_name: str) -> Optional[float]:
+        try:
+            logs = self.store.get(trial_name, "", "", "")
+        except Exception:
+            return None
+        ts = []
+        for lg in logs:
+            r = self.N.parse_rfc3339(str(lg[0])) if isinstance(lg, (tuple, list)) and lg else None
+            if r is not None:
+                ts.append(r[0] + r[1] * 1e-9)
+        return min(ts) if ts else None
 
     def _update_observation(self, trial):
         """UpdateTrialStatusObservation + getMetrics (trial_controller_util.go:124-217); the

@@ -35,6 +35,8 @@ from typing import Dict, List, Tuple
 import torch
 import torch.nn.functional as F
 
+from ..utils.tracing import gpu_range
+
 
 def _pad8(n: int) -> int:
     return (n + 7) // 8 * 8
@@ -183,7 +185,19 @@ class GPT2Flat:
         B, T = idx.shape
         M, H, d = B * T, c.n_head, c.d
         tgt = tgt.reshape(-1)
-        logits = self.forward(idx, save=True)
+        with gpu_range("gpt2.forward"):
+            logits = self.forward(idx, save=True)
+        return self._backward(idx, tgt, logits)
+
+    def _backward(self, idx, tgt, logits):
+        c, ops = self.cfg, self.ops
+        B, T = idx.shape
+        M, H, d = B * T, c.n_head, c.d
+        with gpu_range("gpt2.backward"):
+            return self._backward_body(idx, tgt, logits, B, T, M, H, d)
+
+    def _backward_body(self, idx, tgt, logits, B, T, M, H, d):
+        c, ops = self.cfg, self.ops
         acts, sf, hf, muf, rsf = self._saved
         self._saved = None
         loss_rows, lse_ce = ops.xent_fwd(logits, tgt, self.V)
@@ -233,5 +247,6 @@ class GPT2Flat:
     def optimizer_step(self, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, max_norm=1.0):
         """AdamW on the flat buffers; ``lr_t`` (device scalar) is the learning rate."""
         self.step_t.add_(1.0)
-        self.ops.adamw(self.p32, self.g16, self.m, self.v, self.w16, self.lr_t, self.step_t, beta1, beta2, eps,
-                       weight_decay, max_norm, self.sumsq)
+        with gpu_range("gpt2.adamw"):
+            self.ops.adamw(self.p32, self.g16, self.m, self.v, self.w16, self.lr_t, self.step_t, beta1, beta2, eps,
+                           weight_decay, max_norm, self.sumsq)

@@ -361,3 +361,31 @@ def test_function_kind_via_sdk_tune(manager):
     assert EC.is_succeeded(done), done.status.conditions
     assert client.get_optimal_hyperparameters("tune").best_trial_name
     assert done.status.trials_succeeded == 4
+
+
+def test_trial_timeline_trace(manager, tmp_path):
+    """utils/tracing: every trial leaves created -> launched -> first metric -> done, every
+    GetSuggestions call a span; the Chrome trace export is valid JSON with those events."""
+    import json
+    import os
+
+    e = load_experiment(os.path.join(os.path.dirname(__file__), "..", "examples", "hp-tuning",
+                                     "random-quadratic.yaml"))
+    e.spec.trial_template.trial_spec["spec"]["template"]["spec"]["containers"][0]["command"][0] = PY
+    e.spec.max_trial_count = 3
+    manager.create_experiment(e)
+    done = manager.run_until_complete("random-quadratic", timeout=120)
+    assert EC.is_succeeded(done)
+    tr = manager.tracer
+    names = [t.metadata.name for t in manager.list_trials("random-quadratic")]
+    for n in names:
+        kinds = [(ev["name"], ev["ph"]) for ev in tr.trial_timeline(n)]
+        assert ("trial.created", "i") in kinds and ("trial", "B") in kinds and ("trial", "E") in kinds
+        assert ("trial.first_metric", "i") in kinds
+    assert any(ev["name"] == "suggestion.GetSuggestions" for ev in tr.events)
+    lat = tr.phase_latencies()
+    assert lat["run_s"] > 0 and lat["queue_s"] >= 0
+    path = tmp_path / "trace.json"
+    tr.export(str(path))
+    doc = json.loads(path.read_text())
+    assert any(ev.get("name") == "trial" and ev.get("ph") == "b" for ev in doc["traceEvents"])
