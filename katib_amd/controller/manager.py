@@ -1030,6 +1030,18 @@ class Manager:
         # primary replica finished: stop the rest of the job
         for aux in run.aux:
             self.runtime.kill_trial(aux, False)
+        if self.fault_injector is not None:
+            act = self.fault_injector("exit", tkey)
+            if act == "crash":
+                ev = dict(ev, exit_code=1, early_stopped=False)
+            elif act == "drop_metrics":
+                self.store.remove(tkey[1])
+            elif act == "gpu_fault":
+                ev = dict(ev, exit_code=139, signal=11, early_stopped=False)
+        if ev["signal"] in (6, 11) and run.devices:
+            # a trial that died on SIGSEGV/SIGABRT on a GPU counts as a device fault
+            for d in run.devices:
+                self.slots.record_fault(int(d), self.config.amd.fault_quarantine_threshold)
         self._release(run)
         if run.deleted:
             return

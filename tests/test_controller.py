@@ -389,3 +389,61 @@ def test_trial_timeline_trace(manager, tmp_path):
     tr.export(str(path))
     doc = json.loads(path.read_text())
     assert any(ev.get("name") == "trial" and ev.get("ph") == "b" for ev in doc["traceEvents"])
+
+
+def _cond(t, typ):
+    return any(c.type == typ and c.status == "True" for c in t.status.conditions)
+
+
+def test_fault_injection_paths(manager):
+    """controller/faults.FaultPlan drives each failure path deterministically: a launch
+    failure, a crash on exit, dropped metrics; the rest of the trials succeed."""
+    from katib_amd.controller.faults import FaultPlan
+
+    plan = FaultPlan().add("launch", "fail", index=0).add("exit", "crash", index=1).add("exit", "drop_metrics", index=2)
+    manager.fault_injector = plan
+    e = quadratic_yaml(name="faults", parallel=1, max_trials=5, max_failed=4)
+    manager.create_experiment(e)
+    done = manager.run_until_complete("faults", timeout=120)
+    trials = sorted(manager.list_trials("faults"), key=lambda t: plan._order.get(t.metadata.name, 99))
+    assert [a for _, _, a in plan.log] == ["fail", "crash", "drop_metrics"]
+    assert _cond(trials[0], "Failed") and "LaunchError" in trials[0].status.conditions[-1].reason
+    assert _cond(trials[1], "Failed")  # crash, backoffLimit 0
+    assert _cond(trials[2], "MetricsUnavailable")
+    assert all(_cond(t, "Succeeded") for t in trials[3:])
+    assert done.status.trials_succeeded == 2
+
+
+def test_gpu_fault_quarantines_device(tmp_path):
+    """A trial dying on SIGSEGV on a GPU records a device fault; the device is quarantined at
+    the configured threshold and later trials are placed on the remaining devices."""
+    from katib_amd.controller.faults import FaultPlan
+    from katib_amd.controller.manager import Manager
+
+    m = Manager(state_dir=str(tmp_path / "state"), num_devices=2, journal=False)
+    try:
+        m.config.amd.fault_quarantine_threshold = 2
+        m.fault_injector = FaultPlan().add("exit", "gpu_fault", index=None, times=2)
+        e = quadratic_yaml(name="gfault", parallel=1, max_trials=4, max_failed=4, extra_spec="""
+trialTemplate:
+  primaryContainerName: training-container
+  trialParameters: [{name: a, reference: a}, {name: b, reference: b}]
+  trialSpec:
+    apiVersion: batch/v1
+    kind: Job
+    spec:
+      template:
+        spec:
+          containers:
+          - name: training-container
+            image: python
+            command: ["%s", "-c", "print('result=${trialParameters.a}${trialParameters.b}'[:8])"]
+            resources: {limits: {amd.com/gpu: 1}}
+          restartPolicy: Never
+""" % PY)
+        m.create_experiment(e)
+        done = m.run_until_complete("gfault", timeout=120)
+        assert done.status.trials_failed == 2 and done.status.trials_succeeded == 2
+        assert len(m.slots.quarantined()) >= 1
+    finally:
+        m.shutdown()
