@@ -444,6 +444,7 @@ void fold_f64(std::vector<py::tuple> segs) {
 void register_xgmi(py::module& m);  // xgmi_bind.cpp
 void register_conv(py::module& m);  // conv_bind.cpp
 void register_transformer(py::module& m);  // transformer_bind.cpp
+void register_batchnorm(py::module& m);  // batchnorm_bind.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, transformer, xGMI all-reduce)";
@@ -463,4 +464,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_xgmi(m);
   register_conv(m);
   register_transformer(m);
+  register_batchnorm(m);
 }

@@ -4,7 +4,9 @@
 (3x3 stem, no max-pool, [2, 2, 2, 2] basic blocks, 64-512 channels). MI355X
 specifics: channels-last activations, bf16 autocast (fp32 master weights), every
 convolution on the hand-written implicit-GEMM MFMA kernels (``ops/conv.py``,
-``--conv torch`` switches back to MIOpen), device-resident synthetic data, and the
+``--conv torch`` switches back to MIOpen), every batch norm with its residual add and
+ReLU fused on the NHWC kernels (``ops/batchnorm.py``, ``--bn torch`` for MIOpen),
+device-resident synthetic data, and the
 whole train step (forward, loss, backward, SGD+Nesterov momentum) captured as one
 HIP graph.
 
@@ -20,10 +22,22 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import batchnorm as hbn
 from ..ops import conv as hconv
 from .common import CapturedStep, Timer, device, pattern_images, report
 
 Conv = hconv.Conv2d  # HIP implicit GEMM on GPU, stock nn.Conv2d on CPU
+BN = hbn.BatchNorm2d  # HIP NHWC batch norm (+ residual + ReLU) on GPU, stock module on CPU
+
+
+class _TorchBN(nn.BatchNorm2d):
+    """MIOpen batch norm with the same (residual, relu) calling convention."""
+
+    def forward(self, x, residual=None, relu=False):
+        y = super().forward(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
 
 
 def parse_args(argv):
@@ -40,6 +54,7 @@ def parse_args(argv):
     p.add_argument("--capture", type=int, default=1)
     p.add_argument("--max-steps", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
     p.add_argument("--conv", default="hip", choices=["hip", "torch"], help="convolution backend on GPU")
+    p.add_argument("--bn", default="hip", choices=["hip", "torch"], help="batch-norm backend on GPU")
     return p.parse_args(argv)
 
 
@@ -47,24 +62,24 @@ class BasicBlock(nn.Module):
     def __init__(self, cin, cout, stride):
         super().__init__()
         self.conv1 = Conv(cin, cout, 3, stride, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(cout)
+        self.bn1 = BN(cout)
         self.conv2 = Conv(cout, cout, 3, 1, 1, bias=False)
-        self.bn2 = nn.BatchNorm2d(cout)
-        self.short = None
+        self.bn2 = BN(cout)
+        self.short_conv = self.short_bn = None
         if stride != 1 or cin != cout:
-            self.short = nn.Sequential(Conv(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+            self.short_conv, self.short_bn = Conv(cin, cout, 1, stride, bias=False), BN(cout)
 
     def forward(self, x):
-        out = F.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return F.relu(out + (x if self.short is None else self.short(x)))
+        out = self.bn1(self.conv1(x), relu=True)
+        sc = x if self.short_conv is None else self.short_bn(self.short_conv(x))
+        return self.bn2(self.conv2(out), residual=sc, relu=True)  # relu(bn2(conv2) + shortcut), one kernel
 
 
 class ResNet18(nn.Module):
     def __init__(self, width=64, classes=10):
         super().__init__()
         w = width
-        self.stem = nn.Sequential(Conv(3, w, 3, 1, 1, bias=False), nn.BatchNorm2d(w), nn.ReLU())
+        self.stem_conv, self.stem_bn = Conv(3, w, 3, 1, 1, bias=False), BN(w)
         layers, cin = [], w
         for i, cout in enumerate((w, 2 * w, 4 * w, 8 * w)):
             stride = 1 if i == 0 else 2
@@ -74,14 +89,15 @@ class ResNet18(nn.Module):
         self.fc = nn.Linear(cin, classes)
 
     def forward(self, x):
-        x = self.layers(self.stem(x))
+        x = self.layers(self.stem_bn(self.stem_conv(x), relu=True))
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 
 def main(argv=None):
-    global Conv
+    global Conv, BN
     args = parse_args(argv if argv is not None else [])
     Conv = hconv.Conv2d if args.conv == "hip" else nn.Conv2d
+    BN = hbn.BatchNorm2d if args.bn == "hip" else _TorchBN
     dev = device()
     torch.manual_seed(args.seed)
     cuda = dev.type == "cuda"
