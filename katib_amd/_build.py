@@ -105,16 +105,28 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950") 
               "-D_GLIBCXX_USE_CXX11_ABI=" + str(int(torch._C._GLIBCXX_USE_CXX11_ABI)),
               "-fno-gpu-rdc", "-Wno-unused-result", "-Wno-deprecated-declarations"]
     inc = [f"-I{p}" for p in torch_inc + [py_inc, HIP_SRC]]
-    objs = []
+    objs, cmds = [], []
+    headers = sorted(glob.glob(os.path.join(HIP_SRC, "*.h")))
     for s in srcs:
         o = os.path.join(build_dir, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer(o, [s] + sorted(glob.glob(os.path.join(HIP_SRC, "*.h")))):
+        if force or _newer(o, [s] + headers):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            cmd = [hipcc] + common + inc + lang + ["-c", s, "-o", o]
+            cmds.append([hipcc] + common + inc + lang + ["-c", s, "-o", o])
+    # One hipcc per translation unit, run concurrently (bounded by MAX_JOBS / CPU count).
+    jobs = max(1, min(len(cmds) or 1, int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 4), 16))
+    pending, running = list(cmds), []
+    while pending or running:
+        while pending and len(running) < jobs:
+            cmd = pending.pop(0)
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
-            subprocess.check_call(cmd)
+            running.append((cmd, subprocess.Popen(cmd)))
+        cmd, proc = running.pop(0)
+        if proc.wait() != 0:
+            for _, p in running:
+                p.wait()
+            raise subprocess.CalledProcessError(proc.returncode, cmd)
     link = [hipcc, "-shared", "-fPIC", f"--offload-arch={arch}"] + objs + [
         f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
         f"-Wl,-rpath,{torch_lib}", "-o", out + ".tmp"]

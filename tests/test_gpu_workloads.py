@@ -26,7 +26,7 @@ def test_pbt_gpt2_p2p_handoff(tmp_path):
         e = load_experiment(os.path.join(EX, "pbt", "pbt-gpt2-small.yaml"))
         spec = e.spec.trial_template.trial_spec["spec"]
         spec["args"] = [a for a in spec["args"] if not a.startswith("--steps") and not a.startswith("--batch")] + [
-            "--model=tiny", "--steps=10", "--num-tokens=50000", "--batch-size=4"]
+            "--model=mini", "--steps=10", "--num-tokens=50000", "--batch-size=4"]
         for s in e.spec.algorithm.algorithm_settings:
             if s.name == "n_population":
                 s.value = "5"
