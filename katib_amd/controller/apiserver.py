@@ -28,6 +28,7 @@ same exceptions as the in-process one.
 from __future__ import annotations
 
 import json
+import os
 import re
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
@@ -99,6 +100,9 @@ class ApiServer:
             logs = m.get_observation_log(_q(query, "trialName"), _q(query, "metricName", ""),
                                          _q(query, "startTime", ""), _q(query, "endTime", ""))
             return _json({"metricLogs": [{"timeStamp": t, "metric": {"name": n, "value": v}} for t, n, v in logs]})
+        ui = self._ui(method, path.rstrip("/"), query, body)
+        if ui is not None:
+            return ui
         if path.rstrip("/") == "/katib/fetch_hp_job_info":
             return _json(self._hp_job_info(_q(query, "experimentName"), _q(query, "namespace")))
         if path.rstrip("/") == "/katib/fetch_hp_job_trial_info":
@@ -161,6 +165,102 @@ class ApiServer:
                 return _json(self._get(m.get_suggestion, name, ns, "suggestions").to_k8s())
             return _json({"items": [s.to_k8s() for s in m.list_suggestions(ns)]})
         raise _Err(405, "MethodNotAllowed", "%s not allowed on %s" % (method, path))
+
+    # ------------------------------------------------------------------ UI backend
+    def _ui(self, method, path, query, body):
+        """The UI backend routes of ``cmd/ui/v1beta1/main.go:48-70`` (handlers in
+        ``pkg/ui/v1beta1/backend.go``) on the in-process store, plus the single-page UI
+        (``ui/index.html``) at ``/`` and ``/katib/``. Returns None for other paths."""
+        m = self.m
+        if path in ("", "/katib") and method == "GET":
+            with open(os.path.join(os.path.dirname(__file__), "ui", "index.html"), "rb") as f:
+                return 200, "text/html; charset=utf-8", f.read()
+        if path == "/katib/fetch_experiments":  # backend.go:138-179, util.go:36-66 (ExperimentView)
+            ns = query.get("namespace") or [None]
+            out = []
+            for n in ns:
+                for e in m.list_experiments(n):
+                    conds = (e.status.conditions if e.status else None) or []
+                    view = {"name": e.metadata.name, "namespace": e.metadata.namespace,
+                            "type": "nas" if e.spec.nas_config is not None else "hp",
+                            "status": conds[-1].type if conds else ""}
+                    view.update(e.to_k8s().get("status") or {})
+                    out.append(view)
+            return _json(out)
+        if path == "/katib/create_experiment" and method == "POST":  # backend.go:86-136
+            data = _load_body(body)
+            doc = data.get("postData") if isinstance(data, dict) and "postData" in data else None
+            if doc is None:
+                raise _Err(500, "InternalError", "Couldn't load the 'postData' field of the request's data")
+            try:
+                out = m.create_experiment(V1beta1Experiment.from_k8s(doc))
+            except (ValidationError, ValueError) as e:
+                raise _Err(500, "InternalError", str(e))
+            return _json(out.to_k8s())
+        if path == "/katib/delete_experiment":  # backend.go:181-263
+            name, ns = _q(query, "experimentName"), _q(query, "namespace")
+            self._get(m.get_experiment, name, ns, "experiments")
+            m.delete_experiment(name, ns)
+            return self._ui(method, "/katib/fetch_experiments", {"namespace": [ns]}, b"")
+        if path == "/katib/fetch_experiment":  # backend.go:463-512
+            return _json(self._get(m.get_experiment, _q(query, "experimentName"), _q(query, "namespace"),
+                                   "experiments").to_k8s())
+        if path == "/katib/fetch_suggestion":  # backend.go:514-564
+            return _json(self._get(m.get_suggestion, _q(query, "suggestionName"), _q(query, "namespace"),
+                                   "suggestions").to_k8s())
+        if path == "/katib/fetch_trial":  # backend.go:566-615
+            return _json(self._get(m.get_trial, _q(query, "trialName"), _q(query, "namespace"),
+                                   "trials").to_k8s())
+        if path == "/katib/fetch_trial_logs":  # backend.go:617-700: the primary container's log
+            name, ns = _q(query, "trialName"), _q(query, "namespace")
+            self._get(m.get_trial, name, ns, "trials")
+            log = os.path.join(m.state_dir, "trials", ns, name, "metrics.log")
+            text = ""
+            if os.path.exists(log):
+                with open(log, errors="replace") as f:
+                    text = f.read()
+            return _json(text)
+        if path == "/katib/fetch_namespaces":  # backend.go:439-461
+            nss = {e.metadata.namespace for e in m.list_experiments(None)} | {n for n, _, _ in m.configmaps.list()}
+            return _json(sorted(nss | {"default"}))
+        if path == "/katib/fetch_trial_templates":  # backend.go:265-289, util.go:80-130
+            return _json({"Data": self._templates_view()})
+        if path in ("/katib/add_template", "/katib/edit_template", "/katib/delete_template") and method == "POST":
+            return _json({"Data": self._update_template(path.rsplit("/", 1)[1].split("_")[0], _load_body(body))})
+        return None
+
+    def _templates_view(self):
+        by_ns = {}
+        for ns, name, data in self.m.configmaps.trial_templates():
+            by_ns.setdefault(ns, []).append({"ConfigMapName": name, "Templates": [
+                {"Path": k, "Yaml": v} for k, v in sorted(data.items())]})
+        return [{"ConfigMapNamespace": ns, "ConfigMaps": cms} for ns, cms in sorted(by_ns.items())]
+
+    def _update_template(self, action, data):
+        """``updateTrialTemplates`` (util.go:180-240): add / edit (rename path) / delete one
+        template entry; a ConfigMap left empty is deleted."""
+        ns, name = data["updatedConfigMapNamespace"], data["updatedConfigMapName"]
+        path = data["updatedConfigMapPath"]
+        store = self.m.configmaps
+        try:
+            templates = dict(store.get(ns, name))
+        except KeyError:
+            if action != "add":
+                raise _Err(500, "InternalError", 'configmaps "%s" not found' % name)
+            templates = {}
+        if action == "add":
+            templates[path] = data["updatedTemplateYaml"]
+        elif action == "edit":
+            templates.pop(data["configMapPath"], None)
+            templates[path] = data["updatedTemplateYaml"]
+        else:
+            templates.pop(path, None)
+        if templates:
+            self.m.add_configmap(ns, name, templates, {C.LABEL_TRIAL_TEMPLATE_CONFIGMAP_NAME:
+                                                       C.LABEL_TRIAL_TEMPLATE_CONFIGMAP_VALUE})
+        else:
+            store.delete(ns, name)
+        return self._templates_view()
 
     @staticmethod
     def _get(fn, name, ns, plural):

@@ -167,3 +167,59 @@ def test_suggestion_server_grpc():
             assert HealthStub(ch).Check(api.HealthCheckRequest(service="")).status == 1
     finally:
         _stop(p)
+
+
+def test_ui_backend_routes(manager):
+    """UI backend routes of cmd/ui/v1beta1/main.go:48-70 on the in-process server: index,
+    experiments CRUD, trial/suggestion fetch, trial logs, namespaces, template CRUD."""
+    import urllib.error
+    import urllib.request
+
+    from katib_amd.api.yaml_io import load_experiment
+    from katib_amd.controller.apiserver import ApiServer
+
+    srv = ApiServer(manager, port=0).start()
+    base = "http://127.0.0.1:%d" % srv.port
+
+    def call(path, body=None):
+        req = urllib.request.Request(base + path, data=None if body is None else json.dumps(body).encode(),
+                                     method="GET" if body is None else "POST")
+        try:
+            return urllib.request.urlopen(req).read()
+        except urllib.error.HTTPError as ex:
+            raise AssertionError("%s: %s" % (path, ex.read().decode()))
+
+    try:
+        assert b"Katib experiments" in call("/katib/")
+        e = load_experiment(EXAMPLE)
+        e.spec.max_trial_count, e.spec.parallel_trial_count, e.spec.max_failed_trial_count = 2, 1, 1
+        call("/katib/create_experiment/", {"postData": e.to_k8s()})
+        manager.run_until_complete("random-quadratic", timeout=120)
+        exps = json.loads(call("/katib/fetch_experiments/?namespace=default"))
+        assert [(x["name"], x["type"], x["status"]) for x in exps] == [("random-quadratic", "hp", "Succeeded")]
+        assert exps[0]["trialsSucceeded"] == 2
+        got = json.loads(call("/katib/fetch_experiment/?experimentName=random-quadratic&namespace=default"))
+        assert got["spec"]["maxTrialCount"] == 2
+        sug = json.loads(call("/katib/fetch_suggestion/?suggestionName=random-quadratic&namespace=default"))
+        assert sug["kind"] == "Suggestion"
+        trial = manager.list_trials("random-quadratic")[0].metadata.name
+        tj = json.loads(call("/katib/fetch_trial/?trialName=%s&namespace=default" % trial))
+        assert tj["metadata"]["name"] == trial
+        logs = json.loads(call("/katib/fetch_trial_logs/?trialName=%s&namespace=default" % trial))
+        assert "result=" in logs
+        assert "default" in json.loads(call("/katib/fetch_namespaces"))
+        # template add / edit / delete (util.go:180-240)
+        tpl = {"updatedConfigMapNamespace": "default", "updatedConfigMapName": "my-templates",
+               "updatedConfigMapPath": "a.yaml", "updatedTemplateYaml": "kind: Job\n"}
+        view = json.loads(call("/katib/add_template/", tpl))["Data"]
+        names = {(d["ConfigMapNamespace"], c["ConfigMapName"]) for d in view for c in d["ConfigMaps"]}
+        assert ("default", "my-templates") in names
+        view = json.loads(call("/katib/edit_template/", dict(tpl, configMapPath="a.yaml", updatedConfigMapPath="b.yaml",
+                                                               updatedTemplateYaml="kind: Job # v2\n")))["Data"]
+        cm = [c for d in view for c in d["ConfigMaps"] if c["ConfigMapName"] == "my-templates"][0]
+        assert cm["Templates"] == [{"Path": "b.yaml", "Yaml": "kind: Job # v2\n"}]
+        view = json.loads(call("/katib/delete_template/", dict(tpl, updatedConfigMapPath="b.yaml")))["Data"]
+        assert not [c for d in view for c in d["ConfigMaps"] if c["ConfigMapName"] == "my-templates"]
+        assert json.loads(call("/katib/delete_experiment/?experimentName=random-quadratic&namespace=default")) == []
+    finally:
+        srv.stop()
