@@ -216,12 +216,20 @@ class DartsSearch:
     def _segments(self):
         """List of (callable, collective-after) in order."""
         c = self.comm
+        hd = None
+        if self.device.type == "cuda":
+            from ..ops import darts as dops
+
+            if dops.backend() == "hip":
+                from ..ops import hip_darts as hd
+        begin = (lambda: hd.arena_begin(self.device)) if hd else (lambda: None)
+        end = hd.arena_end if hd else (lambda: None)
         return [
-            (lambda: self._seg_virtual(self.static["tx"], self.static["ty"]), [self.gW]),
+            (lambda: (begin(), self._seg_virtual(self.static["tx"], self.static["ty"])), [self.gW]),
             (lambda: self._seg_unrolled(self.static["vx"], self.static["vy"]), [self.gWv, self.gAv]),
             (lambda: self._seg_hessian(self.static["tx"], self.static["ty"]), [self.alpha_grad]),
             (lambda: (self._seg_alpha_step(), self._seg_weight(self.static["tx"], self.static["ty"])), [self.gW]),
-            (lambda: self._seg_weight_update(), []),
+            (lambda: (self._seg_weight_update(), end()), []),
         ]
 
     def _run_eager(self):

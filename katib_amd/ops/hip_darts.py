@@ -52,6 +52,56 @@ _CAP = {"combine_fwd": 3, "dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_b
 _REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
 
 
+class _Arena:
+    """Step-scoped fp64 workspace for the BN-statistics / reduction accumulators.
+
+    A DARTS step requests ~150 small zeroed fp64 buffers; zeroing each one was its own
+    fill launch. Between :func:`arena_begin` and :func:`arena_end` they are bump-allocated
+    from one buffer that is zeroed by a single launch at the start of the step (captured
+    into the step's HIP graph with the rest). The first step sizes the arena; buffers that
+    a captured graph may reference are never freed."""
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+        self.keep: List[torch.Tensor] = []
+        self.off = 0
+        self.used = 0
+        self.need = 0
+        self.active = False
+
+
+_ARENA = _Arena()
+
+
+def arena_begin(device):
+    a = _ARENA
+    if a.need and (a.buf is None or a.buf.numel() < a.need):
+        if a.buf is not None:
+            a.keep.append(a.buf)
+        a.buf = torch.zeros(a.need, dtype=F64, device=device)
+    elif a.buf is not None:
+        a.buf.zero_()
+    a.off, a.used, a.active = 0, 0, True
+
+
+def arena_end():
+    a = _ARENA
+    a.need = max(a.need, a.used)
+    a.active = False
+
+
+def zeros64(n: int, device) -> torch.Tensor:
+    a = _ARENA
+    if a.active:
+        step = (n + 31) // 32 * 32  # 256-byte aligned slices
+        a.used += step
+        if a.buf is not None and a.off + step <= a.buf.numel() and a.buf.device == device:
+            t = a.buf[a.off:a.off + n]
+            a.off += step
+            return t
+    return torch.zeros(n, dtype=F64, device=device)
+
+
 def register_grad_replicas(buf: torch.Tensor):
     """Declare ``buf`` ([REP][n] fp32, contiguous) a replicated gradient accumulator:
     ``.grad`` views into its row 0 receive kernel atomics into all REP rows."""
@@ -174,7 +224,7 @@ class _MixedNode(torch.autograd.Function):
             edges.append(_Edge(i, xs[i], ws[i], specs[i], bns[i], params[off:off + nparams[i]]))
             off += nparams[i]
         nslots = sum(e.spec.nbn for e in edges)
-        stats = torch.zeros(max(nslots, 1) * slot, dtype=F64, device=dev) if training else None
+        stats = zeros64(max(nslots, 1) * slot, dev) if training else None
         base = 0
         for e in edges:
             e.slot0 = base
@@ -300,7 +350,7 @@ class _MixedNode(torch.autograd.Function):
         for e in edges:
             e.nred = (len(e.zl) + 1) * C + 1
             sizes.append(REP * (e.nred + e.w.numel()))
-        buf = torch.zeros(sum(sizes), dtype=F64, device=dev)
+        buf = zeros64(sum(sizes), dev)
         o = 0
         calls, segs = [], []
         for e, sz in zip(edges, sizes):
@@ -327,7 +377,7 @@ class _MixedNode(torch.autograd.Function):
         # ---- separable convs: both second stages, one fold, both first stages
         seps = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("separable_convolution")]
         if seps:
-            red1 = torch.zeros(len(seps) * REP * 2 * C, dtype=F64, device=dev) if training else None
+            red1 = zeros64(len(seps) * REP * 2 * C, dev) if training else None
             pw2, dw2 = [], defaultdict(list)
             for n, (e, k, prim) in enumerate(seps):
                 K = int(prim[-1])
@@ -452,7 +502,7 @@ class _StdConvBN(torch.autograd.Function):
         Cout = w1.shape[0] * (2 if fr else 1)
         Ho, Wo = (H // 2, W // 2) if fr else (H, W)
         cnt = N * Ho * Wo
-        stats = torch.zeros(REP * 2 * Cout, dtype=F64, device=x.device) if training else None
+        stats = zeros64(REP * 2 * Cout, x.device) if training else None
         z = torch.empty(N, Cout, Ho, Wo, device=x.device)
         if fr:
             _K.pw_fwd([(x, w1, z, stats, 0, 0), (x, w2, z, stats, Cout // 2, 1)], 2)
@@ -474,7 +524,7 @@ class _StdConvBN(torch.autograd.Function):
         bn, fr, Cout, training = ctx.meta
         dout = dout.contiguous()
         nred = 2 * Cout + 1
-        red = torch.zeros(REP * nred, dtype=F64, device=x.device)
+        red = zeros64(REP * nred, x.device)
         if training:
             _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
             _K.fold_f64([(red, nred, nred)])
