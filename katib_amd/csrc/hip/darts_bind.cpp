@@ -446,6 +446,7 @@ void register_conv(py::module& m);  // conv_bind.cpp
 void register_transformer(py::module& m);  // transformer_bind.cpp
 void register_batchnorm(py::module& m);  // batchnorm_bind.cpp
 void register_mlp(py::module& m);  // mlp_bind.cpp
+void register_stem(py::module& m);  // stem_bind.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, transformer, xGMI all-reduce)";
@@ -467,4 +468,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_transformer(m);
   register_batchnorm(m);
   register_mlp(m);
+  register_stem(m);
 }

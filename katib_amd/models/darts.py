@@ -266,7 +266,11 @@ class DartsNetwork:
         L, ops = self.layout, self.ops
         wn = [F.softmax(a, dim=-1) for a in normal]
         wr = [F.softmax(a, dim=-1) for a in reduce]
-        s = F.conv2d(x, P["stem.conv"], padding=1)
+        hd = self.ops.hip_module() if self.ops.hip_enabled(x) else None
+        if hd is not None and hd.stem_supported(x, P["stem.conv"]):
+            s = hd.stem_conv(x, P["stem.conv"])
+        else:
+            s = F.conv2d(x, P["stem.conv"], padding=1)
         s = self._bn(s, "stem.bn", bn, training, P["stem.bn.weight"], P["stem.bn.bias"])
         s0 = s1 = s
         for ci, cell in enumerate(L.cells):

@@ -560,3 +560,51 @@ def supported(x: torch.Tensor, stride: int) -> bool:
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     return (C <= 256 and C * C <= 4096 and Wo <= 64 and 64 % Wo == 0 and Ho % (64 // Wo) == 0
             and H == Ho * stride and W == Wo * stride)
+
+
+# --------------------------------------------------------------------------------- stem
+class _StemConv(torch.autograd.Function):
+    """Stem Conv2d(Cin, C_stem, 3, padding=1, bias=False) (reference
+    ``examples/v1beta1/trial-images/darts-cnn-cifar10/model.py:90-93``) on the direct
+    stem kernels: forward + weight gradient; the data gradient (never needed for the
+    input image) falls back to ``torch.nn.grad.conv2d_input``."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x, w = x.contiguous(), w.contiguous()
+        N, _, H, W = x.shape
+        y = torch.empty(N, w.shape[0], H, W, device=x.device, dtype=x.dtype)
+        _K.stem_conv_fwd(x, w, y)
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        gx = gw = None
+        if ctx.needs_input_grad[1]:
+            chunks = stem_chunks(x, w.shape[0])
+            partial = torch.empty(chunks, w.numel(), device=x.device, dtype=torch.float32)
+            gw = torch.empty_like(w)
+            _K.stem_conv_wgrad(x, dy, partial, gw)
+        if ctx.needs_input_grad[0]:
+            gx = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=1)
+        return gx, gw
+
+
+def stem_chunks(x: torch.Tensor, cout: int) -> int:
+    """Pixel chunks of the weight-gradient grid: >= ~512 workgroups over (chunk, Cout),
+    each thread covering a handful of pixels."""
+    pixels = x.shape[0] * x.shape[2] * x.shape[3]
+    return max(1, min(pixels // 1024, max(16, 1024 // cout)))
+
+
+def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 4
+            and x.shape[1] in (1, 3) and tuple(w.shape[1:]) == (x.shape[1], 3, 3) and w.shape[0] <= 64
+            and x.numel() < (1 << 31) // 64)
+
+
+def stem_conv(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return _StemConv.apply(x, w)

@@ -201,3 +201,32 @@ def test_mixed_node_matches_torch(C, cell_idx, node):
     _close(gW_h, gW_t, "dW", rtol=1e-3, atol=1e-4)
     _close(m_h, m_t, "running_mean", rtol=1e-3, atol=1e-5)
     _close(v_h, v_t, "running_var", rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H", [(128, 3, 4, 32), (128, 3, 48, 32), (5, 3, 64, 7), (3, 1, 20, 28)])
+def test_stem_conv_vs_torch(N, Cin, Cout, H):
+    """Direct stem conv kernels (forward + weight gradient) vs F.conv2d in fp32."""
+    import torch.nn.functional as F
+
+    from katib_amd.ops import hip_darts as hd
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(N, Cin, H, H, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.3).to(dev)
+    dy = torch.randn(N, Cout, H, H, generator=g).to(dev)
+    assert hd.stem_supported(x, w)
+    w1 = w.clone().requires_grad_(True)
+    y = hd.stem_conv(x, w1)
+    y.backward(dy)
+    w2 = w.clone().requires_grad_(True)
+    yr = F.conv2d(x, w2, padding=1)
+    yr.backward(dy)
+    torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(w1.grad, w2.grad, rtol=1e-4, atol=1e-3 * (N * H * H) ** 0.5)
+    # the input-gradient fallback path
+    x1 = x.clone().requires_grad_(True)
+    hd.stem_conv(x1, w).backward(dy)
+    x2 = x.clone().requires_grad_(True)
+    F.conv2d(x2, w, padding=1).backward(dy)
+    torch.testing.assert_close(x1.grad, x2.grad, rtol=1e-4, atol=1e-4)
