@@ -336,6 +336,7 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdBatch bt) {
 // ------------------------------------------------------------------------------------------------
 // combine_fwd: out = sum_k w[k] * BN_k(z_k) + wid * x  (elementwise), running stats in block 0
 // ------------------------------------------------------------------------------------------------
+template <bool V4>
 __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
   // All edges of a node in one pass: out = sum_e [ sum_k w_e[k] * BN_ek(z_ek) + w_e[id] * x_e ].
   const CombineFwdArgs& a0 = bt.e[0];
@@ -371,6 +372,31 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
         b.rvar[c] = (1.f - a.momentum) * b.rvar[c] + a.momentum * (float)vu;
       }
     }
+  }
+  if (V4) {
+    // 4 consecutive elements per thread (HW % 4 == 0: one channel), 16-byte loads/stores;
+    // the host picks this path only when every operand pointer is 16-byte aligned
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const size_t total4 = total / 4;
+    for (size_t i4 = (size_t)blockIdx.x * 256 + threadIdx.x; i4 < total4; i4 += (size_t)gridDim.x * 256) {
+      const int c = (int)((i4 * 4 / HW) % C);
+      f4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < ne; ++e) {
+        const CombineFwdArgs& a = bt.e[e];
+        const float* sw = sW + e * (kMaxOps + 1);
+        for (int k = 0; k < a.nops; ++k) {
+          const int j = (e * kMaxOps + k) * C + c;
+          const float sc = sw[k] * sInv[j], sh = sc * sMean[j];
+          const f4 z = reinterpret_cast<const f4*>(a.z[k])[i4];
+          acc += z * sc - sh;
+        }
+        if (a.xid) acc += sw[kMaxOps] * reinterpret_cast<const f4*>(a.xid)[i4];
+      }
+      if (a0.gamma) acc = acc * a0.gamma[c] + a0.beta[c];
+      f4* o = reinterpret_cast<f4*>(a0.out) + i4;
+      *o = a0.accumulate ? *o + acc : acc;
+    }
+    return;
   }
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
     int c = (int)((i / HW) % C);
@@ -902,9 +928,16 @@ void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st) {
 void launch_combine_fwd(const CombineFwdBatch& b, hipStream_t st) {
   const CombineFwdArgs& a = b.e[0];
   size_t total = (size_t)a.N * a.C * a.HW;
-  int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
+  auto al16 = [](const void* p) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  bool v4 = a.HW % 4 == 0 && al16(a.out);
+  for (int e = 0; e < b.n && v4; ++e) {
+    v4 = al16(b.e[e].xid);
+    for (int k = 0; k < b.e[e].nops && v4; ++k) v4 = al16(b.e[e].z[k]);
+  }
+  int blocks = (int)std::min<size_t>(((v4 ? total / 4 : total) + 255) / 256, 2048);
   size_t lds = sizeof(float) * (2 * b.n * kMaxOps * a.C + b.n * (kMaxOps + 1));
-  hipLaunchKernelGGL(combine_fwd_kernel, dim3(blocks), dim3(256), lds, st, b);
+  if (v4) hipLaunchKernelGGL(combine_fwd_kernel<true>, dim3(blocks), dim3(256), lds, st, b);
+  else hipLaunchKernelGGL(combine_fwd_kernel<false>, dim3(blocks), dim3(256), lds, st, b);
 }
 
 void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st) {
