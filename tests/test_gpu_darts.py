@@ -230,3 +230,26 @@ def test_stem_conv_vs_torch(N, Cin, Cout, H):
     x2 = x.clone().requires_grad_(True)
     F.conv2d(x2, w, padding=1).backward(dy)
     torch.testing.assert_close(x1.grad, x2.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_combine_fwd_vector_and_scalar_paths(offset):
+    """combine_fwd takes the 16-byte vector path for aligned operands and the scalar path
+    otherwise (offset=1 shifts the BN input by one float); both match the fp32 formula
+    out = w0 * BN(z) + w_id * x (eval-mode BN from running statistics)."""
+    from katib_amd.ops import hip_darts as hd
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(3)
+    N, C, H, W = 4, 8, 16, 16
+    base = torch.randn(N * C * H * W + 1, generator=g).to(dev)
+    z = base[offset:offset + N * C * H * W].view(N, C, H, W)
+    x = torch.randn(N, C, H, W, generator=g).to(dev)
+    rm = (torch.randn(C, generator=g) * 0.1).to(dev)
+    rv = (torch.rand(C, generator=g) + 0.5).to(dev)
+    w = torch.tensor([0.7, 0.3], device=dev)
+    bn = hd._bn(None, rm, rv, N * H * W, False, 1e-5, C)
+    out = torch.empty(N, C, H, W, device=dev)
+    hd._K.combine_fwd([([z], [bn], [0], w, 1, x, [])], None, None, out, 0.1, False, False)
+    ref = 0.7 * (z - rm[None, :, None, None]) / torch.sqrt(rv[None, :, None, None] + 1e-5) + 0.3 * x
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
