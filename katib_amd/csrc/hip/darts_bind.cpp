@@ -232,7 +232,10 @@ void combine_fwd(std::vector<py::tuple> calls, OptT gamma, OptT beta, Tensor out
     a.nupd = upd.size();
     for (size_t k = 0; k < upd.size(); ++k) a.upd[k] = make_bn(upd[k], C);
     a.w = ptr_or_null<float>(w); a.id_idx = id_idx; a.xid = ptr_or_null<float>(xid);
-    if (a.xid) TORCH_CHECK(xid->sizes() == out.sizes(), "identity shape");
+    if (a.xid) {
+      check_f32(*xid, "xid");
+      TORCH_CHECK(xid->sizes() == out.sizes(), "identity shape");
+    }
     a.gamma = ptr_or_null<float>(gamma); a.beta = ptr_or_null<float>(beta);
     a.out = out.data_ptr<float>(); a.momentum = momentum; a.update_running = update_running;
     a.accumulate = accumulate;

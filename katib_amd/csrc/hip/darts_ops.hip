@@ -386,9 +386,10 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
         const float* sw = sW + e * (kMaxOps + 1);
         for (int k = 0; k < a.nops; ++k) {
           const int j = (e * kMaxOps + k) * C + c;
-          const float sc = sw[k] * sInv[j], sh = sc * sMean[j];
+          // same rounding as the scalar path: w * ((z - mean) * inv)
+          const float m = sMean[j], inv = sInv[j];
           const f4 z = reinterpret_cast<const f4*>(a.z[k])[i4];
-          acc += z * sc - sh;
+          acc += sw[k] * ((z - m) * inv);
         }
         if (a.xid) acc += sw[kMaxOps] * reinterpret_cast<const f4*>(a.xid)[i4];
       }
@@ -406,7 +407,7 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
       const float* sw = sW + e * (kMaxOps + 1);
       for (int k = 0; k < a.nops; ++k) {
         const int j = (e * kMaxOps + k) * C + c;
-        acc += sw[k] * (a.z[k][i] - sMean[j]) * sInv[j];
+        acc += sw[k] * ((a.z[k][i] - sMean[j]) * sInv[j]);
       }
       if (a.xid) acc += sw[kMaxOps] * a.xid[i];
     }
@@ -934,7 +935,7 @@ void launch_combine_fwd(const CombineFwdBatch& b, hipStream_t st) {
     v4 = al16(b.e[e].xid);
     for (int k = 0; k < b.e[e].nops && v4; ++k) v4 = al16(b.e[e].z[k]);
   }
-  int blocks = (int)std::min<size_t>(((v4 ? total / 4 : total) + 255) / 256, 2048);
+  int blocks = (int)std::min<size_t>(((v4 ? total / 4 : total) + 255) / 256, (size_t)max_blocks());
   size_t lds = sizeof(float) * (2 * b.n * kMaxOps * a.C + b.n * (kMaxOps + 1));
   if (v4) hipLaunchKernelGGL(combine_fwd_kernel<true>, dim3(blocks), dim3(256), lds, st, b);
   else hipLaunchKernelGGL(combine_fwd_kernel<false>, dim3(blocks), dim3(256), lds, st, b);

@@ -32,10 +32,10 @@ def exp(name, algo, settings=None, params=None, command=None, parallel=3, max_tr
     return {"apiVersion": "kubeflow.org/v1beta1", "kind": "Experiment",
             "metadata": {"namespace": "kubeflow", "name": name}, "spec": spec}
 
-def write(sub, fname, ref, doc, note=""):
+def write(sub, fname, ref, doc, note="", trial=None):
     os.makedirs(os.path.join(R, sub), exist_ok=True)
     head = "# Counterpart of the reference's examples/v1beta1/%s.\n" % ref
-    head += "# CPU-only trial: F(a, b) = 4a - b^2 (maximum 8 at a=2, b=0)%s.\n" % note
+    head += "# CPU-only trial: %s%s.\n" % (trial or "F(a, b) = 4a - b^2 (maximum 8 at a=2, b=0)", note)
     with open(os.path.join(R, sub, fname), "w") as f:
         f.write(head + yaml.safe_dump(doc, sort_keys=False))
 
@@ -126,7 +126,9 @@ write("metrics-collector", "metrics-collection-strategy.yaml", "metrics-collecto
       exp("metrics-collection-strategy", "tpe", [{"name": "random_state", "value": "10"}],
           command=["python3", "-c", strat_code], max_trials=6,
           objective={"type": "minimize", "objectiveMetricName": "loss", "additionalMetricNames": ["accuracy"],
-                     "metricStrategies": [{"name": "accuracy", "value": "max"}, {"name": "loss", "value": "min"}]}))
+                     "metricStrategies": [{"name": "accuracy", "value": "max"}, {"name": "loss", "value": "min"}]}),
+      trial="over steps s=0..3 it prints loss = (a-1.5)^2 + b^2 + 1/(s+1) and accuracy = a/2 - 0.1 s; "
+            "the strategies keep min(loss) and max(accuracy)")
 
 # resume policies
 write("resume-experiment", "long-running-resume.yaml", "resume-experiment/long-running-resume.yaml",

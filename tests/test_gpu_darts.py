@@ -232,24 +232,74 @@ def test_stem_conv_vs_torch(N, Cin, Cout, H):
     torch.testing.assert_close(x1.grad, x2.grad, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("offset", [0, 1])
-def test_combine_fwd_vector_and_scalar_paths(offset):
-    """combine_fwd takes the 16-byte vector path for aligned operands and the scalar path
-    otherwise (offset=1 shifts the BN input by one float); both match the fp32 formula
-    out = w0 * BN(z) + w_id * x (eval-mode BN from running statistics)."""
+def _combine_case(nedge, nops, training, accumulate, offset, mean_shift):
+    """Run combine_fwd on nedge edges x nops BN inputs (+ identity) with the operands placed at
+    ``offset`` floats into their buffers (offset 1 defeats 16-byte alignment -> scalar path).
+    Returns the kernel output, the updated running stats and an fp64 reference."""
     from katib_amd.ops import hip_darts as hd
 
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(3)
     N, C, H, W = 4, 8, 16, 16
-    base = torch.randn(N * C * H * W + 1, generator=g).to(dev)
-    z = base[offset:offset + N * C * H * W].view(N, C, H, W)
-    x = torch.randn(N, C, H, W, generator=g).to(dev)
-    rm = (torch.randn(C, generator=g) * 0.1).to(dev)
-    rv = (torch.rand(C, generator=g) + 0.5).to(dev)
-    w = torch.tensor([0.7, 0.3], device=dev)
-    bn = hd._bn(None, rm, rv, N * H * W, False, 1e-5, C)
-    out = torch.empty(N, C, H, W, device=dev)
-    hd._K.combine_fwd([([z], [bn], [0], w, 1, x, [])], None, None, out, 0.1, False, False)
-    ref = 0.7 * (z - rm[None, :, None, None]) / torch.sqrt(rv[None, :, None, None] + 1e-5) + 0.3 * x
-    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    n = N * C * H * W
+    out0 = torch.randn(N, C, H, W, generator=g).to(dev)
+    w = torch.softmax(torch.randn(nedge * (nops + 1), generator=g), 0).to(dev)
+    calls, ref = [], out0.double().clone() if accumulate else torch.zeros(N, C, H, W, dtype=torch.float64, device=dev)
+    rms, rvs, exp_rm, exp_rv = [], [], [], []
+    mom = 0.1
+    for e in range(nedge):
+        zs, bns, widx = [], [], []
+        for k in range(nops):
+            base = (torch.randn(n + 4, generator=g) * 0.5 + mean_shift).to(dev)
+            z = base[offset:offset + n].view(N, C, H, W)
+            rm = (torch.randn(C, generator=g) * 0.1).to(dev)
+            rv = (torch.rand(C, generator=g) + 0.5).to(dev)
+            zd = z.double()
+            if training:
+                s1 = zd.sum((0, 2, 3))
+                s2 = (zd * zd).sum((0, 2, 3))
+                stats = torch.zeros(32 * 2 * C, dtype=torch.float64, device=dev)
+                stats[:C], stats[C:2 * C] = s1, s2
+                mean = s1 / (N * H * W)
+                var = (s2 / (N * H * W) - mean * mean).clamp_min(0)
+                cnt = N * H * W
+                exp_rm.append((1 - mom) * rm.double() + mom * mean)
+                exp_rv.append((1 - mom) * rv.double() + mom * var * cnt / (cnt - 1))
+            else:
+                stats, mean, var = None, rm.double(), rv.double()
+                exp_rm.append(rm.double())
+                exp_rv.append(rv.double())
+            rms.append(rm)
+            rvs.append(rv)
+            bns.append(hd._bn(stats, rm, rv, N * H * W, training, 1e-5, C))
+            zs.append(z)
+            widx.append(e * (nops + 1) + k)
+            ref += w[e * (nops + 1) + k].double() * (zd - mean[None, :, None, None]) / torch.sqrt(
+                var[None, :, None, None] + 1e-5)
+        xb = torch.randn(n + 4, generator=g).to(dev)
+        x = xb[offset:offset + n].view(N, C, H, W)
+        id_idx = e * (nops + 1) + nops
+        ref += w[id_idx].double() * x.double()
+        calls.append((zs, bns, widx, w, id_idx, x, []))
+    out = out0.clone()
+    hd._K.combine_fwd(calls, None, None, out, mom, training, accumulate)
+    torch.cuda.synchronize()
+    return out, rms, rvs, ref, exp_rm, exp_rv
+
+
+@pytest.mark.parametrize("nedge,nops,training,accumulate,mean_shift",
+                         [(1, 1, False, False, 0.0), (3, 3, True, True, 0.0), (2, 3, True, False, 0.0),
+                          (3, 1, False, True, 0.0), (2, 2, True, True, 200.0)])
+def test_combine_fwd_vector_and_scalar_paths(nedge, nops, training, accumulate, mean_shift):
+    """combine_fwd takes the 16-byte vector path for aligned operands and the scalar path
+    otherwise (offset 1 shifts every BN input and identity by one float). Both compute
+    w * ((z - mean) * invstd), so they agree with each other to the last ulps and with the
+    fp64 formula sum_e [sum_k w_ek BN(z_ek) + w_e,id x_e] (+ out when accumulating), over
+    several edges, several BN inputs, training-mode statistics with running-stat updates,
+    and a mean 400x the standard deviation."""
+    res = [_combine_case(nedge, nops, training, accumulate, off, mean_shift) for off in (0, 1)]
+    for out, rms, rvs, ref, exp_rm, exp_rv in res:
+        torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4 if mean_shift else 2e-5)
+        for a, b in zip(rms + rvs, exp_rm + exp_rv):
+            torch.testing.assert_close(a.double(), b, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-6, atol=1e-6)
