@@ -92,17 +92,20 @@ class _StudyService(SuggestionService):
 
 
 def _check(settings, rules, algo):
-    """rules: name -> (parser, predicate, error message). Returns error or ''."""
+    """rules: name -> (parser, predicate, message). Returns None when every setting is
+    valid, else the reference's error message (which may be the empty string, as for a
+    negative random_state in optuna/service.py:226-229). ``message`` may be a callable of
+    (name, value) for messages that quote the offending value."""
     for name, value in settings:
         if name not in rules:
             return "unknown setting {} for algorithm {}".format(name, algo)
         parse, pred, msg = rules[name]
         try:
             if not pred(parse(value)):
-                return msg
+                return msg(name, value) if callable(msg) else msg
         except Exception as e:
             return "failed to validate {name}({value}): {exception}".format(name=name, value=value, exception=e)
-    return ""
+    return None
 
 
 def _pairs(request):
@@ -143,7 +146,7 @@ class HyperoptService(_StudyService):
                 "random")
         else:
             err = "unknown algorithm name {}".format(name)
-        if err:
+        if err is not None:
             return self._invalid(context, err)
         return api.ValidateAlgorithmSettingsReply()
 
@@ -171,36 +174,31 @@ class OptunaService(_StudyService):
         raise AlgorithmError("unknown algorithm name {}".format(name))
 
     def ValidateAlgorithmSettings(self, request, context=None):
+        """optuna/service.py:118-262: per-algorithm setting rules, CMA-ES needs >= 2
+        continuous dimensions, grid needs maxTrialCount <= number of combinations."""
         exp = request.experiment
         name = exp.spec.algorithm.algorithm_name
         pairs = _pairs(request)
+        ge0 = lambda k: "{} should be greate or equal than zero".format(k)  # noqa: E731 (reference spelling)
         if name in ("tpe", "multivariate-tpe"):
-            rules = {k: (int, lambda v: v >= 0, "{} should be greate or equal than zero".format(k))
-                     for k in ("n_startup_trials", "n_ei_candidates", "random_state")}
-            err = _check(pairs, rules, name)
+            err = _check(pairs, {k: (int, lambda v: v >= 0, ge0(k))
+                                 for k in ("n_startup_trials", "n_ei_candidates", "random_state")}, name)
         elif name == "cmaes":
             err = _check(pairs, {
-                "restart_strategy": (str, lambda v: v in ("ipop", "None", "none"), None),
-                "sigma": (float, lambda v: v >= 0, "sigma should be greate or equal than zero"),
-                "random_state": (int, lambda v: v >= 0, "random_state should be greate or equal than zero"),
+                "restart_strategy": (str, lambda v: v in ("ipop", "None", "none"),
+                                     lambda k, v: "restart_strategy {} is not supported in CMAES optimization".format(v)),
+                "sigma": (float, lambda v: v >= 0, ge0("sigma")),
+                "random_state": (int, lambda v: v >= 0, ge0("random_state")),
             }, "cmaes")
-            if err is None:
-                rs = dict(pairs).get("restart_strategy")
-                err = "restart_strategy {} is not supported in CMAES optimization".format(rs)
-            if not err and _count_continuous(request) < 2:
+            if err is None and _count_continuous(request) < 2:
                 err = "cmaes only supports two or more dimensional continuous search space."
-        elif name == "random":
-            err = _check(pairs, {"random_state": (int, lambda v: v >= 0, "")}, "random")
-            if err is None:
-                err = ""
-        elif name == "grid":
-            err = _check(pairs, {"random_state": (int, lambda v: v >= 0, "")}, "grid")
-            if not err:
+        elif name in ("random", "grid"):
+            err = _check(pairs, {"random_state": (int, lambda v: v >= 0, "")}, name)
+            if err is None and name == "grid":
                 space = SearchSpace.convert(exp)
                 try:
-                    combos = space.combinations()
                     n = 1
-                    for v in combos.values():
+                    for v in space.combinations().values():
                         n *= len(v)
                     if exp.spec.max_trial_count > n:
                         err = "Max Trial Count: {max_trial} > all possible search combinations: {combinations}".format(
@@ -210,23 +208,9 @@ class OptunaService(_StudyService):
                         parameters=space.params, exception=e)
         else:
             err = "unknown algorithm name {}".format(name)
-        if err is None or err:
-            # reference returns (False, "") for a negative random_state: an empty INVALID_ARGUMENT
-            if err is None:
-                err = ""
-            if err != "" or self._neg_seed(pairs):
-                return self._invalid(context, err)
+        if err is not None:
+            return self._invalid(context, err)
         return api.ValidateAlgorithmSettingsReply()
-
-    @staticmethod
-    def _neg_seed(pairs):
-        for k, v in pairs:
-            if k == "random_state":
-                try:
-                    return int(v) < 0
-                except ValueError:
-                    return False
-        return False
 
 
 # ==================================================================================== goptuna
@@ -287,21 +271,14 @@ class SkoptService(_StudyService):
         name = request.experiment.spec.algorithm.algorithm_name
         if name != "bayesianoptimization":
             return self._invalid(context, "unknown algorithm name {}".format(name))
+        unsupported = lambda k, v: "{} {} is not supported in Bayesian optimization".format(k, v)  # noqa: E731
         err = _check(_pairs(request), {
-            "base_estimator": (str, lambda v: v in ("GP", "RF", "ET", "GBRT"), None),
+            "base_estimator": (str, lambda v: v in ("GP", "RF", "ET", "GBRT"), unsupported),
             "n_initial_points": (int, lambda v: v >= 0, "n_initial_points should be great or equal than zero"),
-            "acq_func": (str, lambda v: v in BayesOptSampler.ACQS, None),
-            "acq_optimizer": (str, lambda v: v in ("auto", "sampling", "lbfgs"), None),
+            "acq_func": (str, lambda v: v in BayesOptSampler.ACQS, unsupported),
+            "acq_optimizer": (str, lambda v: v in ("auto", "sampling", "lbfgs"), unsupported),
             "random_state": (int, lambda v: v >= 0, "random_state should be great or equal than zero"),
         }, "bayesianoptimization")
-        if err is None:
-            d = dict(_pairs(request))
-            if d.get("base_estimator", "GP") not in ("GP", "RF", "ET", "GBRT"):
-                err = "base_estimator {} is not supported in Bayesian optimization".format(d["base_estimator"])
-            elif d.get("acq_func", "gp_hedge") not in BayesOptSampler.ACQS:
-                err = "acq_func {} is not supported in Bayesian optimization".format(d["acq_func"])
-            else:
-                err = "acq_optimizer {} is not supported in Bayesian optimization".format(d.get("acq_optimizer"))
-        if err:
+        if err is not None:
             return self._invalid(context, err)
         return api.ValidateAlgorithmSettingsReply()

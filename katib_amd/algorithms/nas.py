@@ -229,7 +229,7 @@ class EnasService(SuggestionService):
 
     def _setup(self, exp):
         import torch  # noqa: F401
-        from ..models.enas_controller import EnasController
+        from ..models.enas_controller import make_controller
 
         nas = exp.spec.nas_config
         self.num_layers = int(nas.graph_config.num_layers)
@@ -238,7 +238,7 @@ class EnasService(SuggestionService):
         self.search_space = enas_operations(nas.operations)
         self.settings = parse_enas_settings(exp.spec.algorithm.algorithm_settings)
         s = self.settings
-        self.controller = EnasController(
+        self.controller = make_controller(
             num_layers=self.num_layers, num_operations=len(self.search_space),
             hidden_size=s["controller_hidden_size"], temperature=s["controller_temperature"],
             tanh_const=s["controller_tanh_const"], entropy_weight=s["controller_entropy_weight"],
@@ -276,7 +276,7 @@ class EnasService(SuggestionService):
             self._setup(request.experiment)
         n = request.current_request_number if request.current_request_number > 0 else 1
         if self.first:
-            cands = [self.controller.sample_arc() for _ in range(n)]
+            cands = self.controller.sample_arcs(n)
             self.first = False
         else:
             result = self.evaluation_result(request.trials)
@@ -285,12 +285,10 @@ class EnasService(SuggestionService):
                 return api.GetSuggestionsReply()
             if self.opt_direction == api.MINIMIZE:
                 result = -result
-            self.last_train_log = []
-            for step in range(1, self.settings["controller_train_steps"] + 1):
-                log = self.controller.train_once(result)
-                if step % self.settings["controller_log_every_steps"] == 0:
-                    self.last_train_log.append(log)
-            cands = [self.controller.sample_arc() for _ in range(n)]
+            # all controller_train_steps REINFORCE steps (one kernel launch on the HIP backend)
+            self.last_train_log = self.controller.train(result, self.settings["controller_train_steps"],
+                                                        self.settings["controller_log_every_steps"])
+            cands = self.controller.sample_arcs(n)
         self._ckpt()
         pas = []
         for arc in cands:

@@ -10,15 +10,25 @@ logits ``[-q, q]``. Training: REINFORCE ``loss = sum(logp) * (R - baseline)`` +
 ``skip_weight * mean(KL(skip || target))`` with an EMA baseline and Adam.
 
 The controller is ~55k parameters: each sampling step is a chain of [1 x 2H] x
-[2H x 4H] GEMVs - launch-latency bound on any GPU, so it runs on the host by
-default (``device="cpu"``); the suggestion path therefore never competes with
-trials for the MI355X.
+[2H x 4H] GEMVs, hundreds of dependent tiny ops per arc. As PyTorch ops that is
+launch-latency bound on any GPU, so this module (:class:`EnasController`) runs on
+the host and serves as the numerics oracle. On MI355X the service uses
+:class:`EnasControllerHip`: the whole controller - sampling, BPTT, Adam, all
+``controller_train_steps`` REINFORCE steps - is ONE persistent-workgroup HIP launch
+(``csrc/hip/enas_ctrl.hip``), and the arcs of a GetSuggestions call are one more
+launch with a workgroup per arc.
+
+REINFORCE loss as in the reference (``Controller.py:200-222``):
+``loss = sum(CE of the sampled actions) * (R - baseline) + skip_weight * mean(KL)``,
+where CE = -log p, so minimising it raises the log-probability of arcs whose reward
+beats the baseline.
 """
 
 from __future__ import annotations
 
 import math
-from typing import List, Optional, Tuple
+import os
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -69,8 +79,10 @@ class EnasController(torch.nn.Module):
             logits = self.tanh_const * torch.tanh(logits)
         return logits
 
-    def sample(self) -> Tuple[List[int], torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
-        """Returns (flat arc, sum log_prob, sum entropy, mean skip KL, skip count)."""
+    def sample(self, forced: Optional[Sequence[int]] = None
+               ) -> Tuple[List[int], torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+        """Returns (flat arc, sum log_prob, sum entropy, mean skip KL, skip count).
+        ``forced`` replays a given flat arc instead of drawing one (gradient checks)."""
         H = self.H
         c = torch.zeros(1, H)
         h = torch.zeros(1, H)
@@ -82,7 +94,11 @@ class EnasController(torch.nn.Module):
         for layer in range(self.num_layers):
             c, h = self._lstm(inputs, c, h, self.w_lstm)
             logits = self._shape_logits(h @ self.w_soft)
-            op = torch.multinomial(F.softmax(logits, -1), 1, generator=self.gen).view(1)
+            pos = len(arc)
+            if forced is not None:
+                op = torch.tensor([int(forced[pos])])
+            else:
+                op = torch.multinomial(F.softmax(logits, -1), 1, generator=self.gen).view(1)
             arc.append(int(op))
             lp = -F.cross_entropy(logits, op, reduction="sum")
             logps.append(lp)
@@ -92,7 +108,10 @@ class EnasController(torch.nn.Module):
             if layer > 0:
                 q = torch.tanh(h @ self.attn_w_2 + torch.cat(all_hw, 0)) @ self.attn_v  # [layer, 1]
                 sl = self._shape_logits(torch.cat([-q, q], dim=1))  # [layer, 2]
-                skip = torch.multinomial(F.softmax(sl, -1), 1, generator=self.gen).view(-1)
+                if forced is not None:
+                    skip = torch.tensor([int(v) for v in forced[len(arc):len(arc) + layer]])
+                else:
+                    skip = torch.multinomial(F.softmax(sl, -1), 1, generator=self.gen).view(-1)
                 arc.extend(int(s) for s in skip)
                 sp = torch.sigmoid(sl)
                 kls.append(torch.sum(sp * torch.log(sp / targets)))
@@ -113,13 +132,13 @@ class EnasController(torch.nn.Module):
     def sample_arc(self) -> List[int]:
         return self.sample()[0]
 
-    def train_once(self, reward: float):
-        arc, logp, ent, kl, skip_count = self.sample()
+    def train_once(self, reward: float, forced: Optional[Sequence[int]] = None):
+        arc, logp, ent, kl, skip_count = self.sample(forced)
         r = torch.tensor(float(reward))
         if self.entropy_weight is not None:
             r = r + self.entropy_weight * ent
         self.baseline -= (1 - self.baseline_decay) * (self.baseline - r.detach())
-        loss = logp * (r.detach() - self.baseline)
+        loss = -logp * (r.detach() - self.baseline)  # sum of CE (= -log p) times the advantage
         if self.skip_weight is not None:
             loss = loss + self.skip_weight * kl
         self.opt.zero_grad()
@@ -132,6 +151,22 @@ class EnasController(torch.nn.Module):
                 "baseline": float(self.baseline),
                 "skip_rate": float(skip_count) / norm if norm else 0.0}
 
+    def train(self, reward: float, steps: int, log_every: int = 0) -> List[dict]:
+        """``steps`` REINFORCE steps at a fixed reward; returns the log of every
+        ``log_every``-th step (service.py:311-334 loop)."""
+        logs = []
+        for step in range(1, steps + 1):
+            log = self.train_once(reward)
+            if log_every and step % log_every == 0:
+                logs.append(log)
+        return logs
+
+    def sample_arcs(self, n: int) -> List[List[int]]:
+        return [self.sample_arc() for _ in range(n)]
+
+    def named_flat(self) -> dict:
+        return {k: v.detach() for k, v in self.named_parameters()}
+
     def state(self):
         return {"params": {k: v.detach().clone() for k, v in self.state_dict().items()},
                 "opt": self.opt.state_dict(), "train_step": self.train_step}
@@ -140,3 +175,135 @@ class EnasController(torch.nn.Module):
         self.load_state_dict(st["params"])
         self.opt.load_state_dict(st["opt"])
         self.train_step = st["train_step"]
+
+
+PARAM_ORDER = ("w_lstm", "g_emb", "w_emb", "w_soft", "attn_w_1", "attn_w_2", "attn_v")
+
+
+class EnasControllerHip(EnasController):
+    """The same controller on MI355X through the persistent-workgroup HIP kernel.
+
+    Parameters (same init stream as :class:`EnasController`), Adam moments and the
+    baseline live on the GPU in flat buffers laid out as the kernel expects
+    (``PARAM_ORDER``, row-major). ``train`` runs all its REINFORCE steps in one launch;
+    ``sample_arcs(n)`` draws n arcs in one launch (one workgroup per arc). Sampling uses
+    a counter-based RNG (seed, call counter), so arcs differ from the torch backend's
+    draws for the same seed; with ``forced`` arcs both backends compute the same losses,
+    gradients and updates (tests/test_gpu_enas.py).
+    """
+
+    def __init__(self, *args, device=None, **kw):
+        super().__init__(*args, **kw)
+        import importlib
+
+        self._K = importlib.import_module("katib_amd._hipkern")  # raises if the extension is not built
+        if self.H > 64:
+            raise ValueError("the HIP ENAS controller supports controller_hidden_size <= 64")
+        self.device = torch.device(device or "cuda")
+        params = dict(self.named_parameters())
+        self.flat = torch.cat([params[n].detach().reshape(-1) for n in PARAM_ORDER]).to(self.device).contiguous()
+        n = self.flat.numel()
+        assert n == self._K.enas_n_params(self.H, self.num_operations)
+        self.m = torch.zeros(n, device=self.device)
+        self.v = torch.zeros(n, device=self.device)
+        self.g = torch.zeros(n, device=self.device)
+        self.base_t = torch.zeros(1, device=self.device)
+        self.arc_len = self.num_layers * (self.num_layers + 1) // 2
+        self.tape_floats = int(self._K.enas_tape_floats(self.H, self.num_operations, self.num_layers))
+        self._tape = torch.empty(0, device=self.device)
+        self.adam_t = 0
+        self.rng_offset = 0
+        seed = kw.get("seed")
+        self.rng_seed = int(seed) if seed is not None else int.from_bytes(os.urandom(7), "little")
+        self.cfg = {"temperature": self.temperature, "tanh_const": self.tanh_const,
+                    "entropy_weight": self.entropy_weight, "skip_weight": self.skip_weight,
+                    "skip_target": float(self.skip_target), "baseline_decay": float(self.baseline_decay),
+                    "lr": float(self.opt.defaults["lr"]), "beta1": 0.9, "beta2": 0.999, "eps": 1e-8}
+
+    def _tape_for(self, blocks):
+        need = blocks * self.tape_floats
+        if self._tape.numel() < need:
+            self._tape = torch.empty(need, device=self.device)
+        return self._tape
+
+    def sample_arcs(self, n: int, forced: Optional[Sequence[int]] = None) -> List[List[int]]:
+        arcs = torch.empty(n, self.arc_len, dtype=torch.int32, device=self.device)
+        f = None if forced is None else torch.tensor(list(forced), dtype=torch.int32, device=self.device)
+        self._K.enas_sample(self.flat, arcs, self._tape_for(n), self.num_layers, self.num_operations, self.H, self.cfg,
+                            self.rng_seed, self.rng_offset, f)
+        self.rng_offset += n
+        return arcs.cpu().tolist()
+
+    @torch.no_grad()
+    def sample_arc(self) -> List[int]:
+        return self.sample_arcs(1)[0]
+
+    def train_steps(self, reward: float, steps: int, forced: Optional[Sequence[int]] = None):
+        """``steps`` REINFORCE steps in ONE kernel launch; returns (logs [steps, 8], arcs)."""
+        arcs = torch.empty(steps, self.arc_len, dtype=torch.int32, device=self.device)
+        logs = torch.empty(steps, self._K.ENAS_LOG_FIELDS, device=self.device)
+        f = None if forced is None else torch.tensor(list(forced), dtype=torch.int32, device=self.device)
+        self._K.enas_train(self.flat, self.m, self.v, self.g, self._tape_for(1), arcs, logs, self.base_t,
+                           self.num_layers, self.num_operations, self.H, self.cfg, float(reward), steps, self.adam_t,
+                           self.rng_seed, self.rng_offset, f)
+        self.adam_t += steps
+        self.rng_offset += steps
+        self.train_step += steps
+        return logs.cpu(), arcs.cpu()
+
+    def train_once(self, reward: float, forced: Optional[Sequence[int]] = None):
+        return self._log_dict(self.train_steps(reward, 1, forced)[0][0])
+
+    def train(self, reward: float, steps: int, log_every: int = 0) -> List[dict]:
+        logs, _ = self.train_steps(reward, steps)
+        if not log_every:
+            return []
+        return [self._log_dict(logs[i - 1]) for i in range(log_every, steps + 1, log_every)]
+
+    @staticmethod
+    def _log_dict(row):
+        return {"loss": float(row[0]), "entropy": float(row[1]), "grad_norm": float(row[2]),
+                "baseline": float(row[3]), "skip_rate": float(row[4])}
+
+    def named_flat(self) -> dict:
+        out, off = {}, 0
+        params = dict(self.named_parameters())
+        for n in PARAM_ORDER:
+            k = params[n].numel()
+            out[n] = self.flat[off:off + k].view(params[n].shape)
+            off += k
+        return out
+
+    def state(self):
+        return {"backend": "hip", "flat": self.flat.cpu(), "m": self.m.cpu(), "v": self.v.cpu(),
+                "baseline": float(self.base_t), "adam_t": self.adam_t, "rng_seed": self.rng_seed,
+                "rng_offset": self.rng_offset, "train_step": self.train_step}
+
+    def load(self, st):
+        if st.get("backend") != "hip":
+            super().load(st)
+            params = dict(self.named_parameters())
+            self.flat.copy_(torch.cat([params[n].detach().reshape(-1) for n in PARAM_ORDER]))
+            return
+        self.flat.copy_(st["flat"])
+        self.m.copy_(st["m"])
+        self.v.copy_(st["v"])
+        self.base_t.fill_(st["baseline"])
+        self.adam_t, self.rng_seed = st["adam_t"], st["rng_seed"]
+        self.rng_offset, self.train_step = st["rng_offset"], st["train_step"]
+
+
+def make_controller(backend: Optional[str] = None, **kw) -> EnasController:
+    """``backend``: "hip" (MI355X kernel), "torch" (host oracle) or "auto" (default, env
+    ``KATIB_AMD_ENAS_BACKEND``): the HIP kernel when a GPU and the extension are present."""
+    backend = (backend or os.environ.get("KATIB_AMD_ENAS_BACKEND", "auto")).lower()
+    if backend == "torch":
+        return EnasController(**kw)
+    if backend == "hip":
+        return EnasControllerHip(**kw)
+    if torch.cuda.is_available() and kw.get("hidden_size", 64) <= 64:
+        try:
+            return EnasControllerHip(**kw)
+        except (ImportError, OSError):
+            pass
+    return EnasController(**kw)

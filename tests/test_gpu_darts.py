@@ -250,7 +250,8 @@ def _combine_case(nedge, nops, training, accumulate, offset, mean_shift):
     for e in range(nedge):
         zs, bns, widx = [], [], []
         for k in range(nops):
-            base = (torch.randn(n + 4, generator=g) * 0.5 + mean_shift).to(dev)
+            base = torch.zeros(n + 4, device=dev)  # same values at either alignment
+            base[offset:offset + n] = (torch.randn(n, generator=g) * 0.5 + mean_shift).to(dev)
             z = base[offset:offset + n].view(N, C, H, W)
             rm = (torch.randn(C, generator=g) * 0.1).to(dev)
             rv = (torch.rand(C, generator=g) + 0.5).to(dev)
@@ -276,7 +277,8 @@ def _combine_case(nedge, nops, training, accumulate, offset, mean_shift):
             widx.append(e * (nops + 1) + k)
             ref += w[e * (nops + 1) + k].double() * (zd - mean[None, :, None, None]) / torch.sqrt(
                 var[None, :, None, None] + 1e-5)
-        xb = torch.randn(n + 4, generator=g).to(dev)
+        xb = torch.zeros(n + 4, device=dev)
+        xb[offset:offset + n] = torch.randn(n, generator=g).to(dev)
         x = xb[offset:offset + n].view(N, C, H, W)
         id_idx = e * (nops + 1) + nops
         ref += w[id_idx].double() * x.double()
