@@ -646,6 +646,96 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// pw_bwd_px: pw_bwd for narrow layers (Cin * Cout <= 96, the C = 4..12 channels of small
+// supernets). The tiled kernel above spends most of its time in the weight-gradient sum, where
+// Cin * Cout threads (16 of 256 at C = 4) each walk the tile's 64 pixels through LDS. Here
+// every thread owns whole pixels with ALL channels in registers: dz (BN backward on the fly),
+// the layer input, dd = pw^T dz, and a private Cin x Cout weight-gradient accumulator; loads
+// and stores are coalesced across the wave (consecutive pixels), there is no LDS staging and
+// no barrier until the block's single reduction of its accumulators (wave shuffles, then one
+// LDS add per wave and one global atomic vector per block into the block's replica).
+// ------------------------------------------------------------------------------------------------
+template <int CI, int CO>
+__global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
+  const PwBwdArgs& a = bt.e[blockIdx.y];
+  const int HWo = a.Ho * a.Wo, Wo = a.Wo;
+  const int total = a.N * HWo;
+  __shared__ float sC[4 * CO + 1];
+  __shared__ float sGW[CI * CO];
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int c = tid; c < CO; c += 256) {
+    bn_coeffs(a.gs.bn, a.co_off + c, sC[c], sC[CO + c]);
+    gs_means(a.gs, a.co_off + c, sC[2 * CO + c], sC[3 * CO + c]);
+  }
+  if (tid == 0) sC[4 * CO] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
+  for (int i = tid; i < CI * CO; i += 256) sGW[i] = 0.f;
+  __syncthreads();
+  float mean[CO], inv[CO], m1[CO], m2[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) {
+    mean[c] = sC[c];
+    inv[c] = sC[CO + c];
+    m1[c] = sC[2 * CO + c];
+    m2[c] = sC[3 * CO + c];
+  }
+  const float wk = sC[4 * CO];
+  float wpw[CI * CO];  // pointwise weights in registers (the loop's stores could alias them)
+#pragma unroll
+  for (int i = 0; i < CI * CO; ++i) wpw[i] = a.pw[i];
+  float gacc[CI * CO];
+#pragma unroll
+  for (int i = 0; i < CI * CO; ++i) gacc[i] = 0.f;
+  const bool want_w = a.gW != nullptr;
+  for (int p = blockIdx.x * 256 + tid; p < total; p += gridDim.x * 256) {
+    const int n = p / HWo, pp = p - n * HWo;
+    float dz[CO], av[CI];
+#pragma unroll
+    for (int c = 0; c < CO; ++c)
+      dz[c] = bn_bwd_val(a.gs, ((size_t)n * a.CoutTotal + a.co_off + c) * HWo + pp, mean[c], inv[c], wk, m1[c], m2[c]);
+    size_t xi0 = 0;
+    bool inb = true;
+    if (a.mode == 0) {
+#pragma unroll
+      for (int c = 0; c < CI; ++c) av[c] = a.ain[((size_t)n * CI + c) * HWo + pp];
+    } else {
+      const int oy = pp / Wo, ox = pp - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+      inb = iy < a.H && ix < a.W;
+      xi0 = ((size_t)n * CI * a.H + iy) * a.W + ix;
+#pragma unroll
+      for (int c = 0; c < CI; ++c) av[c] = inb ? fmaxf(a.x[xi0 + (size_t)c * a.H * a.W], 0.f) : 0.f;
+    }
+    if (want_w) {
+#pragma unroll
+      for (int co = 0; co < CO; ++co)
+#pragma unroll
+        for (int ci = 0; ci < CI; ++ci) gacc[co * CI + ci] += dz[co] * av[ci];
+    }
+    if (a.need_dx) {
+#pragma unroll
+      for (int ci = 0; ci < CI; ++ci) {
+        float v = 0.f;
+#pragma unroll
+        for (int co = 0; co < CO; ++co) v += wpw[co * CI + ci] * dz[co];
+        if (a.mode == 0) {
+          a.dd[((size_t)n * CI + ci) * HWo + pp] = v;
+        } else if (inb && av[ci] > 0.f) {  // relu'(x): x > 0  <=>  relu(x) > 0
+          a.gx[xi0 + (size_t)ci * a.H * a.W] += v;
+        }
+      }
+    }
+  }
+  if (!want_w) return;
+#pragma unroll
+  for (int i = 0; i < CI * CO; ++i) {
+    const float s = wave_sum(gacc[i]);
+    if (lane == 0) atomicAdd(sGW + i, s);
+  }
+  __syncthreads();
+  float* gW = a.gW + (size_t)rep_slot() * a.gstride;
+  for (int i = tid; i < CI * CO; i += 256) atomicAdd(gW + i, sGW[i]);
+}
+
+// ------------------------------------------------------------------------------------------------
 // dw_bwd: transposed depthwise. For own output rows [oy0, oy0+TR): dW_dw += dd * act(in);
 // for own input rows [oy0*S, (oy0+TR)*S): ga = sum_taps dw * dd, masked by act'(in).
 // PREBN: input = z_prev (pre-BN), act = relu(BN(.)) -> writes g_prev and reductions for BN bwd.
@@ -947,8 +1037,23 @@ void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st) {
                      b);
 }
 
+template <int CI, int CO>
+static bool try_pw_bwd_px(const PwBwdBatch& b, hipStream_t st) {
+  const PwBwdArgs& a = b.e[0];
+  if (a.Cin != CI || a.Cout != CO) return false;
+  const int total = a.N * a.Ho * a.Wo;
+  const int per_edge = std::max(1, std::min((total + 1023) / 1024, max_blocks() / std::max(b.n, 1)));
+  hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO>), dim3(per_edge, b.n), dim3(256), 0, st, b);
+  return true;
+}
+
 void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st) {
   const PwBwdArgs& a = b.e[0];
+  // narrow layers: pixel-per-thread kernel (see pw_bwd_px_kernel)
+  if (try_pw_bwd_px<4, 4>(b, st) || try_pw_bwd_px<8, 8>(b, st) || try_pw_bwd_px<4, 8>(b, st) ||
+      try_pw_bwd_px<8, 4>(b, st) || try_pw_bwd_px<12, 8>(b, st) || try_pw_bwd_px<2, 2>(b, st) ||
+      try_pw_bwd_px<4, 2>(b, st) || try_pw_bwd_px<2, 4>(b, st))
+    return;
   int ntiles = a.N * a.Ho * a.Wo / 64;
   dim3 grid(per_edge_blocks(ntiles, b.n), b.n);
   size_t lds = sizeof(float) * (a.Cout * 65 + a.Cin * 65 + 4 * a.Cout + 4);
