@@ -310,8 +310,11 @@ void pw_bwd(std::vector<py::tuple> calls, int64_t S, int64_t mode, bool need_dx)
     OptT dd = t[4].cast<OptT>(), gx = t[5].cast<OptT>(), gW = t[6].cast<OptT>();
     const int co_off = t[7].cast<int>(), off = t[8].cast<int>();
     const int64_t gstride = t[9].cast<int64_t>();
+    const bool overwrite = t.size() > 10 && t[10].cast<bool>();
     check_f32(pw, "pw"); check_f32(x, "x");
     PwBwdArgs& a = bt.e[i];
+    a.overwrite = overwrite;
+    TORCH_CHECK(!overwrite || (mode == 1 && S == 1 && off == 0), "gx overwrite needs the stride-1 full-coverage form");
     const int Cout = pw.size(0), Cin = pw.size(1);
     Tensor g = gs[0].cast<Tensor>();
     a.N = g.size(0); a.CoutTotal = g.size(1); a.Ho = g.size(2); a.Wo = g.size(3);

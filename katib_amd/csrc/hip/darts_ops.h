@@ -72,6 +72,7 @@ struct PwBwdArgs {
   GradSrc gs; const float* pw; const float* ain; const float* x; float* dd; float* gx; float* gW;
   int gstride;  // floats between gW replicas (0: single accumulator)
   int N, Cin, Cout, CoutTotal, co_off, H, W, Ho, Wo, S, off, mode, need_dx;
+  int overwrite;  // mode 1, stride 1: gx = masked grad instead of += (the kernel covers every pixel)
 };
 
 struct DwBwdArgs {

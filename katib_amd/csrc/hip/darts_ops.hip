@@ -596,7 +596,8 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
                 int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
                 if (iy < a.H && ix < a.W) {
                   size_t xi = (((size_t)n * Cin + ci) * a.H + iy) * a.W + ix;
-                  if (a.x[xi] > 0.f) a.gx[xi] += v;
+                  if (a.overwrite) a.gx[xi] = a.x[xi] > 0.f ? v : 0.f;
+                  else if (a.x[xi] > 0.f) a.gx[xi] += v;
                 }
               }
             }
@@ -614,7 +615,8 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
             int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
             if (iy < a.H && ix < a.W) {
               size_t xi = (((size_t)n * Cin + ciu) * a.H + iy) * a.W + ix;
-              if (a.x[xi] > 0.f) a.gx[xi] += v;
+              if (a.overwrite) a.gx[xi] = a.x[xi] > 0.f ? v : 0.f;
+              else if (a.x[xi] > 0.f) a.gx[xi] += v;
             }
           }
         }
@@ -718,6 +720,8 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
         for (int co = 0; co < CO; ++co) v += wpw[co * CI + ci] * dz[co];
         if (a.mode == 0) {
           a.dd[((size_t)n * CI + ci) * HWo + pp] = v;
+        } else if (a.overwrite) {  // stride 1: every input pixel is some thread's own
+          a.gx[xi0 + (size_t)ci * a.H * a.W] = av[ci] > 0.f ? v : 0.f;
         } else if (inb && av[ci] > 0.f) {  // relu'(x): x > 0  <=>  relu(x) > 0
           a.gx[xi0 + (size_t)ci * a.H * a.W] += v;
         }
@@ -896,15 +900,17 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdBatch bt) {
   float* sGa = smem;                                          // [HWo] dz_avg / window count
   float* sGm = smem + HWo;                                    // [HWo] dz_max
   unsigned char* sArg = (unsigned char*)(smem + 2 * HWo);     // [HWo] argmax tap
-  float ma = 0, ia = 1, mm = 0, im = 1, a1 = 0, a2 = 0, m1 = 0, m2 = 0;
-  if (a.ga.z) {
-    bn_coeffs(a.ga.bn, c, ma, ia);
-    gs_means(a.ga, c, a1, a2);
-  }
-  if (a.gm.z) {
-    bn_coeffs(a.gm.bn, c, mm, im);
-    gs_means(a.gm, c, m1, m2);
-  }
+  // the plane's BN coefficients: four threads each sum one pair over the replicas
+  __shared__ float sCo[8];
+  if (threadIdx.x < 8) sCo[threadIdx.x] = (threadIdx.x & 1) ? 1.f : 0.f;
+  __syncthreads();
+  if (threadIdx.x == 0 && a.ga.z) bn_coeffs(a.ga.bn, c, sCo[0], sCo[1]);
+  if (threadIdx.x == 64 && a.ga.z) gs_means(a.ga, c, sCo[2], sCo[3]);
+  if (threadIdx.x == 128 && a.gm.z) bn_coeffs(a.gm.bn, c, sCo[4], sCo[5]);
+  if (threadIdx.x == 192 && a.gm.z) gs_means(a.gm, c, sCo[6], sCo[7]);
+  __syncthreads();
+  const float ma = sCo[0], ia = sCo[1], a1 = a.ga.z ? sCo[2] : 0.f, a2 = a.ga.z ? sCo[3] : 0.f;
+  const float mm = sCo[4], im = sCo[5], m1 = a.gm.z ? sCo[6] : 0.f, m2 = a.gm.z ? sCo[7] : 0.f;
   const float wa = a.ga.w ? a.ga.w[a.ga.widx] : 0.f;
   const float wm = a.gm.w ? a.gm.w[a.gm.widx] : 0.f;
   const float wid = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;

@@ -261,12 +261,19 @@ class DartsNetwork:
             self._specs[e["prefix"]] = spec
         return spec
 
-    def forward(self, x, P: Dict[str, torch.Tensor], normal: List[torch.Tensor], reduce: List[torch.Tensor],
-                bn: BNState, training=True):
+    def forward(self, x, P: Dict[str, torch.Tensor], normal, reduce, bn: BNState, training=True):
+        """``normal`` / ``reduce``: per-node alpha rows (lists of [2+i, K]) or all rows of a
+        cell type as one [rows, K] tensor (one softmax launch per cell type)."""
         L, ops = self.layout, self.ops
+        hd = self.ops.hip_module() if self.ops.hip_enabled(x) else None
+        if hd is not None and self._hip_cells(hd, x):
+            return self._forward_cells(hd, x, P, normal, reduce, bn, training)
+        if torch.is_tensor(normal):
+            normal = self._split_rows(normal)
+        if torch.is_tensor(reduce):
+            reduce = self._split_rows(reduce)
         wn = [F.softmax(a, dim=-1) for a in normal]
         wr = [F.softmax(a, dim=-1) for a in reduce]
-        hd = self.ops.hip_module() if self.ops.hip_enabled(x) else None
         if hd is not None and hd.stem_supported(x, P["stem.conv"]):
             s = hd.stem_conv(x, P["stem.conv"])
         else:
@@ -285,6 +292,85 @@ class DartsNetwork:
                 ei += 2 + n
                 states.append(self.mixed_node(states, edges, P, weights[n], bn, training))
             s0, s1 = s1, torch.cat(states[2:], dim=1)
+        out = F.adaptive_avg_pool2d(s1, 1).flatten(1)
+        return F.linear(out, P["classifier.weight"], P["classifier.bias"])
+
+    # ------------------------------------------------------------------ cell-level HIP path
+    def _split_rows(self, t):
+        out, off = [], 0
+        for n in range(self.layout.N):
+            out.append(t[off:off + 2 + n])
+            off += 2 + n
+        return out
+
+    def _hip_cells(self, hd, x) -> bool:
+        """Whole-cell HIP Functions apply when every edge and preprocess shape is one the
+        kernels support (hip_darts.supported / the 1x1 weight-size limit)."""
+        key = ("__cells_ok__", tuple(x.shape), x.dtype)
+        ok = self._specs.get(key)
+        if ok is None:
+            def tile_ok(C, H, stride):
+                Ho = (H - 1) // stride + 1
+                return C <= 256 and C * C <= 4096 and Ho <= 64 and 64 % Ho == 0 and Ho % (64 // Ho) == 0 \
+                    and H == Ho * stride
+            ok = hasattr(hd, "cell_forward") and x.dtype == torch.float32 and x.dim() == 4
+            h = x.shape[2]
+            for cell in self.layout.cells:
+                C = cell["C"]
+                if cell["reduction"]:
+                    ok = ok and tile_ok(C, h, 2) and tile_ok(C, h // 2, 1)
+                    h //= 2
+                else:
+                    ok = ok and tile_ok(C, h, 1)
+                ok = ok and cell["cpp"] * C <= 4096 and cell["cp"] * C <= 4096
+            self._specs[key] = ok
+        return ok
+
+    def _cell_spec(self, hd, ci):
+        key = "__cell%d" % ci
+        spec = self._specs.get(key)
+        if spec is None:
+            L = self.layout
+            cell = L.cells[ci]
+            pre = "cells.%d" % ci
+            if cell["reduction_prev"]:
+                pre0 = ("fr", [pre + ".pre0.conv1", pre + ".pre0.conv2"], pre + ".pre0.bn")
+            else:
+                pre0 = ("std", [pre + ".pre0.conv"], pre + ".pre0.bn")
+            pre1 = ("std", [pre + ".pre1.conv"], pre + ".pre1.bn")
+            nodes, ei, row = [], 0, 0
+            for n in range(L.N):
+                node = []
+                for e in cell["edges"][ei:ei + 2 + n]:
+                    es, pnames, bn_names = self._edge_spec(hd, e)
+                    node.append((es, [e["prefix"] + "." + q for q in pnames], bn_names, e["src"], row + e["src"]))
+                nodes.append(node)
+                ei += 2 + n
+                row += 2 + n
+            spec = hd.CellSpec(pre0, pre1, nodes, cell["C"])
+            self._specs[key] = spec
+        return spec
+
+    def _forward_cells(self, hd, x, P, normal, reduce, bn, training):
+        L = self.layout
+        an = normal if torch.is_tensor(normal) else torch.cat(list(normal), 0)
+        wn = F.softmax(an, dim=-1)
+        wr = None
+        if L.has_reduce:
+            ar = reduce if torch.is_tensor(reduce) else torch.cat(list(reduce), 0)
+            wr = F.softmax(ar, dim=-1)
+        if hd.stem_supported(x, P["stem.conv"]):
+            s = hd.stem_conv(x, P["stem.conv"])
+        else:
+            s = F.conv2d(x, P["stem.conv"], padding=1)
+        s = self._bn(s, "stem.bn", bn, training, P["stem.bn.weight"], P["stem.bn.bias"])
+        s0 = s1 = s
+        for ci, cell in enumerate(L.cells):
+            spec = self._cell_spec(hd, ci)
+            params = [P[n] for n in spec.names]
+            out = hd.cell_forward(spec, s0, s1, wr if cell["reduction"] else wn, params, bn.get, training,
+                                  self.momentum, self.eps)
+            s0, s1 = s1, out
         out = F.adaptive_avg_pool2d(s1, 1).flatten(1)
         return F.linear(out, P["classifier.weight"], P["classifier.bias"])
 

@@ -106,24 +106,31 @@ class DartsSearch:
         self.bn_v = BNState(layout, dev)
         self.loss_out = torch.zeros((), device=dev)
         self.logits_out = None
-        # leaves
+        # leaves: weights are views of W / W'; alphas are ONE [rows, K] leaf per cell type
+        # (normal, reduce) so each forward runs one softmax per cell type
         self.Pw = _Leaves(layout.views(self.W), layout.views(self.gW))
         self.Pv = _Leaves(layout.views(self.Wv), layout.views(self.gWv))
-        an, ar = layout.alpha_views(self.A)
-        gn, gr = layout.alpha_views(self.gA)
-        self.An, self.Ar = an, ar
-        for v, gv in zip(an + ar, gn + gr):
-            v.requires_grad_(True)
-            v.grad = gv
-        avn, avr = layout.alpha_views(self.Av)
-        gvn, gvr = layout.alpha_views(self.gAv)
-        self.Avn, self.Avr = avn, avr
-        for v, gv in zip(avn + avr, gvn + gvr):
-            v.requires_grad_(True)
-            v.grad = gv
+        self.An, self.Ar = layout.alpha_views(self.A)  # per-node views (genotype)
+        self.Aw, self.gAw = self._alpha_leaves(self.A, self.gA)
+        self.Avw, _ = self._alpha_leaves(self.Av, self.gAv)
         self.W_detached = layout.views(self.W.detach())
         self.graphs = None
         self.static = None
+
+    def _alpha_leaves(self, A, gA):
+        rows, K = self.layout.n_alpha_rows, len(self.layout.prims)
+        leaves, grads = [], []
+        for t in range(2 if self.layout.has_reduce else 1):
+            v = A[t * rows * K:(t + 1) * rows * K].view(rows, K)
+            g = gA[t * rows * K:(t + 1) * rows * K].view(rows, K)
+            v.requires_grad_(True)
+            v.grad = g
+            leaves.append(v)
+            grads.append(g)
+        return leaves, grads
+
+    def _arch(self, leaves):
+        return leaves[0], (leaves[1] if len(leaves) > 1 else [])
 
     # ------------------------------------------------------------------ pieces
     def _loss(self, x, y, P, an, ar, bn):
@@ -137,7 +144,7 @@ class DartsSearch:
     def _seg_virtual(self, tx, ty):
         """FWD1/BWD1 -> gW (not yet reduced)."""
         self.gW.zero_()
-        loss, _ = self._loss(tx, ty, self.Pw.views, self.An, self.Ar, self.bn)
+        loss, _ = self._loss(tx, ty, self.Pw.views, *self._arch(self.Aw), self.bn)
         loss.backward(inputs=self.Pw.list)
         self._fold(self.gW_rep)
 
@@ -151,8 +158,8 @@ class DartsSearch:
             self.Av.copy_(self.A)
         self.gWv.zero_()
         self.gAv.zero_()
-        loss, _ = self._loss(vx, vy, self.Pv.views, self.Avn, self.Avr, self.bn_v)
-        loss.backward(inputs=self.Pv.list + self.Avn + self.Avr)
+        loss, _ = self._loss(vx, vy, self.Pv.views, *self._arch(self.Avw), self.bn_v)
+        loss.backward(inputs=self.Pv.list + self.Avw)
         self._fold(self.gWv_rep)
 
     def _seg_hessian(self, tx, ty):
@@ -161,14 +168,14 @@ class DartsSearch:
             self.eps.copy_(0.01 / self.gWv.norm())
             self.W.add_(self.gWv * self.eps)
         self.gA.zero_()
-        loss, _ = self._loss(tx, ty, self.W_detached, self.An, self.Ar, self.bn)
-        loss.backward(inputs=self.An + self.Ar)
+        loss, _ = self._loss(tx, ty, self.W_detached, *self._arch(self.Aw), self.bn)
+        loss.backward(inputs=self.Aw)
         with torch.no_grad():
             self.gAp.copy_(self.gA)
             self.W.sub_(self.gWv * (2.0 * self.eps))
         self.gA.zero_()
-        loss, _ = self._loss(tx, ty, self.W_detached, self.An, self.Ar, self.bn)
-        loss.backward(inputs=self.An + self.Ar)
+        loss, _ = self._loss(tx, ty, self.W_detached, *self._arch(self.Aw), self.bn)
+        loss.backward(inputs=self.Aw)
         with torch.no_grad():
             self.W.add_(self.gWv * self.eps)
             # alpha.grad = d_alpha - xi * (d+ - d-) / (2 eps)
@@ -193,7 +200,7 @@ class DartsSearch:
         """FWD5/BWD5 -> gW (+ alpha grads ignored), logits/loss kept for metrics."""
         self.gW.zero_()
         self.gA.zero_()
-        loss, logits = self._loss(tx, ty, self.Pw.views, self.An, self.Ar, self.bn)
+        loss, logits = self._loss(tx, ty, self.Pw.views, *self._arch(self.Aw), self.bn)
         loss.backward(inputs=self.Pw.list)
         self._fold(self.gW_rep)
         with torch.no_grad():
@@ -312,7 +319,7 @@ class DartsSearch:
     # ------------------------------------------------------------------ eval / genotype
     @torch.no_grad()
     def evaluate(self, x, y):
-        logits = self.net.forward(x, self.layout.views(self.W), self.An, self.Ar, self.bn, training=False)
+        logits = self.net.forward(x, self.layout.views(self.W), *self._arch(self.Aw), self.bn, training=False)
         loss = F.cross_entropy(logits, y)
         top1, top5 = accuracy(logits, y)
         return loss, top1, top5

@@ -47,6 +47,18 @@ except ImportError as e:  # pragma: no cover - machines without the build
 
 F64 = torch.float64
 REP = int(_K.REP)
+# FOLD=1 (default): a fold_f64 launch sums the REP replicas of each cross-workgroup reduction
+# before its consumers (which then read rep=1); FOLD=0 (KATIB_HIP_FOLD=0): consumers sum the
+# replicas themselves and the fold launches disappear. Measured on MI355X (B5 step): 13.3 ms
+# with the folds, 17.1 ms without - every consumer workgroup re-reading 32 replicas costs more
+# than ~180 small fold launches.
+FOLD = __import__("os").environ.get("KATIB_HIP_FOLD", "1") != "0"
+_R = 1 if FOLD else REP
+
+
+def _fold64(segs):
+    if FOLD:
+        _K.fold_f64(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
 _CAP = {"combine_fwd": 3, "dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 8,
         "dw_bwd": 8, "pool_bwd": 8}
 _REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
@@ -155,7 +167,7 @@ class EdgeSpec:
 def _bn(stats: Optional[torch.Tensor], rm, rv, count: int, training: bool, eps: float, C: int):
     """BN reference tuple for the kernels; ``stats`` ([REP][2C]) is folded before use."""
     if training:
-        return (stats, rm, rv, 1.0 / count, False, eps, 1, 2 * C)
+        return (stats, rm, rv, 1.0 / count, False, eps, _R, 2 * C)
     return (None, rm, rv, 1.0 / count, True, eps, 1, 2 * C)
 
 
@@ -204,128 +216,267 @@ class _Edge:
         self.id_done = False
 
 
+def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=None):
+    """One node's forward (all kernels of every incoming edge); ``out`` may be a preallocated
+    contiguous buffer (the cell writes each node straight into its concat slot). Returns
+    (out, edges) - ``edges`` is the state :func:`_node_backward` needs."""
+    E = len(specs)
+    xs = [t.contiguous() for t in xs]
+    N, C = xs[0].shape[:2]
+    S0 = specs[0].stride
+    Ho = (xs[0].shape[2] - 1) // S0 + 1
+    Wo = (xs[0].shape[3] - 1) // S0 + 1
+    cnt = N * Ho * Wo
+    dev = xs[0].device
+    slot = REP * 2 * C
+    edges, off = [], 0
+    for i in range(E):
+        edges.append(_Edge(i, xs[i], ws[i], specs[i], bns[i], params_list[i]))
+    nslots = sum(e.spec.nbn for e in edges)
+    stats = zeros64(max(nslots, 1) * slot, dev) if training else None
+    base = 0
+    for e in edges:
+        e.slot0 = base
+        e.refs = [_bn(stats[(base + i) * slot:(base + i + 1) * slot] if training else None, e.bn[i][0],
+                      e.bn[i][1], cnt, training, eps, C) for i in range(e.spec.nbn)]
+        base += e.spec.nbn
+
+    def st(e, i):
+        return stats[(e.slot0 + i) * slot:(e.slot0 + i + 1) * slot] if training else None
+
+    def new():
+        return torch.empty(N, C, Ho, Wo, device=dev)
+
+    # ---- stage 1: grouped by (K, dilation, stride, pad)
+    dw_groups = defaultdict(list)
+    pool_groups = defaultdict(list)
+    fr_calls = []
+    stage1, stage2 = [], []
+    for e in edges:
+        for k, prim in enumerate(e.spec.prims):
+            if prim == "none":
+                continue
+            sl = e.spec.slots.get(prim, ())
+            if prim.startswith("separable_convolution"):
+                K = int(prim[-1])
+                d1, z1 = new(), new()
+                dw_groups[(K, 1, e.S, K // 2)].append(
+                    (e.x, e.P[prim + ".0.dw"], e.P[prim + ".0.pw"], None, d1, z1, st(e, sl[0])))
+                e.saved[prim] = [d1, z1]
+                stage1.append(e.slot0 + sl[0])
+                stage2.append(e.slot0 + sl[1])
+            elif prim.startswith("dilated_convolution"):
+                K = int(prim[-1])
+                d, z = new(), new()
+                dw_groups[(K, 2, e.S, (K // 2) * 2)].append(
+                    (e.x, e.P[prim + ".dw"], e.P[prim + ".pw"], None, d, z, st(e, sl[0])))
+                e.zs[k], e.bns[k] = z, e.refs[sl[0]]
+                e.saved[prim] = (d, z)
+                stage1.append(e.slot0 + sl[0])
+            elif prim in ("avg_pooling_3x3", "max_pooling_3x3"):
+                if "pool" not in e.saved:
+                    za, zm = new(), new()
+                    am = torch.empty(N, C, Ho, Wo, dtype=torch.uint8, device=dev)
+                    sa = e.spec.slots.get("avg_pooling_3x3")
+                    sm = e.spec.slots.get("max_pooling_3x3")
+                    pool_groups[e.S].append((e.x, za, zm, st(e, sa[0]) if sa else None,
+                                             st(e, sm[0]) if sm else None, am))
+                    e.saved["pool"] = (za, zm, am)
+                e.zs[k] = e.saved["pool"][0 if prim == "avg_pooling_3x3" else 1]
+                e.bns[k] = e.refs[sl[0]]
+                stage1.append(e.slot0 + sl[0])
+            elif prim == "skip_connection":
+                if e.S == 1:
+                    e.id_idx, e.xid = k, e.x
+                    continue
+                z = new()
+                fr_calls.append((e.x, e.P[prim + ".conv1"], z, st(e, sl[0]), 0, 0))
+                fr_calls.append((e.x, e.P[prim + ".conv2"], z, st(e, sl[0]), C // 2, 1))
+                e.zs[k], e.bns[k] = z, e.refs[sl[0]]
+                e.saved[prim] = (z,)
+                stage1.append(e.slot0 + sl[0])
+            else:
+                raise ValueError(prim)
+            e.widx.append(k)
+    for (K, dil, S, pad), calls in dw_groups.items():
+        _launch("dwpw_fwd", calls, K, dil, S, pad, True)
+    for S, calls in pool_groups.items():
+        _launch("pool_fwd", calls, S)
+    if fr_calls:
+        _launch("pw_fwd", fr_calls, 2)
+    if training and stage1:
+        _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage1))])
+    # ---- separable stage 2 (stride 1, input BN-apply prologue)
+    s2_groups = defaultdict(list)
+    for e in edges:
+        for k, prim in enumerate(e.spec.prims):
+            if prim.startswith("separable_convolution"):
+                K = int(prim[-1])
+                sl = e.spec.slots[prim]
+                d1, z1 = e.saved[prim]
+                d2, z2 = new(), new()
+                s2_groups[K].append((z1, e.P[prim + ".1.dw"], e.P[prim + ".1.pw"], e.refs[sl[0]], d2, z2,
+                                     st(e, sl[1])))
+                e.upd.append(e.refs[sl[0]])
+                e.zs[k], e.bns[k] = z2, e.refs[sl[1]]
+                e.saved[prim] = (d1, z1, d2, z2)
+    for K, calls in s2_groups.items():
+        _launch("dwpw_fwd", calls, K, 1, 1, K // 2, True)
+    if training and stage2:
+        _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage2))])
+    # ---- weighted sums into the node output
+    if out is None:
+        out = torch.empty(N, C, Ho, Wo, device=dev)
+    ccalls = []
+    for e in edges:
+        e.zl = [e.zs[k] for k in e.widx]
+        e.bl = [e.bns[k] for k in e.widx]
+        ccalls.append((e.zl, e.bl, e.widx, e.w, e.id_idx, e.xid, e.upd if training else []))
+    cap = _CAP["combine_fwd"]
+    for i in range(0, E, cap):
+        _K.combine_fwd(ccalls[i:i + cap], None, None, out, momentum, training, i > 0)
+    return out, edges
+
+
+def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
+    """One node's backward. ``gx_of(i)`` is the input-gradient buffer of edge i (edges of
+    different nodes that read the same state share one buffer); ``take_first(i)`` is True for
+    the first kernel that writes it (it overwrites instead of accumulating, so no memset);
+    weight gradients go through ``sinks`` under the keys ``pkey(edge, name)``. Buffers no
+    kernel wrote (an edge whose only primitive is ``none``) are the caller's to zero.
+    The alpha-weight gradients stay in ``edge.gw`` (f64, folded)."""
+    E = len(edges)
+    dout = dout.contiguous()
+    dev = dout.device
+
+    def sink(e, name):
+        return sinks.get(e.P[name], pkey(e, name))
+
+    # ---- BN-backward sums and d(alpha) for every edge, one fold
+    sizes = []
+    for e in edges:
+        e.nred = (len(e.zl) + 1) * C + 1
+        sizes.append(REP * (e.nred + e.w.numel()))
+    buf = zeros64(sum(sizes), dev)
+    o = 0
+    calls, segs = [], []
+    for e, sz in zip(edges, sizes):
+        e.red = buf[o:o + REP * e.nred]
+        e.gw = buf[o + REP * e.nred:o + sz]
+        o += sz
+        calls.append((dout, e.zl, e.bl, e.x if e.id_idx >= 0 else None, e.red, e.widx, e.id_idx, e.gw))
+        segs += [(e.red, e.nred, e.nred), (e.gw, e.w.numel(), e.w.numel())]
+    _launch("combine_bwd_reduce", calls)
+    _K.fold_f64(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
+
+    def src(e, k, z):  # GradSrc of a weighted, BN'd op output
+        j = e.widx.index(k)
+        return (dout, z, e.red[:C], e.red[(1 + j) * C:(2 + j) * C], e.bl[j], e.w, k, _R, e.nred)
+
+    gxs = [gx_of(e.i) for e in edges]
+
+    # ---- separable convs: both second stages, one fold, both first stages
+    seps = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("separable_convolution")]
+    if seps:
+        red1 = zeros64(len(seps) * REP * 2 * C, dev) if training else None
+        pw2, dw2 = [], defaultdict(list)
+        for n, (e, k, prim) in enumerate(seps):
+            K = int(prim[-1])
+            d1, z1, d2, z2 = e.saved[prim]
+            dd2 = torch.empty_like(d2)
+            g, gst = sink(e, prim + ".1.pw")
+            pw2.append((src(e, k, z2), e.P[prim + ".1.pw"], d2, z1, dd2, None, g, 0, 0, gst))
+            g1 = torch.empty_like(z1)
+            r1 = red1[n * REP * 2 * C:(n + 1) * REP * 2 * C] if training else None
+            g, gst = sink(e, prim + ".1.dw")
+            dw2[K].append((z1, e.refs[e.spec.slots[prim][0]], e.P[prim + ".1.dw"], dd2, g1, g, r1, gst, False))
+            e.saved[prim + "/g1"] = (g1, r1)
+        _launch("pw_bwd", pw2, 1, 0, True)
+        for K, calls in dw2.items():
+            _launch("dw_bwd", calls, K, 1, 1, K // 2)
+        if training:
+            _fold64([(red1[n * REP * 2 * C:(n + 1) * REP * 2 * C], 2 * C, 2 * C) for n in range(len(seps))])
+        pw1, dw1 = [], defaultdict(list)
+        for e, k, prim in seps:
+            K = int(prim[-1])
+            d1, z1, d2, z2 = e.saved[prim]
+            g1, r1 = e.saved[prim + "/g1"]
+            b1 = e.refs[e.spec.slots[prim][0]]
+            gs1 = (g1, z1, r1[:C] if training else None, r1[C:2 * C] if training else None, b1, None, 0, _R, 2 * C)
+            dd1 = torch.empty_like(d1)
+            g, gst = sink(e, prim + ".0.pw")
+            pw1.append((gs1, e.P[prim + ".0.pw"], d1, e.x, dd1, None, g, 0, 0, gst))
+            g, gst = sink(e, prim + ".0.dw")
+            dw1[(K, e.S)].append((e.x, None, e.P[prim + ".0.dw"], dd1, gxs[e.i], g, None, gst, take_first(e.i)))
+        _launch("pw_bwd", pw1, 1, 0, True)
+        for (K, S), calls in dw1.items():
+            _launch("dw_bwd", calls, K, 1, S, K // 2)
+    # ---- dilated convs
+    dils = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("dilated_convolution")]
+    if dils:
+        pwd, dwd = [], defaultdict(list)
+        for e, k, prim in dils:
+            K = int(prim[-1])
+            d, z = e.saved[prim]
+            dd = torch.empty_like(d)
+            g, gst = sink(e, prim + ".pw")
+            pwd.append((src(e, k, z), e.P[prim + ".pw"], d, e.x, dd, None, g, 0, 0, gst))
+            g, gst = sink(e, prim + ".dw")
+            dwd[(K, e.S)].append((e.x, None, e.P[prim + ".dw"], dd, gxs[e.i], g, None, gst, take_first(e.i)))
+        _launch("pw_bwd", pwd, 1, 0, True)
+        for (K, S), calls in dwd.items():
+            _launch("dw_bwd", calls, K, 2, S, (K // 2) * 2)
+    # ---- pools (+ the identity skip of stride-1 edges)
+    pools = defaultdict(list)
+    for e in edges:
+        if "pool" not in e.saved:
+            continue
+        za, zm, am = e.saved["pool"]
+        ga = gm = None
+        for k, p in enumerate(e.spec.prims):
+            if p == "avg_pooling_3x3":
+                ga = src(e, k, za)
+            elif p == "max_pooling_3x3":
+                gm = src(e, k, zm)
+        pools[e.S].append((ga, gm, e.x, dout if e.id_idx >= 0 else None, e.w, e.id_idx, gxs[e.i], am,
+                           take_first(e.i)))
+        e.id_done = True
+    for S, calls in pools.items():
+        _launch("pool_bwd", calls, S)
+    for e in edges:
+        if e.id_idx >= 0 and not e.id_done:
+            if take_first(e.i):
+                torch.mul(dout, e.w[e.id_idx], out=gxs[e.i])
+            else:
+                gxs[e.i].add_(dout * e.w[e.id_idx])
+    # ---- stride-2 skip (FactorizedReduce): scattered adds, so its gx must exist already
+    frc = []
+    for e in edges:
+        if "skip_connection" in e.saved:
+            if take_first(e.i):
+                gxs[e.i].zero_()
+            k = e.spec.prims.index("skip_connection")
+            (z,) = e.saved["skip_connection"]
+            gs = src(e, k, z)
+            g, gst = sink(e, "skip_connection.conv1")
+            frc.append((gs, e.P["skip_connection.conv1"], None, e.x, None, gxs[e.i], g, 0, 0, gst))
+            g, gst = sink(e, "skip_connection.conv2")
+            frc.append((gs, e.P["skip_connection.conv2"], None, e.x, None, gxs[e.i], g, C // 2, 1, gst))
+    if frc:
+        _launch("pw_bwd", frc, 2, 1, True)
+
+
 class _MixedNode(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, *flat):
         specs, bns, training, momentum, eps, nparams = meta
         E = len(specs)
-        xs = [t.contiguous() for t in flat[:E]]
-        ws = flat[E:2 * E]
-        params = flat[2 * E:]
-        N, C = xs[0].shape[:2]
-        S0 = specs[0].stride
-        Ho = (xs[0].shape[2] - 1) // S0 + 1
-        Wo = (xs[0].shape[3] - 1) // S0 + 1
-        cnt = N * Ho * Wo
-        dev = xs[0].device
-        slot = REP * 2 * C
-        edges, off = [], 0
-        for i in range(E):
-            edges.append(_Edge(i, xs[i], ws[i], specs[i], bns[i], params[off:off + nparams[i]]))
-            off += nparams[i]
-        nslots = sum(e.spec.nbn for e in edges)
-        stats = zeros64(max(nslots, 1) * slot, dev) if training else None
-        base = 0
-        for e in edges:
-            e.slot0 = base
-            e.refs = [_bn(stats[(base + i) * slot:(base + i + 1) * slot] if training else None, e.bn[i][0],
-                          e.bn[i][1], cnt, training, eps, C) for i in range(e.spec.nbn)]
-            base += e.spec.nbn
-
-        def st(e, i):
-            return stats[(e.slot0 + i) * slot:(e.slot0 + i + 1) * slot] if training else None
-
-        def new():
-            return torch.empty(N, C, Ho, Wo, device=dev)
-
-        # ---- stage 1: grouped by (K, dilation, stride, pad)
-        dw_groups = defaultdict(list)
-        pool_groups = defaultdict(list)
-        fr_calls = []
-        stage1, stage2 = [], []
-        for e in edges:
-            for k, prim in enumerate(e.spec.prims):
-                if prim == "none":
-                    continue
-                sl = e.spec.slots.get(prim, ())
-                if prim.startswith("separable_convolution"):
-                    K = int(prim[-1])
-                    d1, z1 = new(), new()
-                    dw_groups[(K, 1, e.S, K // 2)].append(
-                        (e.x, e.P[prim + ".0.dw"], e.P[prim + ".0.pw"], None, d1, z1, st(e, sl[0])))
-                    e.saved[prim] = [d1, z1]
-                    stage1.append(e.slot0 + sl[0])
-                    stage2.append(e.slot0 + sl[1])
-                elif prim.startswith("dilated_convolution"):
-                    K = int(prim[-1])
-                    d, z = new(), new()
-                    dw_groups[(K, 2, e.S, (K // 2) * 2)].append(
-                        (e.x, e.P[prim + ".dw"], e.P[prim + ".pw"], None, d, z, st(e, sl[0])))
-                    e.zs[k], e.bns[k] = z, e.refs[sl[0]]
-                    e.saved[prim] = (d, z)
-                    stage1.append(e.slot0 + sl[0])
-                elif prim in ("avg_pooling_3x3", "max_pooling_3x3"):
-                    if "pool" not in e.saved:
-                        za, zm = new(), new()
-                        am = torch.empty(N, C, Ho, Wo, dtype=torch.uint8, device=dev)
-                        sa = e.spec.slots.get("avg_pooling_3x3")
-                        sm = e.spec.slots.get("max_pooling_3x3")
-                        pool_groups[e.S].append((e.x, za, zm, st(e, sa[0]) if sa else None,
-                                                 st(e, sm[0]) if sm else None, am))
-                        e.saved["pool"] = (za, zm, am)
-                    e.zs[k] = e.saved["pool"][0 if prim == "avg_pooling_3x3" else 1]
-                    e.bns[k] = e.refs[sl[0]]
-                    stage1.append(e.slot0 + sl[0])
-                elif prim == "skip_connection":
-                    if e.S == 1:
-                        e.id_idx, e.xid = k, e.x
-                        continue
-                    z = new()
-                    fr_calls.append((e.x, e.P[prim + ".conv1"], z, st(e, sl[0]), 0, 0))
-                    fr_calls.append((e.x, e.P[prim + ".conv2"], z, st(e, sl[0]), C // 2, 1))
-                    e.zs[k], e.bns[k] = z, e.refs[sl[0]]
-                    e.saved[prim] = (z,)
-                    stage1.append(e.slot0 + sl[0])
-                else:
-                    raise ValueError(prim)
-                e.widx.append(k)
-        for (K, dil, S, pad), calls in dw_groups.items():
-            _launch("dwpw_fwd", calls, K, dil, S, pad, True)
-        for S, calls in pool_groups.items():
-            _launch("pool_fwd", calls, S)
-        if fr_calls:
-            _launch("pw_fwd", fr_calls, 2)
-        if training and stage1:
-            _K.fold_f64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage1))])
-        # ---- separable stage 2 (stride 1, input BN-apply prologue)
-        s2_groups = defaultdict(list)
-        for e in edges:
-            for k, prim in enumerate(e.spec.prims):
-                if prim.startswith("separable_convolution"):
-                    K = int(prim[-1])
-                    sl = e.spec.slots[prim]
-                    d1, z1 = e.saved[prim]
-                    d2, z2 = new(), new()
-                    s2_groups[K].append((z1, e.P[prim + ".1.dw"], e.P[prim + ".1.pw"], e.refs[sl[0]], d2, z2,
-                                         st(e, sl[1])))
-                    e.upd.append(e.refs[sl[0]])
-                    e.zs[k], e.bns[k] = z2, e.refs[sl[1]]
-                    e.saved[prim] = (d1, z1, d2, z2)
-        for K, calls in s2_groups.items():
-            _launch("dwpw_fwd", calls, K, 1, 1, K // 2, True)
-        if training and stage2:
-            _K.fold_f64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage2))])
-        # ---- weighted sums into the node output
-        out = torch.empty(N, C, Ho, Wo, device=dev)
-        ccalls = []
-        for e in edges:
-            e.zl = [e.zs[k] for k in e.widx]
-            e.bl = [e.bns[k] for k in e.widx]
-            ccalls.append((e.zl, e.bl, e.widx, e.w, e.id_idx, e.xid, e.upd if training else []))
-        cap = _CAP["combine_fwd"]
-        for i in range(0, E, cap):
-            _K.combine_fwd(ccalls[i:i + cap], None, None, out, momentum, training, i > 0)
-        ctx.meta = (edges, training, C)
+        params, off = [], 2 * E
+        for n in nparams:
+            params.append(flat[off:off + n])
+            off += n
+        out, edges = _node_forward(flat[:E], flat[E:2 * E], specs, bns, params, training, momentum, eps)
+        ctx.meta = (edges, training, out.shape[1])
         ctx.save_for_backward(*flat)
         return out
 
@@ -334,135 +485,21 @@ class _MixedNode(torch.autograd.Function):
         flat = ctx.saved_tensors
         edges, training, C = ctx.meta
         E = len(edges)
-        dout = dout.contiguous()
-        dev = dout.device
         sinks = _Sinks()
         pbase, acc = [], 2 * E
         for e in edges:
             pbase.append(acc)
             acc += len(e.spec.pnames)
-
-        def sink(e, name):
-            return sinks.get(e.P[name], pbase[e.i] + e.spec.pidx[name])
-
-        # ---- BN-backward sums and d(alpha) for every edge, one fold
-        sizes = []
-        for e in edges:
-            e.nred = (len(e.zl) + 1) * C + 1
-            sizes.append(REP * (e.nred + e.w.numel()))
-        buf = zeros64(sum(sizes), dev)
-        o = 0
-        calls, segs = [], []
-        for e, sz in zip(edges, sizes):
-            e.red = buf[o:o + REP * e.nred]
-            e.gw = buf[o + REP * e.nred:o + sz]
-            o += sz
-            calls.append((dout, e.zl, e.bl, e.x if e.id_idx >= 0 else None, e.red, e.widx, e.id_idx, e.gw))
-            segs += [(e.red, e.nred, e.nred), (e.gw, e.w.numel(), e.w.numel())]
-        _launch("combine_bwd_reduce", calls)
-        _K.fold_f64(segs)
-
-        def src(e, k, z):  # GradSrc of a weighted, BN'd op output
-            j = e.widx.index(k)
-            return (dout, z, e.red[:C], e.red[(1 + j) * C:(2 + j) * C], e.bl[j], e.w, k, 1, e.nred)
-
         gxs = [torch.empty_like(e.x) for e in edges]
-        first = [True] * E  # the first kernel writing gx[e] overwrites it
+        first = [True] * E
 
         def take_first(i):
             f = first[i]
             first[i] = False
             return f
 
-        # ---- separable convs: both second stages, one fold, both first stages
-        seps = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("separable_convolution")]
-        if seps:
-            red1 = zeros64(len(seps) * REP * 2 * C, dev) if training else None
-            pw2, dw2 = [], defaultdict(list)
-            for n, (e, k, prim) in enumerate(seps):
-                K = int(prim[-1])
-                d1, z1, d2, z2 = e.saved[prim]
-                dd2 = torch.empty_like(d2)
-                g, gst = sink(e, prim + ".1.pw")
-                pw2.append((src(e, k, z2), e.P[prim + ".1.pw"], d2, z1, dd2, None, g, 0, 0, gst))
-                g1 = torch.empty_like(z1)
-                r1 = red1[n * REP * 2 * C:(n + 1) * REP * 2 * C] if training else None
-                g, gst = sink(e, prim + ".1.dw")
-                dw2[K].append((z1, e.refs[e.spec.slots[prim][0]], e.P[prim + ".1.dw"], dd2, g1, g, r1, gst, False))
-                e.saved[prim + "/g1"] = (g1, r1)
-            _launch("pw_bwd", pw2, 1, 0, True)
-            for K, calls in dw2.items():
-                _launch("dw_bwd", calls, K, 1, 1, K // 2)
-            if training:
-                _K.fold_f64([(red1[n * REP * 2 * C:(n + 1) * REP * 2 * C], 2 * C, 2 * C) for n in range(len(seps))])
-            pw1, dw1 = [], defaultdict(list)
-            for e, k, prim in seps:
-                K = int(prim[-1])
-                d1, z1, d2, z2 = e.saved[prim]
-                g1, r1 = e.saved[prim + "/g1"]
-                b1 = e.refs[e.spec.slots[prim][0]]
-                gs1 = (g1, z1, r1[:C] if training else None, r1[C:2 * C] if training else None, b1, None, 0, 1, 2 * C)
-                dd1 = torch.empty_like(d1)
-                g, gst = sink(e, prim + ".0.pw")
-                pw1.append((gs1, e.P[prim + ".0.pw"], d1, e.x, dd1, None, g, 0, 0, gst))
-                g, gst = sink(e, prim + ".0.dw")
-                dw1[(K, e.S)].append((e.x, None, e.P[prim + ".0.dw"], dd1, gxs[e.i], g, None, gst, take_first(e.i)))
-            _launch("pw_bwd", pw1, 1, 0, True)
-            for (K, S), calls in dw1.items():
-                _launch("dw_bwd", calls, K, 1, S, K // 2)
-        # ---- dilated convs
-        dils = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("dilated_convolution")]
-        if dils:
-            pwd, dwd = [], defaultdict(list)
-            for e, k, prim in dils:
-                K = int(prim[-1])
-                d, z = e.saved[prim]
-                dd = torch.empty_like(d)
-                g, gst = sink(e, prim + ".pw")
-                pwd.append((src(e, k, z), e.P[prim + ".pw"], d, e.x, dd, None, g, 0, 0, gst))
-                g, gst = sink(e, prim + ".dw")
-                dwd[(K, e.S)].append((e.x, None, e.P[prim + ".dw"], dd, gxs[e.i], g, None, gst, take_first(e.i)))
-            _launch("pw_bwd", pwd, 1, 0, True)
-            for (K, S), calls in dwd.items():
-                _launch("dw_bwd", calls, K, 2, S, (K // 2) * 2)
-        # ---- pools (+ the identity skip of stride-1 edges)
-        pools = defaultdict(list)
-        for e in edges:
-            if "pool" not in e.saved:
-                continue
-            za, zm, am = e.saved["pool"]
-            ga = gm = None
-            for k, p in enumerate(e.spec.prims):
-                if p == "avg_pooling_3x3":
-                    ga = src(e, k, za)
-                elif p == "max_pooling_3x3":
-                    gm = src(e, k, zm)
-            pools[e.S].append((ga, gm, e.x, dout if e.id_idx >= 0 else None, e.w, e.id_idx, gxs[e.i], am,
-                               take_first(e.i)))
-            e.id_done = True
-        for S, calls in pools.items():
-            _launch("pool_bwd", calls, S)
-        for e in edges:
-            if e.id_idx >= 0 and not e.id_done:
-                if take_first(e.i):
-                    torch.mul(dout, e.w[e.id_idx], out=gxs[e.i])
-                else:
-                    gxs[e.i].add_(dout * e.w[e.id_idx])
-        # ---- stride-2 skip (FactorizedReduce): scattered adds, so its gx must exist already
-        frc = []
-        for e in edges:
-            if "skip_connection" in e.saved:
-                if take_first(e.i):
-                    gxs[e.i].zero_()
-                k = e.spec.prims.index("skip_connection")
-                (z,) = e.saved["skip_connection"]
-                gs = src(e, k, z)
-                g, gst = sink(e, "skip_connection.conv1")
-                frc.append((gs, e.P["skip_connection.conv1"], None, e.x, None, gxs[e.i], g, 0, 0, gst))
-                g, gst = sink(e, "skip_connection.conv2")
-                frc.append((gs, e.P["skip_connection.conv2"], None, e.x, None, gxs[e.i], g, C // 2, 1, gst))
-        if frc:
-            _launch("pw_bwd", frc, 2, 1, True)
+        _node_backward(edges, training, C, dout, lambda i: gxs[i], take_first, sinks,
+                       lambda e, name: pbase[e.i] + e.spec.pidx[name])
         for i in range(E):
             if first[i]:  # an edge whose only primitive is "none"
                 gxs[i].zero_()
@@ -490,58 +527,186 @@ def mixed_edge(x, w, spec: EdgeSpec, bn: List[Tuple[torch.Tensor, torch.Tensor]]
 
 
 # --------------------------------------------------------------------------------- preprocess
-class _StdConvBN(torch.autograd.Function):
-    """ReLU -> 1x1 conv (ReLUConvBN, operations.py) or FactorizedReduce (two stride-2
-    1x1 convs on offset grids, channel-concatenated) -> BN(affine=False)."""
+def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2):
+    """ReLU -> 1x1 conv (ReLUConvBN, operations.py) or FactorizedReduce (two stride-2 1x1
+    convs on offset grids, channel-concatenated) -> BN(affine=False). Returns (out, state)."""
+    x = x.contiguous()
+    N, Cin, H, W = x.shape
+    fr = w2 is not None
+    Cout = w1.shape[0] * (2 if fr else 1)
+    Ho, Wo = (H // 2, W // 2) if fr else (H, W)
+    cnt = N * Ho * Wo
+    stats = zeros64(REP * 2 * Cout, x.device) if training else None
+    z = torch.empty(N, Cout, Ho, Wo, device=x.device)
+    if fr:
+        _K.pw_fwd([(x, w1, z, stats, 0, 0), (x, w2, z, stats, Cout // 2, 1)], 2)
+    else:
+        _K.pw_fwd([(x, w1, z, stats, 0, 0)], 1)
+    if training:
+        _fold64([(stats, 2 * Cout, 2 * Cout)])
+    bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
+    out = torch.empty_like(z)
+    _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], None, None, out, momentum, training, False)
+    return out, (x, z, w1, w2, bn, fr, Cout, training)
 
+
+def _stdconv_backward(state, dout, need_x, sinks, keys):
+    """Returns the input gradient (or None); weight gradients through ``sinks``."""
+    x, z, w1, w2, bn, fr, Cout, training = state
+    dout = dout.contiguous()
+    nred = 2 * Cout + 1
+    red = zeros64(REP * nred, x.device)
+    if training:
+        _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
+        _fold64([(red, nred, nred)])
+    gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0, _R, nred)
+    g1, s1 = sinks.get(w1, keys[0])
+    if fr:  # the two stride-2 grids leave 3 of 4 input pixels untouched: start from zeros
+        gx = torch.zeros_like(x) if need_x else None
+        g2, s2 = sinks.get(w2, keys[1])
+        _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1), (gs, w2, None, x, None, gx, g2, Cout // 2, 1, s2)],
+                  2, 1, need_x)
+    else:  # stride 1 covers every input pixel: the kernel overwrites gx (no fill)
+        gx = torch.empty_like(x) if need_x else None
+        _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1, True)], 1, 1, need_x)
+    return gx
+
+
+class _StdConvBN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, rm, rv, training, momentum, eps, w1, w2):
-        x = x.contiguous()
-        N, Cin, H, W = x.shape
-        fr = w2 is not None
-        Cout = w1.shape[0] * (2 if fr else 1)
-        Ho, Wo = (H // 2, W // 2) if fr else (H, W)
-        cnt = N * Ho * Wo
-        stats = zeros64(REP * 2 * Cout, x.device) if training else None
-        z = torch.empty(N, Cout, Ho, Wo, device=x.device)
-        if fr:
-            _K.pw_fwd([(x, w1, z, stats, 0, 0), (x, w2, z, stats, Cout // 2, 1)], 2)
-        else:
-            _K.pw_fwd([(x, w1, z, stats, 0, 0)], 1)
-        if training:
-            _K.fold_f64([(stats, 2 * Cout, 2 * Cout)])
-        bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
-        out = torch.empty_like(z)
-        _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], None, None, out, momentum, training, False)
-        ctx.meta = (bn, fr, Cout, training)
-        ctx.save_for_backward(x, z, w1, *([w2] if fr else []))
+        out, state = _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2)
+        ctx.state = state
+        ctx.save_for_backward(x, w1, *([w2] if w2 is not None else []))
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, z, w1, *rest = ctx.saved_tensors
-        w2 = rest[0] if rest else None
-        bn, fr, Cout, training = ctx.meta
-        dout = dout.contiguous()
-        nred = 2 * Cout + 1
-        red = zeros64(REP * nred, x.device)
-        if training:
-            _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
-            _K.fold_f64([(red, nred, nred)])
-        gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0, 1, nred)
-        need_x = ctx.needs_input_grad[0]
-        gx = torch.zeros_like(x) if need_x else None
         sinks = _Sinks()
         grads = [None, None, None]
-        g1, s1 = sinks.get(w1, 1)
-        if fr:
-            g2, s2 = sinks.get(w2, 2)
-            _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1), (gs, w2, None, x, None, gx, g2, Cout // 2, 1, s2)],
-                      2, 1, need_x)
-        else:
-            _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1)], 1, 1, need_x)
+        gx = _stdconv_backward(ctx.state, dout, ctx.needs_input_grad[0], sinks, (1, 2))
+        ctx.state = None
         sinks.finish(grads)
         return gx, None, None, None, None, None, grads[1], grads[2]
+
+
+# --------------------------------------------------------------------------------- cell
+class CellSpec:
+    """Static description of one DARTS cell for :func:`cell_forward`: the two preprocess
+    layers (``(kind, param names, bn name)``, kind ``std`` or ``fr``) and, per node, its
+    edges as ``(EdgeSpec, param names, bn names, source state, alpha row)``."""
+
+    def __init__(self, pre0, pre1, nodes, C):
+        self.pre0, self.pre1, self.nodes, self.C = pre0, pre1, nodes, C
+        self.names = list(pre0[1]) + list(pre1[1])
+        for node in nodes:
+            for _, pnames, _, _, _ in node:
+                self.names += pnames
+        self.index = {n: i for i, n in enumerate(self.names)}
+
+
+class _Cell(torch.autograd.Function):
+    """A whole cell - preprocess(s0), preprocess(s1), every node, the concat - as ONE autograd
+    Function with a hand-scheduled backward. Node outputs are written straight into a
+    node-major buffer [nodes][N][C][H][W] (one transpose copy makes the concat), and the
+    backward keeps one gradient buffer per cell state: nodes run in reverse, each edge's input
+    gradient goes into its source state's buffer (the first kernel to touch a buffer
+    overwrites it, later ones accumulate), so the per-consumer gradient buffers, their
+    autograd additions, the concat-slice copies and the zero fills of the per-node path
+    disappear. The alpha gradients of all edges come back as one [rows, K] tensor."""
+
+    @staticmethod
+    def forward(ctx, meta, s0, s1, wts, *params):
+        spec, bn_of, training, momentum, eps = meta
+        P = dict(zip(spec.names, params))
+        def pre(x, p):
+            kind, pnames, bname = p
+            rm, rv = bn_of(bname)
+            if kind == "fr":
+                return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], P[pnames[1]])
+            return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], None)
+        t0, st0 = pre(s0, spec.pre0)
+        t1, st1 = pre(s1, spec.pre1)
+        states = [t0, t1]
+        N, C = t0.shape[0], spec.C
+        nn_ = len(spec.nodes)
+        S = [e[0].stride for e in spec.nodes[0]]
+        Ho = (t0.shape[2] - 1) // max(S) + 1 if S else t0.shape[2]
+        Wo = (t0.shape[3] - 1) // max(S) + 1 if S else t0.shape[3]
+        O = torch.empty(nn_, N, C, Ho, Wo, device=t0.device)
+        node_states = []
+        for i, node in enumerate(spec.nodes):
+            xs = [states[src] for _, _, _, src, _ in node]
+            ws = [wts[row] for _, _, _, _, row in node]
+            specs = [es for es, _, _, _, _ in node]
+            bns = [[bn_of(b) for b in bnames] for _, _, bnames, _, _ in node]
+            plist = [[P[n] for n in pnames] for _, pnames, _, _, _ in node]
+            out, edges = _node_forward(xs, ws, specs, bns, plist, training, momentum, eps, out=O[i])
+            states.append(out)
+            node_states.append(edges)
+        y = O.permute(1, 0, 2, 3, 4).reshape(N, nn_ * C, Ho, Wo)
+        ctx.cell = (spec, training, st0, st1, node_states, states, wts.shape)
+        ctx.save_for_backward(s0, s1, wts, *params)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        spec, training, st0, st1, node_states, states, wshape = ctx.cell
+        ctx.cell = None
+        saved = ctx.saved_tensors
+        params = saved[3:]
+        nn_ = len(spec.nodes)
+        N, C = dy.shape[0], spec.C
+        Ho, Wo = dy.shape[2], dy.shape[3]
+        # node-major copy of the incoming gradient: one buffer per node state
+        gO = dy.reshape(N, nn_, C * Ho * Wo).transpose(0, 1).contiguous().view(nn_, N, C, Ho, Wo)
+        gS = [None, None] + [gO[i] for i in range(nn_)]
+        first = [True, True] + [False] * nn_
+        sinks = _Sinks()
+        want_ga = ctx.needs_input_grad[3]
+        ga_rows = [None] * nn_
+        for i in reversed(range(nn_)):
+            node = spec.nodes[i]
+            edges = node_states[i]
+            srcs = [src for _, _, _, src, _ in node]
+            for src in srcs:
+                if gS[src] is None:
+                    gS[src] = torch.empty_like(states[src])
+
+            def take_first(k, srcs=srcs):
+                f = first[srcs[k]]
+                first[srcs[k]] = False
+                return f
+
+            _node_backward(edges, training, C, gS[2 + i], lambda k, srcs=srcs: gS[srcs[k]], take_first, sinks,
+                           lambda e, name, node=node: 4 + spec.index[node[e.i][1][e.spec.pidx[name]]])
+            if want_ga:  # a node's alpha rows are consecutive, nodes in row order
+                ga_rows[i] = [e.gw[:wshape[1]] for e in edges]
+        for j in (0, 1):
+            if first[j]:  # only "none" primitives read this state
+                gS[j] = torch.zeros_like(states[j])
+        grads = [None] * (4 + len(params))
+        need = ctx.needs_input_grad
+        gs0 = _stdconv_backward(st0, gS[0], need[1], sinks, _pre_keys(spec, spec.pre0))
+        gs1 = _stdconv_backward(st1, gS[1], need[2], sinks, _pre_keys(spec, spec.pre1))
+        grads[1], grads[2] = gs0, gs1
+        if want_ga:
+            grads[3] = torch.cat([g for rows in ga_rows for g in rows]).view(wshape).to(torch.float32)
+        sinks.finish(grads)
+        return tuple(grads)
+
+
+def _pre_keys(spec, pre):
+    names = pre[1]
+    return tuple(4 + spec.index[n] for n in names) + ((None,) if len(names) == 1 else ())
+
+
+def cell_forward(spec: CellSpec, s0, s1, wts, params: Sequence[torch.Tensor], bn_of, training: bool,
+                 momentum: float = 0.1, eps: float = 1e-5):
+    """A DARTS cell on the HIP kernels (see :class:`_Cell`). ``wts`` [rows, K] are the
+    softmax weights of this cell type; ``params`` follow ``spec.names``; ``bn_of(name)`` gives
+    the (running mean, running var) views of a BN layer."""
+    return _Cell.apply((spec, bn_of, training, momentum, eps), s0, s1, wts, *params)
 
 
 def relu_conv_bn(x, w, rm, rv, training, momentum=0.1, eps=1e-5):

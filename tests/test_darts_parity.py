@@ -225,8 +225,8 @@ def test_forward_backward_matches_oracle():
     model.train()
     ref_logits = model(x)
     F.cross_entropy(ref_logits, y).backward()
-    loss, logits = ours._loss(x, y, ours.Pw.views, ours.An, ours.Ar, ours.bn)
-    loss.backward(inputs=ours.Pw.list + ours.An + ours.Ar)
+    loss, logits = ours._loss(x, y, ours.Pw.views, *ours._arch(ours.Aw), ours.bn)
+    loss.backward(inputs=ours.Pw.list + ours.Aw)
     torch.testing.assert_close(logits, ref_logits, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(ours.gW, _flat(w.grad for w in model.weights()), rtol=1e-3, atol=1e-5)
     torch.testing.assert_close(ours.gA, _flat(a.grad for a in model.alphas()), rtol=1e-3, atol=1e-6)
