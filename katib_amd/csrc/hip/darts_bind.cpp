@@ -135,6 +135,17 @@ void dwpw_fwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, i
     const int TR = 64 / Wo;
     const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
     a.chunk = pick_chunk(C, IR * IW, C * 64 + 4 * C);
+    if (C == 4 || C == 8) {
+      // dwpw_plane: `chunk` = row bands per image, ~2048 workgroups per launch and >= 4
+      // output rows per band, capped so the staged band fits 64 KB of LDS
+      int nb = std::max(1, std::min(Ho / 4, 2048 / std::max(N * (int)calls.size(), 1)));
+      auto band_bytes = [&](int b) {
+        const int BR = (Ho + b - 1) / b;
+        return (size_t)C * ((BR - 1) * S + (K - 1) * dil + 1) * (W + 2 * pad) * sizeof(float);
+      };
+      while (band_bytes(nb) > 65536 && nb < Ho) ++nb;
+      a.chunk = nb;
+    }
     a.use_mfma = (use_mfma && C % 16 == 0) ? 1 : 0;
     if (i == 0) prebn = inbn.has_value();
     TORCH_CHECK(inbn.has_value() == prebn, "edges in a batch must agree on the input BN");

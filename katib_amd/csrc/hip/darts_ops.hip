@@ -46,13 +46,31 @@ int max_blocks() {
 }
 void set_max_blocks(int n) { g_max_blocks = n; }
 
+// s += p[r*rs], s2 += p[r*rs + off2] over r < rep replicas, 8 replicas (16 loads) in flight per
+// step instead of one dependent load-add per replica
+__device__ __forceinline__ void sum_replicas(const double* p, int rep, int rs, int off2, double& s, double& s2) {
+  s = 0.0;
+  s2 = 0.0;
+  for (int r0 = 0; r0 < rep; r0 += 8) {
+    double a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = r0 + u < rep;
+      a[u] = ok ? p[(size_t)(r0 + u) * rs] : 0.0;
+      b[u] = ok ? p[(size_t)(r0 + u) * rs + off2] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s += a[u];
+      s2 += b[u];
+    }
+  }
+}
+
 // batch mean / biased variance of channel c from the replicated (sum, sum of squares)
 __device__ __forceinline__ void bn_moments(const BNRef& b, int c, double& m, double& v) {
-  double s = 0.0, s2 = 0.0;
-  for (int r = 0; r < b.rep; ++r) {
-    s += b.sums[(size_t)r * b.rstride + c];
-    s2 += b.sums[(size_t)r * b.rstride + b.C + c];
-  }
+  double s, s2;
+  sum_replicas(b.sums + c, b.rep, b.rstride, b.C, s, s2);
   m = s * (double)b.inv_count;
   v = s2 * (double)b.inv_count - m * m;
   if (v < 0) v = 0;
@@ -77,9 +95,11 @@ __device__ __forceinline__ void gs_means(const GradSrc& gs, int c, float& m1, fl
     return;
   }
   double s1 = 0.0, s2 = 0.0;
-  for (int r = 0; r < gs.rep; ++r) {
-    s1 += gs.S1[(size_t)r * gs.rstride + c];
-    s2 += gs.S2[(size_t)r * gs.rstride + c];
+  if (gs.rep == 1) {
+    s1 = gs.S1[c];
+    s2 = gs.S2[c];
+  } else {
+    sum_replicas(gs.S1 + c, gs.rep, gs.rstride, (int)(gs.S2 - gs.S1), s1, s2);
   }
   m1 = (float)(s1 * (double)gs.bn.inv_count);
   m2 = (float)(s2 * (double)gs.bn.inv_count);
@@ -135,6 +155,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
     for (int c0 = 0; c0 < C; c0 += a.chunk) {
       const int cn = min(a.chunk, C - c0);
       const int tot = cn * IR * IW;
+      #pragma unroll 4  // keep several global loads of the staging pass in flight
       for (int i = tid; i < tot; i += 256) {
         int cc = i / (IR * IW), r = (i / IW) % IR, q = i % IW;
         int iy = iy0 + r, ix = ix0 + q, c = c0 + cc;
@@ -223,6 +244,99 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// dwpw_plane: dwpw_fwd for narrow layers (C <= 8). One workgroup per image: the whole input
+// plane of every channel (zero-padded, ReLU / BN-apply+ReLU on the way in) is staged in LDS
+// with one coalesced burst, then each thread owns output pixels with ALL channels in registers:
+// depthwise KxK from LDS, pointwise C x C in registers, BN statistics per thread, one block
+// reduction at the end. Against the 64-pixel tiles (halo rows re-read per tile: 5x the input
+// for a dilated 5x5 on 2-row tiles, a barrier-separated load/compute chain per tile) this
+// reads each input pixel once and has a single barrier before the compute.
+// ------------------------------------------------------------------------------------------------
+template <int K, int DIL, int S, bool PREBN, int C>
+__global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
+  const DwPwFwdArgs& a = bt.e[blockIdx.y];
+  constexpr int KK = K * K;
+  const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, pad = a.pad;
+  // workgroup = (image n, band of BR output rows); the band's input rows + halo are staged
+  const int nb = a.chunk, BR = (Ho + nb - 1) / nb;  // chunk carries the band count
+  const int n = blockIdx.x / nb, band = blockIdx.x - n * nb;
+  const int oy0 = band * BR, oy1 = min(Ho, oy0 + BR);
+  const int HP = (BR - 1) * S + (K - 1) * DIL + 1, WP = W + 2 * pad, PL = HP * WP;
+  const int iyb = oy0 * S - pad;  // input row of staged row 0
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sIn = smem;  // [C][HP][WP]
+  __shared__ float sMean[C], sInv[C], sStat[2 * C];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < C) {
+    if (PREBN) bn_coeffs(a.inbn, tid, sMean[tid], sInv[tid]);
+    sStat[tid] = 0.f;
+    sStat[C + tid] = 0.f;
+  }
+  __syncthreads();
+  // staging: one wave per (channel, row); the row index is wave-uniform, lanes sweep columns
+  const float* xin = a.x + (size_t)n * C * H * W;
+#pragma unroll 4
+  for (int row = wave; row < C * HP; row += 4) {
+    const int c = row / HP, r = row - c * HP, iy = iyb + r;
+    const bool rok = iy >= 0 && iy < H;
+    const float* src = xin + ((size_t)c * H + (rok ? iy : 0)) * W;
+    for (int q = lane; q < WP; q += 64) {
+      const int ix = q - pad;
+      float v = 0.f;
+      if (rok && ix >= 0 && ix < W) {
+        v = src[ix];
+        if (PREBN) v = (v - sMean[c]) * sInv[c];
+        v = fmaxf(v, 0.f);
+      }
+      sIn[row * WP + q] = v;
+    }
+  }
+  __syncthreads();
+  float st1[C], st2[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) st1[c] = st2[c] = 0.f;
+  const int HWo = Ho * Wo;
+  float* dn = a.d + (size_t)n * C * HWo;
+  float* zn = a.z + (size_t)n * C * HWo;
+  for (int p = oy0 * Wo + tid; p < oy1 * Wo; p += 256) {
+    const int oy = p / Wo, ox = p - oy * Wo;
+    float d[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float* src = sIn + c * PL + ((oy - oy0) * S) * WP + ox * S;
+      const float* wk = a.dw + c * KK;  // uniform -> scalar loads
+      float acc = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) acc += wk[ky * K + kx] * src[ky * DIL * WP + kx * DIL];
+      d[c] = acc;
+      dn[(size_t)c * HWo + p] = acc;
+    }
+#pragma unroll
+    for (int co = 0; co < C; ++co) {
+      float z = 0.f;
+#pragma unroll
+      for (int ci = 0; ci < C; ++ci) z += a.pw[co * C + ci] * d[ci];
+      zn[(size_t)co * HWo + p] = z;
+      st1[co] += z;
+      st2[co] += z * z;
+    }
+  }
+  if (!a.stats) return;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float v1 = wave_sum(st1[c]), v2 = wave_sum(st2[c]);
+    if (lane == 0) {
+      atomicAdd(sStat + c, v1);
+      atomicAdd(sStat + C + c, v2);
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * C) atomicAdd(a.stats + rep_slot() * 2 * C + tid, (double)sStat[tid]);
+}
+
+// ------------------------------------------------------------------------------------------------
 // pw_fwd: z[:, co_off + co] = pw . relu(x) at (oy*S + off, ox*S + off); StdConv / FR half
 // grid: N*Ho*Wo/64 blocks of 64-pixel tiles; Cin, Cout <= 256
 // ------------------------------------------------------------------------------------------------
@@ -240,6 +354,7 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdBatch bt) {
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int pix0 = t * P;  // flat over N*Ho*Wo (HWo % 64 == 0)
     const int n = pix0 / HWo, prem = pix0 % HWo;
+    #pragma unroll 4  // keep several global loads of the staging pass in flight
     for (int i = tid; i < Cin * P; i += 256) {
       int ci = i / P, p = i % P;
       int pp = prem + p, oy = pp / Wo, ox = pp % Wo;
@@ -524,11 +639,13 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
   const int nbi = Cin / 16, nblk = (Cout / 16) * nbi;
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int pix0 = t * P, n = pix0 / HWo, prem = pix0 % HWo;
+    #pragma unroll 4  // keep several global loads of the staging pass in flight
     for (int i = tid; i < Cout * P; i += 256) {
       int co = i / P, p = i % P;
       size_t gi = ((size_t)n * a.CoutTotal + a.co_off + co) * HWo + prem + p;
       sDz[co * PS + p] = bn_bwd_val(a.gs, gi, sMean[co], sInv[co], wk, sM1[co], sM2[co]);
     }
+    #pragma unroll 4  // keep several global loads of the staging pass in flight
     for (int i = tid; i < Cin * P; i += 256) {
       int ci = i / P, p = i % P;
       int pp = prem + p;
@@ -784,12 +901,14 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
     const float* ddn = a.dd + (size_t)n * C * Ho * Wo;
     for (int c0 = 0; c0 < C; c0 += a.chunk) {
       const int cn = min(a.chunk, C - c0);
+      #pragma unroll 4  // keep several global loads of the staging pass in flight
       for (int i = tid; i < cn * OR * Wo; i += 256) {
         int cc = i / (OR * Wo), rr = (i / Wo) % OR, q = i % Wo;
         int oy = oy0 - h + rr;
         sDD[i] = (oy >= 0 && oy < Ho) ? ddn[((size_t)(c0 + cc) * Ho + oy) * Wo + q] : 0.f;
       }
       if (a.gW) {
+        #pragma unroll 4  // keep several global loads of the staging pass in flight
         for (int i = tid; i < cn * IR * IW; i += 256) {
           int cc = i / (IR * IW), rr = (i / IW) % IR, q = i % IW;
           int iy = iy0 + rr, ix = -pad + q, c = c0 + cc;
@@ -957,9 +1076,26 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdBatch bt) {
 // ------------------------------------------------------------------------------------------------
 static int per_edge_blocks(int tiles, int n) { return std::max(1, std::min(tiles, max_blocks() / std::max(n, 1))); }
 
+template <int K, int DIL, int S, int C>
+static void launch_dwpw_plane_t(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
+  const DwPwFwdArgs& a = b.e[0];
+  const int nb = a.chunk, BR = (a.Ho + nb - 1) / nb;
+  const size_t lds = sizeof(float) * C * ((BR - 1) * S + (K - 1) * DIL + 1) * (a.W + 2 * a.pad);
+  dim3 grid(a.N * nb, b.n);
+  if (prebn) hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, true, C>), grid, dim3(256), lds, st, b);
+  else hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, false, C>), grid, dim3(256), lds, st, b);
+}
+
+// row-band kernel for C = 4 / 8 (the staged band fits 64 KB of LDS by construction)
+static bool plane_ok(const DwPwFwdArgs& a) { return a.C == 4 || a.C == 8; }
+
 template <int K, int DIL, int S>
 static void launch_dwpw_fwd_t(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
   const DwPwFwdArgs& a = b.e[0];
+  if (plane_ok(a)) {
+    if (a.C == 4) return launch_dwpw_plane_t<K, DIL, S, 4>(b, prebn, st);
+    return launch_dwpw_plane_t<K, DIL, S, 8>(b, prebn, st);
+  }
   const int TR = 64 / a.Wo;
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
   const int IW = (a.Wo - 1) * S + (K - 1) * DIL + 1;
@@ -1048,7 +1184,7 @@ static bool try_pw_bwd_px(const PwBwdBatch& b, hipStream_t st) {
   const PwBwdArgs& a = b.e[0];
   if (a.Cin != CI || a.Cout != CO) return false;
   const int total = a.N * a.Ho * a.Wo;
-  const int per_edge = std::max(1, std::min((total + 1023) / 1024, max_blocks() / std::max(b.n, 1)));
+  const int per_edge = std::max(1, std::min((total + 255) / 256, max_blocks() / std::max(b.n, 1)));
   hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO>), dim3(per_edge, b.n), dim3(256), 0, st, b);
   return true;
 }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Memory-side bytes per DARTS kernel (B5 step, eager): FETCH_SIZE / WRITE_SIZE in their own
+# passes, with the kernel trace for durations -> achieved bandwidth per kernel.
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- \
+  python3 bench.py --steps 2 --warmup 1 --capture 0 --valid-batches 1 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- \
+  python3 bench.py --steps 2 --warmup 1 --capture 0 --valid-batches 1 > gpurun_out/pmc_write.log 2>&1 || exit $?
+python3 scripts/pmc_bw.py gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/darts_b5_bw.txt || exit 1
