@@ -14,7 +14,8 @@ batches of 128, printing ``Training-Accuracy``, ``Training-Loss``,
 
 MI355X specifics: channels-last bf16 convolutions on the hand-written implicit-GEMM
 MFMA kernels (``ops/conv.py``; TF 'same' padding handled inside the kernel's gather,
-depthwise convolutions stay on MIOpen), the train step
+depthwise convolutions stay on MIOpen), batch norm on the NHWC bf16 HIP kernels
+(``ops/batchnorm.py``, channel counts that are multiples of 8), the train step
 captured as a HIP graph, synthetic CIFAR-10-shaped data in HBM, and data parallelism
 over the trial's GPUs (``WORLD_SIZE`` ranks, RCCL all-reduce of the flat gradient)
 in place of ``tf.distribute.MirroredStrategy``.
@@ -31,6 +32,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import batchnorm as hbn
 from ..ops import conv as hconv
 from .common import CapturedStep, Timer, device, pattern_images, report
 
@@ -69,17 +71,17 @@ class Op(nn.Module):
 
         if self.kind == "convolution":
             f, k, s = geti("num_filter", 64), geti("filter_size", 3), geti("stride", 1)
-            self.body = nn.Sequential(_SameConv(cin, f, k, s), nn.BatchNorm2d(f, eps=1e-3, momentum=0.01))
+            self.body = nn.Sequential(_SameConv(cin, f, k, s), hbn.BatchNorm2d(f, eps=1e-3, momentum=0.01))
             self.cout, self.hw = f, -(-hw // s)
         elif self.kind == "separable_convolution":
             f, k, s, dm = geti("num_filter", 64), geti("filter_size", 3), geti("stride", 1), geti("depth_multiplier", 1)
             self.body = nn.Sequential(_SameConv(cin, cin * dm, k, s, groups=cin, bias=False),
-                                      hconv.Conv2d(cin * dm, f, 1), nn.BatchNorm2d(f, eps=1e-3, momentum=0.01))
+                                      hconv.Conv2d(cin * dm, f, 1), hbn.BatchNorm2d(f, eps=1e-3, momentum=0.01))
             self.cout, self.hw = f, -(-hw // s)
         elif self.kind == "depthwise_convolution":
             k, s, dm = geti("filter_size", 3), geti("stride", 1), geti("depth_multiplier", 1)
             self.body = nn.Sequential(_SameConv(cin, cin * dm, k, s, groups=cin),
-                                      nn.BatchNorm2d(cin * dm, eps=1e-3, momentum=0.01))
+                                      hbn.BatchNorm2d(cin * dm, eps=1e-3, momentum=0.01))
             self.cout, self.hw = cin * dm, -(-hw // s)
         elif self.kind == "reduction":
             if hw == 1:
