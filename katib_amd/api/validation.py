@@ -218,11 +218,73 @@ def _validate_trial_template(inst, template_getter):
         raise ValidationError("metadata.name and metadata.namespace in spec.trialTemplate must be omitted")
     if not run_spec.get("apiVersion") or not run_spec.get("kind"):
         raise ValidationError("APIVersion and Kind in spec.trialTemplate must be specified")
-    if run_spec.get("kind") == C.JOB_KIND_JOB and str(run_spec.get("apiVersion")).startswith("batch/"):
-        containers = (((run_spec.get("spec") or {}).get("template") or {}).get("spec") or {}).get("containers")
-        if not isinstance(containers, list) or not containers:
-            raise ValidationError("invalid spec.trialTemplate: unable to convert spec.TrialTemplate to Job: "
-                                  "spec.template.spec.containers is required")
+    validate_trial_job(run_spec)
+
+
+# Field sets of the batch/v1 Job object graph down to the containers. A template field
+# outside them would be dropped by the typed conversion, which the reference rejects
+# (validator.go:376-421: convert to batchv1.Job, diff, only "remove" ops allowed).
+# ``None`` marks a subtree that is not checked further.
+_CONTAINER = dict.fromkeys((
+    "name", "image", "command", "args", "workingDir", "ports", "envFrom", "env", "resources", "resizePolicy",
+    "restartPolicy", "volumeMounts", "volumeDevices", "livenessProbe", "readinessProbe", "startupProbe",
+    "lifecycle", "terminationMessagePath", "terminationMessagePolicy", "imagePullPolicy", "securityContext",
+    "stdin", "stdinOnce", "tty"))
+_CONTAINER.update(command=[None], args=[None])
+_POD_SPEC = dict.fromkeys((
+    "volumes", "ephemeralContainers", "restartPolicy", "terminationGracePeriodSeconds",
+    "activeDeadlineSeconds", "dnsPolicy", "nodeSelector", "serviceAccountName", "serviceAccount",
+    "automountServiceAccountToken", "nodeName", "hostNetwork", "hostPID", "hostIPC", "shareProcessNamespace",
+    "securityContext", "imagePullSecrets", "hostname", "subdomain", "affinity", "schedulerName", "tolerations",
+    "hostAliases", "priorityClassName", "priority", "dnsConfig", "readinessGates", "runtimeClassName",
+    "enableServiceLinks", "preemptionPolicy", "overhead", "topologySpreadConstraints", "setHostnameAsFQDN", "os",
+    "hostUsers", "schedulingGates", "resourceClaims"))
+_POD_SPEC.update(containers=[_CONTAINER], initContainers=[_CONTAINER])
+_META = dict.fromkeys((
+    "name", "generateName", "namespace", "selfLink", "uid", "resourceVersion", "generation", "creationTimestamp",
+    "deletionTimestamp", "deletionGracePeriodSeconds", "labels", "annotations", "ownerReferences", "finalizers",
+    "managedFields"))
+_JOB_SPEC = dict.fromkeys((
+    "parallelism", "completions", "activeDeadlineSeconds", "podFailurePolicy", "successPolicy", "backoffLimit",
+    "backoffLimitPerIndex", "maxFailedIndexes", "selector", "manualSelector", "ttlSecondsAfterFinished",
+    "completionMode", "suspend", "podReplacementPolicy", "managedBy"))
+_JOB_SPEC["template"] = {"metadata": _META, "spec": _POD_SPEC}
+_JOB = {"apiVersion": None, "kind": None, "metadata": _META, "spec": _JOB_SPEC, "status": None}
+
+
+def _schema_diff(obj, schema, path):
+    if schema is None or obj is None:
+        return None
+    if isinstance(schema, list):
+        if not isinstance(obj, list):
+            return "%s: expected a list, got %s" % (path, type(obj).__name__)
+        for i, v in enumerate(obj):
+            err = _schema_diff(v, schema[0], "%s/%d" % (path, i))
+            if err:
+                return err
+        return None
+    if not isinstance(obj, dict):
+        return "%s: expected an object, got %s" % (path, type(obj).__name__)
+    for k, v in obj.items():
+        if k not in schema:
+            return "%s/%s - %s" % (path, k, json.dumps(v))
+        err = _schema_diff(v, schema[k], "%s/%s" % (path, k))
+        if err:
+            return err
+    return None
+
+
+def validate_trial_job(run_spec: dict):
+    """validateTrialJob (validator.go:376-395): only batch/v1 Jobs are checked."""
+    if run_spec.get("kind") != C.JOB_KIND_JOB or run_spec.get("apiVersion") != "batch/v1":
+        return
+    err = _schema_diff(run_spec, _JOB, "")
+    if err:
+        raise ValidationError("unable to convert spec.TrialTemplate to %s: %s" % (C.JOB_KIND_JOB, err))
+    containers = (((run_spec.get("spec") or {}).get("template") or {}).get("spec") or {}).get("containers")
+    if not containers:
+        raise ValidationError("invalid spec.trialTemplate: unable to convert spec.TrialTemplate to Job: "
+                              "spec.template.spec.containers is required")
 
 
 def _parse_spec(s: str):

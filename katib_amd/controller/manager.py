@@ -1097,10 +1097,11 @@ class Manager:
         self.tracer.end(tkey[1], phase=phase, reason=reason)
         kind = run.plan.kind if run.plan else C.JOB_KIND_JOB
         status = job_status(kind, phase, reason, message)
-        succeeded = gjson.matches(status, trial.spec.success_condition or "")
-        failed = gjson.matches(status, trial.spec.failure_condition or "")
+        st = gjson.deployed_job_status(status, trial.spec.success_condition or "",
+                                       trial.spec.failure_condition or "", trial_running=True) or {}
+        failed, succeeded = st.get("condition") == "Failed", st.get("condition") == "Succeeded"
         ns = tkey[0]
-        if failed and not succeeded:
+        if failed:
             if not TC.is_failed(trial) and not TC.is_early_stopped(trial):
                 TC.mark_failed(trial, "%s. Job reason: %s" % (C.TRIAL_FAILED_REASON, reason) if reason
                                else C.TRIAL_FAILED_REASON,

@@ -98,6 +98,11 @@ PYBIND11_MODULE(_native, m) {
     default_filter_scan(line, out);
     return out;
   });
+  m.def("re2_to_ecmascript", [](const std::string& re) {
+    bool icase = false;
+    std::string out = re2_to_ecmascript(re, &icase);
+    return py::make_tuple(out, icase);
+  });
 
   py::class_<ObservationStore, std::shared_ptr<ObservationStore>>(m, "ObservationStore")
       .def(py::init<>())

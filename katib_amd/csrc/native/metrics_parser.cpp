@@ -5,6 +5,7 @@
 #include <charconv>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <sstream>
 
 #include "json_mini.hpp"
@@ -103,6 +104,109 @@ std::string line_timestamp(const std::string& line) {
   return tok;
 }
 
+// Go's regexp (RE2 syntax) -> std::regex ECMAScript. RE2 reads a brace that does not
+// form a repetition `{n}`, `{n,}`, `{n,m}` as a literal; ECMAScript rejects it, so such
+// braces are escaped (the reference's own examples use `{metricName: ...}` filters).
+// Named groups `(?P<n>` / `(?<n>` become plain capturing groups, `\A`/`\z` anchors
+// map to ^/$, `\Q...\E` quoting is expanded and a leading `(?i)` sets icase.
+std::string re2_to_ecmascript(const std::string& re, bool* icase) {
+  std::string out;
+  size_t i = 0;
+  const size_t n = re.size();
+  if (icase) *icase = false;
+  if (re.compare(0, 4, "(?i)") == 0) {
+    if (icase) *icase = true;
+    i = 4;
+  }
+  bool in_class = false;
+  auto quantifier_len = [&](size_t at) -> size_t {  // length of a valid {..} repetition at `at`, else 0
+    size_t k = at + 1, d1 = 0, d2 = 0;
+    while (k < n && is_digit(re[k])) ++k, ++d1;
+    if (d1 == 0) return 0;
+    if (k < n && re[k] == ',') {
+      ++k;
+      while (k < n && is_digit(re[k])) ++k, ++d2;
+    }
+    if (k < n && re[k] == '}') return k - at + 1;
+    return 0;
+  };
+  while (i < n) {
+    char c = re[i];
+    if (c == '\\' && i + 1 < n) {
+      char d = re[i + 1];
+      if (!in_class && d == 'A') {
+        out += '^';
+      } else if (!in_class && d == 'z') {
+        out += '$';
+      } else if (d == 'Q') {
+        size_t e = re.find("\\E", i + 2);
+        std::string lit = re.substr(i + 2, e == std::string::npos ? std::string::npos : e - i - 2);
+        for (char l : lit) {
+          if (std::strchr("\\^$.|?*+()[]{}/-", l)) out += '\\';
+          out += l;
+        }
+        i = e == std::string::npos ? n : e + 2;
+        continue;
+      } else {
+        out += c;
+        out += d;
+      }
+      i += 2;
+      continue;
+    }
+    if (in_class) {
+      if (c == ']') in_class = false;
+      out += c;
+      ++i;
+      continue;
+    }
+    if (c == '[') {
+      in_class = true;
+      out += c;
+      ++i;
+      if (i < n && re[i] == '^') out += re[i++];
+      if (i < n && re[i] == ']') out += "\\]", ++i;  // leading ']' is literal in RE2
+      continue;
+    }
+    if (c == '(' && re.compare(i, 4, "(?P<") == 0) {
+      size_t e = re.find('>', i);
+      if (e != std::string::npos) {
+        out += '(';
+        i = e + 1;
+        continue;
+      }
+    }
+    if (c == '(' && re.compare(i, 3, "(?<") == 0 && i + 3 < n && re[i + 3] != '=' && re[i + 3] != '!') {
+      size_t e = re.find('>', i);
+      if (e != std::string::npos) {
+        out += '(';
+        i = e + 1;
+        continue;
+      }
+    }
+    if (c == '{') {
+      const size_t q = quantifier_len(i);
+      const bool has_atom = !out.empty() && out.back() != '(' && out.back() != '|';
+      if (q && has_atom) {
+        out.append(re, i, q);
+        i += q;
+        continue;
+      }
+      out += "\\{";
+      ++i;
+      continue;
+    }
+    if (c == '}') {
+      out += "\\}";
+      ++i;
+      continue;
+    }
+    out += c;
+    ++i;
+  }
+  return out;
+}
+
 MetricsParser::MetricsParser(std::vector<std::string> names, std::vector<std::string> filters, MetricsFormat fmt)
     : names_(std::move(names)), filters_(std::move(filters)), fmt_(fmt) {
   if (filters_.empty()) filters_.push_back(kDefaultFilter);
@@ -111,7 +215,11 @@ MetricsParser::MetricsParser(std::vector<std::string> names, std::vector<std::st
       regexes_.push_back(nullptr);
     } else {
       try {
-        regexes_.push_back(std::make_shared<std::regex>(f, std::regex::ECMAScript));
+        bool icase = false;
+        const std::string ecma = re2_to_ecmascript(f, &icase);
+        auto flags = std::regex::ECMAScript;
+        if (icase) flags |= std::regex::icase;
+        regexes_.push_back(std::make_shared<std::regex>(ecma, flags));
       } catch (const std::regex_error&) {
         // regexp.Compile errors are ignored by GetFilterRegexpList (nil regexp);
         // validation rejects such filters before we get here.

@@ -55,6 +55,7 @@ void default_filter_scan(const std::string& line, std::vector<std::pair<std::str
 std::string line_timestamp(const std::string& line);
 bool go_parse_float(const std::string& s, double& v);
 std::string trim_space(const std::string& s);
+std::string re2_to_ecmascript(const std::string& re, bool* icase = nullptr);
 std::string go_format_float_f(double v);
 
 }  // namespace katib

@@ -128,6 +128,44 @@ def set_trial_status(address: str, trial: str) -> None:
         EarlyStoppingStub(ch).SetTrialStatus(api.SetTrialStatusRequest(trial_name=trial), timeout=60)
 
 
+class CollectError(Exception):
+    """errOpenFile / errFileFormat / errParseJson of CollectObservationLog."""
+
+
+def parse_observation_log(content: str, metrics: List[str], filters: List[str], file_format: str,
+                          parser=None) -> List[Tuple[str, str, str]]:
+    """Parse a finished metrics file body into (timestamp, name, value) rows; when the
+    objective (first metric) never appears the log is one ``unavailable`` row
+    (file-metricscollector.go CollectObservationLog)."""
+    from .. import native
+
+    if file_format not in ("TEXT", "JSON"):
+        raise CollectError("format must be set to TEXT or JSON")
+    if parser is None:
+        parser = native.load().MetricsParser(list(metrics), list(filters or []), 1 if file_format == "JSON" else 0)
+    try:
+        logs = parser.parse_content(content)
+    except ValueError as e:
+        raise CollectError("failed to parse JSON line: %s" % e)
+    if metrics and not any(n == metrics[0] for _, n, _ in logs):
+        from ..api.models import ZERO_TIME
+
+        logs = [(ZERO_TIME, metrics[0], "unavailable")]
+    return logs
+
+
+def collect_observation_log(path: str, metrics: List[str], filters: List[str],
+                            file_format: str) -> List[Tuple[str, str, str]]:
+    if file_format not in ("TEXT", "JSON"):
+        raise CollectError("format must be set to TEXT or JSON")
+    try:
+        with open(path, errors="replace") as f:
+            content = f.read()
+    except OSError as e:
+        raise CollectError("failed to open file: %s" % e)
+    return parse_observation_log(content, metrics, filters, file_format)
+
+
 def collect(args, reporter=report, status_setter=set_trial_status) -> int:
     from .. import native
 
@@ -181,11 +219,7 @@ def collect(args, reporter=report, status_setter=set_trial_status) -> int:
         time.sleep(args.poll)
     code = child.wait() if child is not None else 0
     content = open(args.path, errors="replace").read() if os.path.exists(args.path) else ""
-    logs = parser.parse_content(content)
-    if not any(n == names[0] for _, n, _ in logs):
-        from ..api.models import ZERO_TIME
-
-        logs = [(ZERO_TIME, names[0], "unavailable")]
+    logs = parse_observation_log(content, names, filters, args.format, parser)
     reporter(args.db_manager, args.trial_name, logs)
     if early and args.earlystop:
         status_setter(args.earlystop, args.trial_name)

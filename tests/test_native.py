@@ -160,3 +160,24 @@ def test_template_render():
     assert N.render_template("x=${trialParameters.lr} y=${trialParameters.lr}", {"lr": "0.1"}) == "x=0.1 y=0.1"
     assert N.unresolved_placeholders("${trialParameters.a} and ${trialParameters.b}") == [
         "${trialParameters.a}", "${trialParameters.b}"]
+
+
+@pytest.mark.parametrize("re2,ecma,icase", [
+    (r"{metricName: ([\w|-]+), metricValue: ((-?\d+)(\.\d+)?)}",
+     r"\{metricName: ([\w|-]+), metricValue: ((-?\d+)(\.\d+)?)\}", False),
+    (r"(?P<name>\w+)=(\d+)", r"(\w+)=(\d+)", False),
+    (r"a{2,3}b{4}c{5,}", r"a{2,3}b{4}c{5,}", False),
+    (r"x{a}", r"x\{a\}", False),
+    (r"(?i)loss=(\d)", r"loss=(\d)", True),
+    (r"[]a](x)", r"[\]a](x)", False),
+    (r"\Qa.b\E(\d)", r"a\.b(\d)", False),
+    (r"\A(\w+)=(\d)\z", r"^(\w+)=(\d)$", False),
+])
+def test_re2_filter_translation(re2, ecma, icase):
+    """Go RE2 filter syntax the reference accepts (literal braces, named groups, \\Q..\\E)."""
+    assert N.re2_to_ecmascript(re2) == (ecma, icase)
+
+
+def test_brace_filter_parses():
+    p = N.MetricsParser(["accuracy"], [r"{metricName: ([\w|-]+), metricValue: ((-?\d+)(\.\d+)?)}"], 0)
+    assert p.parse_line("{metricName: accuracy, metricValue: 0.5}") == [("0001-01-01T00:00:00Z", "accuracy", "0.5")]
