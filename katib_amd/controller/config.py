@@ -11,6 +11,7 @@ worker pool, state directory.
 
 from __future__ import annotations
 
+import copy
 import os
 import re
 from dataclasses import dataclass, field
@@ -63,6 +64,7 @@ class KatibConfig:
     healthz_addr: str = ":18080"
     experiment_suggestion_name: str = "default"
     amd: AmdConfig = field(default_factory=AmdConfig)
+    raw: Dict = field(default_factory=dict)  # the defaulted katib-config.yaml document
 
     @staticmethod
     def _service_from_image(image: str) -> Optional[str]:
@@ -76,8 +78,12 @@ class KatibConfig:
         cfg = cls()
         if not d:
             return cfg
+        from ..api import katibconfig as KC
+
+        cfg.raw = KC.set_defaults(copy.deepcopy(d))  # reference defaulting (defaults.go)
         init = (d.get("init") or {}).get("controller") or {}
         if init.get("trialResources"):
+            KC.trial_resources_to_gvks(init["trialResources"])
             cfg.trial_resources = list(init["trialResources"])
         cfg.metrics_addr = init.get("metricsAddr", cfg.metrics_addr)
         cfg.healthz_addr = init.get("healthzAddr", cfg.healthz_addr)
