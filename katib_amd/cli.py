@@ -301,6 +301,30 @@ def cmd_metrics_collector(a, rest):
     return collect(parse_args(rest))
 
 
+def cmd_inject(a):
+    """Print the pod with the metrics collector injected (the /mutate-pod webhook's
+    rewrite) for running a trial's pod on a cluster."""
+    import yaml
+
+    from .api import katibconfig as KC
+    from .controller.inject import mutate_pod
+
+    with open(a.trial) as f:
+        trial = yaml.safe_load(f)
+    with open(a.pod) as f:
+        pod = yaml.safe_load(f)
+    kind = (((trial.get("spec") or {}).get("metricsCollector") or {}).get("collector") or {}).get("kind", "StdOut")
+    cfg = {}
+    if a.config:
+        entries = (KC.load_file(a.config).get("runtime") or {}).get("metricsCollectors") or []
+        cfg = next((e for e in entries if e.get("kind") == kind), {})
+    md = trial.get("metadata") or {}
+    exp = (md.get("labels") or {}).get("katib.kubeflow.org/experiment", "")
+    sugg = {(md.get("namespace"), exp): a.early_stopping_algorithm} if a.early_stopping_algorithm else None
+    print(yaml.safe_dump(mutate_pod(pod, trial, cfg, a.image, sugg, a.db_manager or None), sort_keys=False), end="")
+    return 0
+
+
 def build_parser():
     p = argparse.ArgumentParser(prog="katib-amd", description="Katib-compatible AutoML engine for MI355X nodes")
     sub = p.add_subparsers(dest="cmd", required=True)
@@ -363,6 +387,15 @@ def build_parser():
     d.set_defaults(fn=cmd_db_manager)
 
     sub.add_parser("metrics-collector", help="file/StdOut metrics collector (reference flags)", add_help=False)
+
+    inj = sub.add_parser("inject", help="print a trial pod with the metrics-collector sidecar injected")
+    inj.add_argument("--trial", required=True, help="Trial manifest (YAML)")
+    inj.add_argument("--pod", required=True, help="Pod manifest (YAML)")
+    inj.add_argument("--config", default="", help="katib-config.yaml (metricsCollectors entry for the kind)")
+    inj.add_argument("--image", default="", help="collector image (overrides the config)")
+    inj.add_argument("--early-stopping-algorithm", default="", help="algorithm serving -s-earlystop")
+    inj.add_argument("--db-manager", default="", help="DBManager address (default from KATIB_DB_MANAGER_*)")
+    inj.set_defaults(fn=cmd_inject)
     return p
 
 
