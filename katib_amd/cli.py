@@ -279,6 +279,18 @@ def cmd_db_manager(a):
     from . import native
     from .rpc.server import make_server
 
+    db = (a.db or os.environ.get("DB_NAME", "")).lower()
+    if db not in ("", "native"):
+        from .db.sql import new_observation_db
+
+        store = new_observation_db(db, connect_timeout=a.connect_timeout)
+        srv = make_server(a.address, store=store)
+        srv.start()
+        print("db-manager listening on %s (%s backend)" % (a.address, db), flush=True)
+        _wait_signal()
+        srv.stop(0)
+        store.close()
+        return 0
     N = native.load()
     store = N.ObservationStore()
     if a.journal:
@@ -384,6 +396,8 @@ def build_parser():
     d = sub.add_parser("db-manager", help="DBManager gRPC server on the native observation store")
     d.add_argument("--address", default="0.0.0.0:6789")
     d.add_argument("--journal", default="", help="append-only journal file for persistence")
+    d.add_argument("--db", default="", help="native (default) | sqlite | mysql | postgres (else $DB_NAME)")
+    d.add_argument("--connect-timeout", type=float, default=60.0, help="seconds to wait for the database")
     d.set_defaults(fn=cmd_db_manager)
 
     sub.add_parser("metrics-collector", help="file/StdOut metrics collector (reference flags)", add_help=False)

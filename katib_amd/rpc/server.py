@@ -1,6 +1,7 @@
 """gRPC servers - wire-compatible with the reference services.
 
-* ``DBManager`` on the native observation store (``cmd/db-manager/v1beta1/main.go:37-121``),
+* ``DBManager`` on the native observation store or a SQL backend (``katib_amd.db.sql``)
+  (``cmd/db-manager/v1beta1/main.go:37-121``),
 * ``Suggestion`` exposing any in-process algorithm service (so external Katib
   controllers or tools can use our algorithms, and ``tools`` written against the
   reference protocol keep working; ``cmd/suggestion/*/main.py``),
@@ -96,15 +97,28 @@ class EarlyStoppingServicer:
 
 
 class HealthServicer:
-    def __init__(self, serving=("", "manager.v1beta1.Suggestion", "manager.v1beta1.DBManager",
-                                "manager.v1beta1.EarlyStopping")):
+    """Health.Check; with a database-backed store the DB is probed with ``SELECT 1``
+    (db-manager main.go:70-89) and a failing probe reports NOT_SERVING."""
+
+    def __init__(self, serving=("", "grpc.health.v1.Health", "manager.v1beta1.Suggestion",
+                                "manager.v1beta1.DBManager", "manager.v1beta1.EarlyStopping"), store=None):
         self.serving = set(serving)
+        self.store = store
 
     def Check(self, request, context):
-        st = api.HealthCheckResponse.SERVING if request.service in self.serving else \
-            api.HealthCheckResponse.SERVICE_UNKNOWN if hasattr(api.HealthCheckResponse, "SERVICE_UNKNOWN") \
-            else api.HealthCheckResponse.UNKNOWN
-        return api.HealthCheckResponse(status=st)
+        if request.service not in self.serving:
+            st = api.HealthCheckResponse.SERVICE_UNKNOWN if hasattr(api.HealthCheckResponse, "SERVICE_UNKNOWN") \
+                else api.HealthCheckResponse.UNKNOWN
+            return api.HealthCheckResponse(status=st)
+        probe = getattr(self.store, "select_one", None)
+        if probe is not None:
+            try:
+                probe()
+            except Exception as e:
+                if context is not None:
+                    context.set_details("Failed to execute `SELECT 1` probe: %s" % e)
+                return api.HealthCheckResponse(status=api.HealthCheckResponse.NOT_SERVING)
+        return api.HealthCheckResponse(status=api.HealthCheckResponse.SERVING)
 
 
 def _handler(service_name, servicer):
@@ -128,7 +142,7 @@ def make_server(address: str = "0.0.0.0:6789", store=None, suggestion_service=No
         handlers.append(_handler("Suggestion", SuggestionServicer(suggestion_service)))
     if early_stopping_service is not None:
         handlers.append(_handler("EarlyStopping", EarlyStoppingServicer(early_stopping_service)))
-    hs = HealthServicer()
+    hs = HealthServicer(store=store)
     handlers.append(grpc.method_handlers_generic_handler("grpc.health.v1.Health", {
         "Check": _unary(hs.Check, api.HealthCheckRequest, api.HealthCheckResponse)}))
     server.add_generic_rpc_handlers(handlers)
