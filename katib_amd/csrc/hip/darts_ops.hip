@@ -1072,6 +1072,182 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdBatch bt) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// dw_bwd_plane: dw_bwd for narrow layers (C <= 16), the backward twin of dwpw_plane. One
+// workgroup per (image, band of input rows): the dd rows the band's input pixels reach (plus a
+// zero border of PO = ceil(pad/S), so every tap lands inside the staged grid) and act(in) of the
+// band are staged with one coalesced burst (and, when accumulating, the current input gradient),
+// then
+//   input grads : thread per own input pixel, all channels: ga = sum_taps w * dd (transposed
+//                 depthwise gather from LDS), masked by act'(in); PREBN keeps the BN-backward
+//                 sums per thread and reduces once per block;
+//   weight grads: thread per (channel, tap[, pixel part]) summing act(in) * dd over the band.
+// Every input pixel belongs to exactly one band, so both sums are complete without overlap.
+// Replaces the 64-pixel tiles whose halo rows were re-staged per tile behind two barriers.
+// ------------------------------------------------------------------------------------------------
+template <int K, int DIL, int S, bool PREBN, int C>
+__global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb, int dbg) {
+  const DwBwdArgs& a = bt.e[blockIdx.y];
+  constexpr int KK = K * K, PAD = (K - 1) / 2 * DIL, PO = (PAD + S - 1) / S, SH = S == 2 ? 1 : 0;
+  const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int n = blockIdx.x / nb, band = blockIdx.x - n * nb;
+  const int BRi = H / nb, iy0 = band * BRi, nrow = BRi;
+  const int oyA = (iy0 - PAD) >> SH;                 // floor division (S in {1, 2})
+  const int oyB = (iy0 + nrow - 1 + PAD) >> SH;
+  const int ODR = oyB - oyA + 1, ODW = Wo + 2 * PO, NP = nrow * W;
+  const bool accum = !PREBN && !a.overwrite;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sDD = smem;                    // [C][ODR][ODW]
+  float* sIn = sDD + C * ODR * ODW;     // [C][nrow][W] act(in)
+  float* sOld = sIn + C * NP;           // [C][nrow][W] current gradient (accumulate mode)
+  __shared__ float sMean[C], sInv[C], sRed[2 * C], sGW[C * KK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < C) {
+    if (PREBN) bn_coeffs(a.inbn, tid, sMean[tid], sInv[tid]);
+    sRed[tid] = 0.f;
+    sRed[C + tid] = 0.f;
+  }
+  for (int i = tid; i < C * KK; i += 256) sGW[i] = 0.f;
+  __syncthreads();
+  // staging with 16-byte loads (the band's rows are contiguous per channel; W, Wo % 4 == 0):
+  // many wide loads in flight per wave, which the one-row-per-wave scalar loop lacked
+  const float* ddn = a.dd + (size_t)n * C * Ho * Wo;
+  const float* xn = a.x + (size_t)n * C * H * W;
+  const int va = max(oyA, 0), vb = min(oyB, Ho - 1), vrows = vb - va + 1;  // staged dd rows inside [0, Ho)
+  {
+    const int q4 = vrows * Wo / 4;  // float4s per channel
+#pragma unroll 4
+    for (int i = tid; i < C * q4; i += 256) {
+      const int c = i / q4, o = (i - c * q4) * 4, r = o / Wo, ox = o - r * Wo;
+      const float4 v = *reinterpret_cast<const float4*>(ddn + ((size_t)c * Ho + va) * Wo + o);
+      float* d = sDD + (c * ODR + va - oyA + r) * ODW + PO + ox;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+    // zero border: rows outside [0, Ho) and the PO columns on each side
+    for (int i = tid; i < C * ODR; i += 256) {
+      const int c = i / ODR, oy = oyA + i - c * ODR;
+      float* d = sDD + i * ODW;
+      if (oy < 0 || oy >= Ho) {
+        for (int q = 0; q < ODW; ++q) d[q] = 0.f;
+      } else {
+        for (int q = 0; q < PO; ++q) d[q] = d[PO + Wo + q] = 0.f;
+      }
+    }
+  }
+  {
+    const int q4 = NP / 4;
+#pragma unroll 4
+    for (int i = tid; i < C * q4; i += 256) {
+      const int c = i / q4, o = (i - c * q4) * 4;
+      float4 v = *reinterpret_cast<const float4*>(xn + ((size_t)c * H + iy0) * W + o);
+      if (PREBN) {
+        const float m = sMean[c], iv = sInv[c];
+        v.x = (v.x - m) * iv;
+        v.y = (v.y - m) * iv;
+        v.z = (v.z - m) * iv;
+        v.w = (v.w - m) * iv;
+      }
+      v.x = fmaxf(v.x, 0.f);
+      v.y = fmaxf(v.y, 0.f);
+      v.z = fmaxf(v.z, 0.f);
+      v.w = fmaxf(v.w, 0.f);
+      *reinterpret_cast<float4*>(sIn + c * NP + o) = v;
+    }
+    if (accum) {
+      const float* gsrc = a.gout + (size_t)n * C * H * W;
+#pragma unroll 4
+      for (int i = tid; i < C * q4; i += 256) {
+        const int c = i / q4, o = (i - c * q4) * 4;
+        *reinterpret_cast<float4*>(sOld + c * NP + o) =
+            *reinterpret_cast<const float4*>(gsrc + ((size_t)c * H + iy0) * W + o);
+      }
+    }
+  }
+  __syncthreads();
+  // input gradients of the band's own pixels
+  float st1[C], st2[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) st1[c] = st2[c] = 0.f;
+  float* gn = a.gout + (size_t)n * C * H * W;
+  for (int p = tid; p < ((dbg & 1) ? 0 : NP); p += 256) {
+    const int r = p / W, ix = p - r * W, iy = iy0 + r;
+    int srow[K], scol[K];
+    float mrow[K], mcol[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int t = iy + PAD - k * DIL, u = ix + PAD - k * DIL;
+      srow[k] = ((t >> SH) - oyA) * ODW;
+      scol[k] = (u >> SH) + PO;
+      mrow[k] = (S == 1 || (t & 1) == 0) ? 1.f : 0.f;
+      mcol[k] = (S == 1 || (u & 1) == 0) ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float* wk = a.dw + c * KK;  // uniform -> scalar loads
+      const float* dd = sDD + c * ODR * ODW;
+      float ga = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky) {
+        float rowacc = 0.f;
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const float v = wk[ky * K + kx] * dd[srow[ky] + scol[kx]];
+          rowacc += S == 1 ? v : mcol[kx] * v;
+        }
+        ga += S == 1 ? rowacc : mrow[ky] * rowacc;
+      }
+      const int li = (c * nrow + r) * W + ix;
+      const float act = sIn[li];
+      const size_t gi = ((size_t)c * H + iy) * W + ix;
+      const float g = act > 0.f ? ga : 0.f;
+      if (PREBN) {
+        gn[gi] = g;
+        st1[c] += g;
+        st2[c] += g * act;  // g * y == g * relu(y)
+      } else {
+        gn[gi] = accum ? sOld[li] + g : g;
+      }
+    }
+  }
+  if (PREBN && a.red) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float v1 = wave_sum(st1[c]), v2 = wave_sum(st2[c]);
+      if (lane == 0) {
+        atomicAdd(sRed + c, v1);
+        atomicAdd(sRed + C + c, v2);
+      }
+    }
+  }
+  // depthwise weight gradients over the band: thread per (channel, tap, pixel part)
+  if (a.gW && !(dbg & 2)) {
+    constexpr int JOBS = C * KK, T = JOBS >= 256 ? 1 : 256 / JOBS;
+    for (int j = tid; j < JOBS * T; j += 256) {
+      const int job = j / T, part = j - job * T;
+      const int c = job / KK, tap = job - c * KK, ky = tap / K, kx = tap - ky * K;
+      const float* dd = sDD + c * ODR * ODW;
+      const float* in = sIn + c * NP;
+      float acc = 0.f;
+      for (int r = 0; r < nrow; ++r) {
+        const int t = iy0 + r + PAD - ky * DIL;
+        if (S == 2 && (t & 1)) continue;
+        const float* ddr = dd + ((t >> SH) - oyA) * ODW + PO;
+        const float* inr = in + r * W;
+        for (int ix = part * S + ((S == 2) ? ((PAD - kx * DIL) & 1) : 0); ix < W; ix += T * S)
+          acc += inr[ix] * ddr[(ix + PAD - kx * DIL) >> SH];
+      }
+      atomicAdd(sGW + job, acc);
+    }
+  }
+  __syncthreads();
+  if (PREBN && a.red && tid < 2 * C) atomicAdd(a.red + rep_slot() * 2 * C + tid, (double)sRed[tid]);
+  if (a.gW)
+    for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + (size_t)rep_slot() * a.gstride + i, sGW[i]);
+}
+
+// ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
 static int per_edge_blocks(int tiles, int n) { return std::max(1, std::min(tiles, max_blocks() / std::max(n, 1))); }
@@ -1113,9 +1289,54 @@ void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, h
 #undef DISPATCH
 }
 
+// LDS floats of one dw_bwd_plane band (nb bands per image)
+static size_t dw_plane_floats(const DwBwdArgs& a, int K, int DIL, int S, int nb, bool accum) {
+  const int PAD = (K - 1) / 2 * DIL, PO = (PAD + S - 1) / S, sh = S == 2 ? 1 : 0, BRi = a.H / nb;
+  auto fdiv = [sh](int v) { return v >= 0 ? v >> sh : -((-v + (1 << sh) - 1) >> sh); };
+  const int ODR = fdiv(BRi - 1 + PAD) - fdiv(-PAD) + 2;  // +1: odd bands start at odd rows
+  return (size_t)a.C * ODR * (a.Wo + 2 * PO) + (size_t)a.C * BRi * a.W * (accum ? 2 : 1);
+}
+
+template <int K, int DIL, int S, int C>
+static void launch_dw_bwd_plane_t(const DwBwdBatch& b, bool prebn, hipStream_t st) {
+  const DwBwdArgs& a = b.e[0];
+  bool accum = false;
+  for (int i = 0; i < b.n; ++i) accum |= !prebn && !b.e[i].overwrite;
+  // bands: as few as possible (less halo) while the launch still has ~4 workgroups per CU and a
+  // band stays within 40 KB of LDS
+  int nb = 1;
+  while (nb < 8 && a.H % (2 * nb) == 0 &&
+         (dw_plane_floats(a, K, DIL, S, nb, accum) * 4 > 40 * 1024 || a.N * nb * b.n < 1024))
+    nb *= 2;
+  const size_t lds = sizeof(float) * dw_plane_floats(a, K, DIL, S, nb, accum);
+  dim3 grid(a.N * nb, b.n);
+  static const int dbg = getenv("KATIB_HIP_DWB_DBG") ? atoi(getenv("KATIB_HIP_DWB_DBG")) : 0;  // timing probes
+  if (prebn) hipLaunchKernelGGL((dw_bwd_plane_kernel<K, DIL, S, true, C>), grid, dim3(256), lds, st, b, nb, dbg);
+  else hipLaunchKernelGGL((dw_bwd_plane_kernel<K, DIL, S, false, C>), grid, dim3(256), lds, st, b, nb, dbg);
+}
+
+static bool aligned16(const DwBwdBatch& b) {
+  for (int i = 0; i < b.n; ++i)
+    if (((uintptr_t)b.e[i].x | (uintptr_t)b.e[i].dd | (uintptr_t)b.e[i].gout) & 15) return false;
+  return true;
+}
+
+// plane path: narrow layers whose spatial sizes divide exactly by the stride
+static bool dw_plane_ok(const DwBwdBatch& b, int K, int DIL, int S) {
+  if (getenv("KATIB_HIP_DW_BWD_TILED")) return false;
+  const DwBwdArgs& a = b.e[0];
+  return (a.C == 4 || a.C == 8 || a.C == 16) && a.H == a.Ho * S && a.W == a.Wo * S &&
+         a.pad == (K - 1) / 2 * DIL && a.Wo % 4 == 0 && aligned16(b);
+}
+
 template <int K, int DIL, int S>
 static void launch_dw_bwd_t(const DwBwdBatch& b, bool prebn, hipStream_t st) {
   const DwBwdArgs& a = b.e[0];
+  if (dw_plane_ok(b, K, DIL, S)) {
+    if (a.C == 4) return launch_dw_bwd_plane_t<K, DIL, S, 4>(b, prebn, st);
+    if (a.C == 8) return launch_dw_bwd_plane_t<K, DIL, S, 8>(b, prebn, st);
+    return launch_dw_bwd_plane_t<K, DIL, S, 16>(b, prebn, st);
+  }
   const int TR = 64 / a.Wo;
   const int r = (K - 1) / 2 * DIL, h = (r + S - 1) / S, OR = TR + 2 * h;
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
