@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
 // for a dilated 5x5 on 2-row tiles, a barrier-separated load/compute chain per tile) this
 // reads each input pixel once and has a single barrier before the compute.
 // ------------------------------------------------------------------------------------------------
-template <int K, int DIL, int S, bool PREBN, int C>
+template <int K, int DIL, int S, bool PREBN, int C, bool VEC>
 __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
   const DwPwFwdArgs& a = bt.e[blockIdx.y];
   constexpr int KK = K * K;
@@ -273,22 +273,54 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
     sStat[C + tid] = 0.f;
   }
   __syncthreads();
-  // staging: one wave per (channel, row); the row index is wave-uniform, lanes sweep columns
   const float* xin = a.x + (size_t)n * C * H * W;
+  if (VEC) {
+    // 16-byte loads over the band's contiguous in-range rows, scattered into the padded plane;
+    // the zero border (rows outside [0, H), pad columns) is written separately
+    const int va = max(iyb, 0), vb = min(iyb + HP, H), q4 = (vb - va) * W / 4;
 #pragma unroll 4
-  for (int row = wave; row < C * HP; row += 4) {
-    const int c = row / HP, r = row - c * HP, iy = iyb + r;
-    const bool rok = iy >= 0 && iy < H;
-    const float* src = xin + ((size_t)c * H + (rok ? iy : 0)) * W;
-    for (int q = lane; q < WP; q += 64) {
-      const int ix = q - pad;
-      float v = 0.f;
-      if (rok && ix >= 0 && ix < W) {
-        v = src[ix];
-        if (PREBN) v = (v - sMean[c]) * sInv[c];
-        v = fmaxf(v, 0.f);
+    for (int i = tid; i < C * q4; i += 256) {
+      const int c = i / q4, o = (i - c * q4) * 4, r = o / W, ix = o - r * W;
+      float4 v = *reinterpret_cast<const float4*>(xin + ((size_t)c * H + va) * W + o);
+      if (PREBN) {
+        const float m = sMean[c], iv = sInv[c];
+        v.x = (v.x - m) * iv;
+        v.y = (v.y - m) * iv;
+        v.z = (v.z - m) * iv;
+        v.w = (v.w - m) * iv;
       }
-      sIn[row * WP + q] = v;
+      float* d = sIn + (c * HP + va - iyb + r) * WP + pad + ix;
+      d[0] = fmaxf(v.x, 0.f);
+      d[1] = fmaxf(v.y, 0.f);
+      d[2] = fmaxf(v.z, 0.f);
+      d[3] = fmaxf(v.w, 0.f);
+    }
+    for (int i = tid; i < C * HP; i += 256) {
+      const int iy = iyb + i % HP;
+      float* d = sIn + i * WP;
+      if (iy < 0 || iy >= H) {
+        for (int q = 0; q < WP; ++q) d[q] = 0.f;
+      } else {
+        for (int q = 0; q < pad; ++q) d[q] = d[pad + W + q] = 0.f;
+      }
+    }
+  } else {
+    // one wave per (channel, row); the row index is wave-uniform, lanes sweep columns
+#pragma unroll 4
+    for (int row = wave; row < C * HP; row += 4) {
+      const int c = row / HP, r = row - c * HP, iy = iyb + r;
+      const bool rok = iy >= 0 && iy < H;
+      const float* src = xin + ((size_t)c * H + (rok ? iy : 0)) * W;
+      for (int q = lane; q < WP; q += 64) {
+        const int ix = q - pad;
+        float v = 0.f;
+        if (rok && ix >= 0 && ix < W) {
+          v = src[ix];
+          if (PREBN) v = (v - sMean[c]) * sInv[c];
+          v = fmaxf(v, 0.f);
+        }
+        sIn[row * WP + q] = v;
+      }
     }
   }
   __syncthreads();
@@ -1258,8 +1290,16 @@ static void launch_dwpw_plane_t(const DwPwFwdBatch& b, bool prebn, hipStream_t s
   const int nb = a.chunk, BR = (a.Ho + nb - 1) / nb;
   const size_t lds = sizeof(float) * C * ((BR - 1) * S + (K - 1) * DIL + 1) * (a.W + 2 * a.pad);
   dim3 grid(a.N * nb, b.n);
-  if (prebn) hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, true, C>), grid, dim3(256), lds, st, b);
-  else hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, false, C>), grid, dim3(256), lds, st, b);
+  // 16-byte staging when every row is whole float4s and every input is 16-byte aligned
+  bool vec = a.W % 4 == 0;
+  for (int i = 0; i < b.n; ++i) vec &= ((uintptr_t)b.e[i].x & 15) == 0;
+  if (vec) {
+    if (prebn) hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, true, C, true>), grid, dim3(256), lds, st, b);
+    else hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, false, C, true>), grid, dim3(256), lds, st, b);
+  } else {
+    if (prebn) hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, true, C, false>), grid, dim3(256), lds, st, b);
+    else hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, false, C, false>), grid, dim3(256), lds, st, b);
+  }
 }
 
 // row-band kernel for C = 4 / 8 (the staged band fits 64 KB of LDS by construction)
