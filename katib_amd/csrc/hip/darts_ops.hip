@@ -525,20 +525,35 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
     // the host picks this path only when every operand pointer is 16-byte aligned
     typedef float f4 __attribute__((ext_vector_type(4)));
     const size_t total4 = total / 4;
+    constexpr int EM = CombineFwdBatch::kCap;
     for (size_t i4 = (size_t)blockIdx.x * 256 + threadIdx.x; i4 < total4; i4 += (size_t)gridDim.x * 256) {
       const int c = (int)((i4 * 4 / HW) % C);
+      // issue every operand load first (up to EM * (kMaxOps + 1) in flight), then accumulate in
+      // the scalar path's order: a runtime-bounded load-then-add loop waited on each load in turn
+      f4 zv[EM][kMaxOps], xv[EM];
+#pragma unroll
+      for (int e = 0; e < EM; ++e) {
+        const CombineFwdArgs& a = bt.e[e < ne ? e : 0];
+#pragma unroll
+        for (int k = 0; k < kMaxOps; ++k)
+          if (e < ne && k < a.nops) zv[e][k] = reinterpret_cast<const f4*>(a.z[k])[i4];
+        if (e < ne && a.xid) xv[e] = reinterpret_cast<const f4*>(a.xid)[i4];
+      }
       f4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int e = 0; e < ne; ++e) {
+#pragma unroll
+      for (int e = 0; e < EM; ++e) {
+        if (e >= ne) break;
         const CombineFwdArgs& a = bt.e[e];
         const float* sw = sW + e * (kMaxOps + 1);
-        for (int k = 0; k < a.nops; ++k) {
+#pragma unroll
+        for (int k = 0; k < kMaxOps; ++k) {
+          if (k >= a.nops) break;
           const int j = (e * kMaxOps + k) * C + c;
           // same rounding as the scalar path: w * ((z - mean) * inv)
           const float m = sMean[j], inv = sInv[j];
-          const f4 z = reinterpret_cast<const f4*>(a.z[k])[i4];
-          acc += sw[k] * ((z - m) * inv);
+          acc += sw[k] * ((zv[e][k] - m) * inv);
         }
-        if (a.xid) acc += sw[kMaxOps] * reinterpret_cast<const f4*>(a.xid)[i4];
+        if (a.xid) acc += sw[kMaxOps] * xv[e];
       }
       if (a0.gamma) acc = acc * a0.gamma[c] + a0.beta[c];
       f4* o = reinterpret_cast<f4*>(a0.out) + i4;
@@ -567,6 +582,7 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
 // combine_bwd_reduce: S1[c] = sum dout, S2[k][c] = sum dout * zhat_k, Sid = sum dout * x
 // One block per (n, c) plane.
 // ------------------------------------------------------------------------------------------------
+template <bool V4>
 __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdBatch bt) {
   const CombineBwdArgs& a = bt.e[blockIdx.y];
   const int C = a.C, HW = a.HW;
@@ -579,15 +595,44 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdBatch
   float s2[kMaxOps];
 #pragma unroll
   for (int k = 0; k < kMaxOps; ++k) s2[k] = 0.f;
-  for (int n = g0; n < a.N; n += G) {
-    const size_t base = ((size_t)n * C + c) * HW;
-    for (int i = threadIdx.x; i < HW; i += 256) {
-      float g = a.dout[base + i];
-      s1 += g;
+  if (V4) {
+    // the block's (image, float4) pairs flattened so every thread has work at small HW;
+    // 16-byte loads, all operands of an element issued before use
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int q4 = HW / 4, cnt = (a.N - g0 + G - 1) / G;
+    for (int t = threadIdx.x; t < cnt * q4; t += 256) {
+      const int n = g0 + (t / q4) * G, i4 = t - (t / q4) * q4;
+      const size_t b4 = ((size_t)n * C + c) * q4 + i4;
+      const f4 g = reinterpret_cast<const f4*>(a.dout)[b4];
+      f4 zv[kMaxOps];
 #pragma unroll
       for (int k = 0; k < kMaxOps; ++k)
-        if (k < a.nops) s2[k] += g * (a.z[k][base + i] - sMean[k]) * sInv[k];
-      if (a.xid) sid += g * a.xid[base + i];
+        if (k < a.nops) zv[k] = reinterpret_cast<const f4*>(a.z[k])[b4];
+      f4 xv = {0.f, 0.f, 0.f, 0.f};
+      if (a.xid) xv = reinterpret_cast<const f4*>(a.xid)[b4];
+      s1 += (g.x + g.y) + (g.z + g.w);
+#pragma unroll
+      for (int k = 0; k < kMaxOps; ++k)
+        if (k < a.nops) {
+          const f4 t2 = g * (zv[k] - sMean[k]) * sInv[k];
+          s2[k] += (t2.x + t2.y) + (t2.z + t2.w);
+        }
+      if (a.xid) {
+        const f4 t3 = g * xv;
+        sid += (t3.x + t3.y) + (t3.z + t3.w);
+      }
+    }
+  } else {
+    for (int n = g0; n < a.N; n += G) {
+      const size_t base = ((size_t)n * C + c) * HW;
+      for (int i = threadIdx.x; i < HW; i += 256) {
+        float g = a.dout[base + i];
+        s1 += g;
+#pragma unroll
+        for (int k = 0; k < kMaxOps; ++k)
+          if (k < a.nops) s2[k] += g * (a.z[k][base + i] - sMean[k]) * sInv[k];
+        if (a.xid) sid += g * a.xid[base + i];
+      }
     }
   }
   int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -806,7 +851,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
 // no barrier until the block's single reduction of its accumulators (wave shuffles, then one
 // LDS add per wave and one global atomic vector per block into the block's replica).
 // ------------------------------------------------------------------------------------------------
-template <int CI, int CO>
+template <int CI, int CO, bool V4>
 __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
   const PwBwdArgs& a = bt.e[blockIdx.y];
   const int HWo = a.Ho * a.Wo, Wo = a.Wo;
@@ -837,7 +882,62 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
 #pragma unroll
   for (int i = 0; i < CI * CO; ++i) gacc[i] = 0.f;
   const bool want_w = a.gW != nullptr;
-  for (int p = blockIdx.x * 256 + tid; p < total; p += gridDim.x * 256) {
+  if (V4) {
+    // 4 consecutive pixels per thread with 16-byte loads/stores (HWo % 4 == 0; mode 0, or
+    // mode 1 at stride 1 / offset 0 where the input plane is the output plane)
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const float* src = a.mode == 0 ? a.ain : a.x;
+    for (int t = blockIdx.x * 256 + tid; t < total / 4; t += gridDim.x * 256) {
+      const int p = t * 4, n = p / HWo, pp = p - n * HWo;
+      f4 dz[CO], av[CI];
+#pragma unroll
+      for (int c = 0; c < CO; ++c) {
+        const size_t gi = ((size_t)n * a.CoutTotal + a.co_off + c) * HWo + pp;
+        const f4 zz = *reinterpret_cast<const f4*>(a.gs.z + gi), gg = *reinterpret_cast<const f4*>(a.gs.g + gi);
+        dz[c] = wk * inv[c] * (gg - m1[c] - ((zz - mean[c]) * inv[c]) * m2[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < CI; ++c) {
+        av[c] = *reinterpret_cast<const f4*>(src + ((size_t)n * CI + c) * HWo + pp);
+        if (a.mode != 0) {
+          av[c].x = fmaxf(av[c].x, 0.f);
+          av[c].y = fmaxf(av[c].y, 0.f);
+          av[c].z = fmaxf(av[c].z, 0.f);
+          av[c].w = fmaxf(av[c].w, 0.f);
+        }
+      }
+      if (want_w) {
+#pragma unroll
+        for (int co = 0; co < CO; ++co)
+#pragma unroll
+          for (int ci = 0; ci < CI; ++ci) {
+            const f4 t2 = dz[co] * av[ci];
+            gacc[co * CI + ci] += (t2.x + t2.y) + (t2.z + t2.w);
+          }
+      }
+      if (a.need_dx) {
+#pragma unroll
+        for (int ci = 0; ci < CI; ++ci) {
+          f4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int co = 0; co < CO; ++co) v += wpw[co * CI + ci] * dz[co];
+          const size_t o = ((size_t)n * CI + ci) * HWo + pp;
+          if (a.mode == 0) {
+            *reinterpret_cast<f4*>(a.dd + o) = v;
+          } else {
+            f4 m;
+            m.x = av[ci].x > 0.f ? v.x : 0.f;
+            m.y = av[ci].y > 0.f ? v.y : 0.f;
+            m.z = av[ci].z > 0.f ? v.z : 0.f;
+            m.w = av[ci].w > 0.f ? v.w : 0.f;
+            f4* g = reinterpret_cast<f4*>(a.gx + o);
+            *g = a.overwrite ? m : *g + m;
+          }
+        }
+      }
+    }
+  }
+  for (int p = blockIdx.x * 256 + tid; p < (V4 ? 0 : total); p += gridDim.x * 256) {
     const int n = p / HWo, pp = p - n * HWo;
     float dz[CO], av[CI];
 #pragma unroll
@@ -1254,7 +1354,33 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
     }
   }
   // depthwise weight gradients over the band: thread per (channel, tap, pixel part)
-  if (a.gW && !(dbg & 2)) {
+  if (a.gW && !(dbg & 2) && S == 1) {
+    // stride 1: job = (channel, ky, own row). A 4-pixel quad of the input row (one 16-byte LDS
+    // read) and the 4 + 2*PAD dd values it meets across all K column taps (registers) feed
+    // 4*K multiply-adds: ~1.5 per LDS read against 0.5 for a pixel-by-pixel walk per tap
+    const int JB = C * K * nrow;
+    for (int j = tid; j < JB; j += 256) {
+      const int c = j / (K * nrow), rem = j - c * K * nrow, ky = rem / nrow, r = rem - ky * nrow;
+      const float* ddr = sDD + (c * ODR + iy0 + r + PAD - ky * DIL - oyA) * ODW + PO;
+      const float* inr = sIn + c * NP + r * W;
+      float acc[K];
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) acc[kx] = 0.f;
+      for (int ix = 0; ix < W; ix += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(inr + ix);
+        float dseg[4 + 2 * PAD];  // dseg[m] = dd[ix - PAD + m]
+#pragma unroll
+        for (int m = 0; m < 4 + 2 * PAD; ++m) dseg[m] = ddr[ix - PAD + m];
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const int o = 2 * PAD - kx * DIL;  // in[ix + q] meets dd[ix + q + PAD - kx*DIL]
+          acc[kx] += v.x * dseg[o] + v.y * dseg[o + 1] + v.z * dseg[o + 2] + v.w * dseg[o + 3];
+        }
+      }
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) atomicAdd(sGW + c * KK + ky * K + kx, acc[kx]);
+    }
+  } else if (a.gW && !(dbg & 2)) {
     constexpr int JOBS = C * KK, T = JOBS >= 256 ? 1 : 256 / JOBS;
     for (int j = tid; j < JOBS * T; j += 256) {
       const int job = j / T, part = j - job * T;
@@ -1436,8 +1562,16 @@ void launch_combine_fwd(const CombineFwdBatch& b, hipStream_t st) {
 
 void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st) {
   const CombineBwdArgs& a = b.e[0];
-  hipLaunchKernelGGL(combine_bwd_reduce_kernel, dim3(a.C * channel_groups(a.N, a.C, b.n), b.n), dim3(256), 0, st,
-                     b);
+  bool v4 = a.HW % 4 == 0;
+  for (int e = 0; e < b.n; ++e) {
+    const CombineBwdArgs& x = b.e[e];
+    uintptr_t bits = (uintptr_t)x.dout | (uintptr_t)x.xid;
+    for (int k = 0; k < x.nops; ++k) bits |= (uintptr_t)x.z[k];
+    v4 &= (bits & 15) == 0;
+  }
+  const dim3 grid(a.C * channel_groups(a.N, a.C, b.n), b.n);
+  if (v4) hipLaunchKernelGGL(combine_bwd_reduce_kernel<true>, grid, dim3(256), 0, st, b);
+  else hipLaunchKernelGGL(combine_bwd_reduce_kernel<false>, grid, dim3(256), 0, st, b);
 }
 
 template <int CI, int CO>
@@ -1445,8 +1579,19 @@ static bool try_pw_bwd_px(const PwBwdBatch& b, hipStream_t st) {
   const PwBwdArgs& a = b.e[0];
   if (a.Cin != CI || a.Cout != CO) return false;
   const int total = a.N * a.Ho * a.Wo;
-  const int per_edge = std::max(1, std::min((total + 255) / 256, max_blocks() / std::max(b.n, 1)));
-  hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO>), dim3(per_edge, b.n), dim3(256), 0, st, b);
+  // the 4-pixel vector path measured slower at C = 8 (register pressure: 21.7 vs 17.6 us) and
+  // neutral at C = 4 on MI355X; it stays selectable for experiments (KATIB_HIP_PW_PX_V4=1)
+  bool v4 = CI * CO <= 64 && (a.Ho * a.Wo) % 4 == 0 && getenv("KATIB_HIP_PW_PX_V4");
+  for (int e = 0; e < b.n && v4; ++e) {
+    const PwBwdArgs& x = b.e[e];
+    const bool m1ok = x.mode == 0 || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);
+    const uintptr_t bits = (uintptr_t)x.gs.z | (uintptr_t)x.gs.g | (uintptr_t)(x.mode == 0 ? x.ain : x.x) |
+                           (uintptr_t)(x.mode == 0 ? x.dd : x.gx);
+    v4 = m1ok && (bits & 15) == 0 && x.co_off % 4 == 0;
+  }
+  const int per_edge = std::max(1, std::min(((v4 ? total / 4 : total) + 255) / 256, max_blocks() / std::max(b.n, 1)));
+  if (v4) hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO, true>), dim3(per_edge, b.n), dim3(256), 0, st, b);
+  else hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO, false>), dim3(per_edge, b.n), dim3(256), 0, st, b);
   return true;
 }
 
