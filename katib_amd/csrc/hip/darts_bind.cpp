@@ -465,6 +465,7 @@ void register_batchnorm(py::module& m);  // batchnorm_bind.cpp
 void register_mlp(py::module& m);  // mlp_bind.cpp
 void register_stem(py::module& m);  // stem_bind.cpp
 void register_enas(py::module& m);  // enas_bind.cpp
+void register_dwconv(py::module& m);  // dwconv_bind.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, transformer, xGMI all-reduce)";
@@ -486,6 +487,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_transformer(m);
   register_batchnorm(m);
   register_enas(m);
+  register_dwconv(m);
   register_mlp(m);
   register_stem(m);
 }

@@ -13,8 +13,9 @@ batches of 128, printing ``Training-Accuracy``, ``Training-Loss``,
 ``Validation-Accuracy``, ``Validation-Loss`` per epoch.
 
 MI355X specifics: channels-last bf16 convolutions on the hand-written implicit-GEMM
-MFMA kernels (``ops/conv.py``; TF 'same' padding handled inside the kernel's gather,
-depthwise convolutions stay on MIOpen), batch norm on the NHWC bf16 HIP kernels
+MFMA kernels (``ops/conv.py``; TF 'same' padding handled inside the kernel's gather),
+depthwise convolutions on the NHWC depthwise kernels (``ops/dwconv.py``; the 3-channel
+image input, not a multiple of 8, stays on MIOpen), batch norm on the NHWC bf16 HIP kernels
 (``ops/batchnorm.py``, channel counts that are multiples of 8), the train step
 captured as a HIP graph, synthetic CIFAR-10-shaped data in HBM, and data parallelism
 over the trial's GPUs (``WORLD_SIZE`` ranks, RCCL all-reduce of the flat gradient)
@@ -34,6 +35,7 @@ import torch.nn.functional as F
 
 from ..ops import batchnorm as hbn
 from ..ops import conv as hconv
+from ..ops import dwconv as hdw
 from .common import CapturedStep, Timer, device, pattern_images, report
 
 
@@ -55,6 +57,8 @@ class _SameConv(nn.Module):
         c = self.conv
         if hconv.supported(x, c.weight, c.groups):  # HIP implicit-GEMM (MFMA) path
             return hconv.same_conv2d(x, c.weight, c.bias, self.s)
+        if c.groups > 1 and hdw.supported(x, c.weight, c.groups, self.s):  # HIP depthwise (NHWC) path
+            return hdw.depthwise_same(x, c.weight, c.bias, self.s)
         t, b, _ = _same_pad(x.shape[2], self.k, self.s)
         l, r, _ = _same_pad(x.shape[3], self.k, self.s)
         return self.conv(F.pad(x, (l, r, t, b)))
