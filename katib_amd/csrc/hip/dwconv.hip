@@ -56,35 +56,50 @@ template <int K, int DM>
 __global__ void __launch_bounds__(256) dw_fwd_kernel(Geom g, const __hip_bfloat16* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      __hip_bfloat16* __restrict__ y) {
-  const int Co = g.C * DM, G = Co / 8;
-  const long total = (long)g.N * g.OH * g.OW * G;
+  // thread = (4 consecutive output pixels of a row, 8 channels): each tap's 8 weights are
+  // loaded once for the 4 pixels
+  constexpr int PX = 4;
+  const int Co = g.C * DM, G = Co / 8, QW = (g.OW + PX - 1) / PX;
+  const long total = (long)g.N * g.OH * QW * G;
   for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
     const int gg = (int)(idx % G);
     long p = idx / G;
-    const int ox = (int)(p % g.OW);
-    p /= g.OW;
+    const int ox0 = (int)(p % QW) * PX;
+    p /= QW;
     const int oy = (int)(p % g.OH), n = (int)(p / g.OH);
     const int o0 = gg * 8, c0 = o0 / DM;
-    float acc[8];
+    float acc[PX][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = bias ? bias[o0 + j] : 0.f;
+    for (int j = 0; j < 8; ++j) {
+      const float b0 = bias ? bias[o0 + j] : 0.f;
+#pragma unroll
+      for (int q = 0; q < PX; ++q) acc[q][j] = b0;
+    }
 #pragma unroll
     for (int ky = 0; ky < K; ++ky) {
       const int iy = oy * g.S - g.pt + ky;
       if (iy < 0 || iy >= g.H) continue;
+      const __hip_bfloat16* xrow = x + (((long)n * g.H + iy) * g.W) * g.C + c0;
 #pragma unroll
       for (int kx = 0; kx < K; ++kx) {
-        const int ix = ox * g.S - g.pl + kx;
-        if (ix < 0 || ix >= g.W) continue;
-        float xv[8];
-        load_in8<DM>(x + (((long)n * g.H + iy) * g.W + ix) * g.C + c0, xv);
         const float4* wt = reinterpret_cast<const float4*>(w + (ky * K + kx) * Co + o0);
         const float4 wa = wt[0], wb = wt[1];
-        acc[0] += xv[0] * wa.x, acc[1] += xv[1] * wa.y, acc[2] += xv[2] * wa.z, acc[3] += xv[3] * wa.w;
-        acc[4] += xv[4] * wb.x, acc[5] += xv[5] * wb.y, acc[6] += xv[6] * wb.z, acc[7] += xv[7] * wb.w;
+        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+        for (int q = 0; q < PX; ++q) {
+          const int ix = (ox0 + q) * g.S - g.pl + kx;
+          if (ox0 + q >= g.OW || ix < 0 || ix >= g.W) continue;
+          float xv[8];
+          load_in8<DM>(xrow + (long)ix * g.C, xv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[q][j] += xv[j] * wv[j];
+        }
       }
     }
-    *reinterpret_cast<uint4*>(y + (((long)n * g.OH + oy) * g.OW + ox) * Co + o0) = pack8(acc);
+#pragma unroll
+    for (int q = 0; q < PX; ++q)
+      if (ox0 + q < g.OW)
+        *reinterpret_cast<uint4*>(y + (((long)n * g.OH + oy) * g.OW + ox0 + q) * Co + o0) = pack8(acc[q]);
   }
 }
 
@@ -133,7 +148,9 @@ __global__ void __launch_bounds__(256) dw_dgrad_kernel(Geom g, const __hip_bfloa
 }
 
 // one workgroup per band of output rows (flattened n*OH + oy); job = (channel group, tap):
-// acc[8] over the band's pixels, one partial row per workgroup
+// acc[8] over the band's pixels, one partial row per workgroup. (A (channel group, kernel row)
+// job with K column accumulators reads gy once per K taps but leaves most threads idle at these
+// channel counts: measured 2x slower at K = 5.)
 template <int K, int DM>
 __global__ void __launch_bounds__(256) dw_wgrad_kernel(Geom g, const __hip_bfloat16* __restrict__ x,
                                                        const __hip_bfloat16* __restrict__ gy,
@@ -191,7 +208,7 @@ int wgrad_rows(const Geom& g) {
 
 hipError_t launch_fwd(const Geom& g, const __hip_bfloat16* x, const float* w, const float* bias, __hip_bfloat16* y,
                       hipStream_t st) {
-  const long total = (long)g.N * g.OH * g.OW * (g.C * g.DM / 8);
+  const long total = (long)g.N * g.OH * ((g.OW + 3) / 4) * (g.C * g.DM / 8);
   KATIB_DW_DISPATCH(dw_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, g, x, w, bias, y)
   return hipGetLastError();
 }
