@@ -113,6 +113,48 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Reduce-scatter of M per-lane accumulators across the wave (M a power of two <= 64): at each
+// butterfly step a lane keeps half of its values and sends the other half to its partner, so
+// after log2(M) steps every lane holds one partial and the remaining 6 - log2(M) steps finish
+// the sum: M - 1 + 6 - log2(M) shuffles instead of 6 * M for M separate wave sums. Returns the
+// total of accumulator wave_scatter_index<M>(lane) (identical on the 64 / M lanes sharing it).
+// (each butterfly level is its own instantiation so every register index is a constant: a
+// runtime-bounded level loop made the compiler move the accumulators to scratch)
+template <int H, int D>
+__device__ __forceinline__ void reduce_scatter_level(float* acc, int lane) {
+  if constexpr (H >= 1) {
+    const bool up = (lane & D) != 0;  // upper partner keeps the upper half
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      const float keep = up ? acc[i + H] : acc[i];
+      const float send = up ? acc[i] : acc[i + H];
+      acc[i] = keep + __shfl_xor(send, D, 64);
+    }
+    reduce_scatter_level<H / 2, D / 2>(acc, lane);
+  }
+}
+
+template <int M>
+__device__ __forceinline__ float wave_reduce_scatter(float* acc) {
+  const int lane = threadIdx.x & 63;
+  reduce_scatter_level<M / 2, 32>(acc, lane);
+  float v = acc[0];
+#pragma unroll
+  for (int d = 32 / M; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// accumulator index lane's wave_reduce_scatter<M> result belongs to (lane bits 5, 4, ... select
+// the upper / lower halves in turn)
+template <int M>
+__device__ __forceinline__ int wave_scatter_index(int lane) {
+  int idx = 0;
+#pragma unroll
+  for (int h = M / 2, d = 32; h >= 1; h >>= 1, d >>= 1)
+    if (lane & d) idx += h;
+  return idx;
+}
+
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -356,13 +398,12 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
     }
   }
   if (!a.stats) return;
+  {
+    float st[2 * C];  // [sum | sum of squares], reduce-scattered over the wave
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const float v1 = wave_sum(st1[c]), v2 = wave_sum(st2[c]);
-    if (lane == 0) {
-      atomicAdd(sStat + c, v1);
-      atomicAdd(sStat + C + c, v2);
-    }
+    for (int c = 0; c < C; ++c) st[c] = st1[c], st[C + c] = st2[c];
+    const float v = wave_reduce_scatter<2 * C>(st);
+    if ((lane & (32 / C - 1)) == 0) atomicAdd(sStat + wave_scatter_index<2 * C>(lane), v);
   }
   __syncthreads();
   if (tid < 2 * C) atomicAdd(a.stats + rep_slot() * 2 * C + tid, (double)sStat[tid]);
@@ -461,16 +502,11 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdBatch bt) {
   }
   if (!a.stats_avg && !a.stats_max) return;
   __shared__ float red[4][4];
-  sa = wave_sum(sa);
-  sa2 = wave_sum(sa2);
-  sm = wave_sum(sm);
-  sm2 = wave_sum(sm2);
   int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 0) {
-    red[wave][0] = sa;
-    red[wave][1] = sa2;
-    red[wave][2] = sm;
-    red[wave][3] = sm2;
+  {
+    float v[4] = {sa, sa2, sm, sm2};
+    const float t = wave_reduce_scatter<4>(v);
+    if ((lane & 15) == 0) red[wave][wave_scatter_index<4>(lane)] = t;
   }
   __syncthreads();
   if (threadIdx.x < 4) {
@@ -636,15 +672,17 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdBatch
     }
   }
   int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  s1 = wave_sum(s1);
-  sid = wave_sum(sid);
+  {
+    // [s1, sid, s2[0..kMaxOps)] reduce-scattered over the wave (padded to 16 accumulators)
+    static_assert(kMaxOps + 2 <= 16, "combine_bwd_reduce: accumulators exceed the 16-slot scatter");
+    float v[16];
+    v[0] = s1;
+    v[1] = sid;
 #pragma unroll
-  for (int k = 0; k < kMaxOps; ++k) s2[k] = wave_sum(s2[k]);
-  if (lane == 0) {
-    part[wave][0] = s1;
-    part[wave][1] = sid;
-#pragma unroll
-    for (int k = 0; k < kMaxOps; ++k) part[wave][2 + k] = s2[k];
+    for (int k = 0; k < 14; ++k) v[2 + k] = k < kMaxOps ? s2[k] : 0.f;
+    const float t = wave_reduce_scatter<16>(v);
+    const int j = wave_scatter_index<16>(lane);
+    if ((lane & 3) == 0 && j < kMaxOps + 2) part[wave][j] = t;
   }
   __syncthreads();
   double* red = a.red + (size_t)rep_slot() * a.rstride;
@@ -978,10 +1016,16 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
     }
   }
   if (!want_w) return;
+  constexpr int M = CI * CO;
+  if (M <= 64 && (M & (M - 1)) == 0) {
+    const float s = wave_reduce_scatter<(M <= 64 ? M : 64)>(gacc);
+    if ((lane & (64 / M - 1)) == 0) atomicAdd(sGW + wave_scatter_index<(M <= 64 ? M : 64)>(lane), s);
+  } else {
 #pragma unroll
-  for (int i = 0; i < CI * CO; ++i) {
-    const float s = wave_sum(gacc[i]);
-    if (lane == 0) atomicAdd(sGW + i, s);
+    for (int i = 0; i < M; ++i) {
+      const float s = wave_sum(gacc[i]);
+      if (lane == 0) atomicAdd(sGW + i, s);
+    }
   }
   __syncthreads();
   float* gW = a.gW + (size_t)rep_slot() * a.gstride;
@@ -1344,14 +1388,11 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
     }
   }
   if (PREBN && a.red) {
+    float st[2 * C];  // [sum g | sum g*y], reduce-scattered over the wave
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const float v1 = wave_sum(st1[c]), v2 = wave_sum(st2[c]);
-      if (lane == 0) {
-        atomicAdd(sRed + c, v1);
-        atomicAdd(sRed + C + c, v2);
-      }
-    }
+    for (int c = 0; c < C; ++c) st[c] = st1[c], st[C + c] = st2[c];
+    const float v = wave_reduce_scatter<2 * C>(st);
+    if ((lane & (32 / C - 1)) == 0) atomicAdd(sRed + wave_scatter_index<2 * C>(lane), v);
   }
   // depthwise weight gradients over the band: thread per (channel, tap, pixel part)
   if (a.gW && !(dbg & 2) && S == 1) {
