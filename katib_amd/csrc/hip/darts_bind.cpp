@@ -333,7 +333,7 @@ void pw_bwd(std::vector<py::tuple> calls, int64_t S, int64_t mode, bool need_dx)
     a.Cin = Cin; a.Cout = Cout; a.co_off = co_off; a.S = S; a.off = off; a.mode = mode;
     a.need_dx = need_dx;
     a.H = x.size(2); a.W = x.size(3);
-    TORCH_CHECK(Cin * Cout <= 4096, "pw_bwd supports Cin*Cout <= 4096");
+    TORCH_CHECK(Cin * Cout <= 8192, "pw_bwd supports Cin*Cout <= 8192");
     TORCH_CHECK((a.Ho * a.Wo) % 64 == 0, "Ho*Wo % 64");
     a.pw = pw.data_ptr<float>(); a.x = x.data_ptr<float>();
     a.ain = ptr_or_null<float>(ain); a.dd = ptr_or_null<float>(dd); a.gx = ptr_or_null<float>(gx);

@@ -718,7 +718,7 @@ __device__ __forceinline__ float bn_bwd_val(const GradSrc& gs, size_t i, float m
 // mode 1 (StdConv / FR half): a_in = relu(x) at strided positions; gx += dd * (x > 0).
 // grid: persistent over 64-pixel tiles; weight grads accumulated in registers across tiles.
 // ------------------------------------------------------------------------------------------------
-template <bool MFMA>
+template <bool MFMA, int MBLK = 4>
 __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
   const PwBwdArgs& a = bt.e[blockIdx.y];
   constexpr int P = 64, PS = P + 1;  // padded LDS rows: per-channel row reads hit distinct banks
@@ -743,13 +743,15 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   // weight-grad accumulators live in registers across tiles.
   // scalar path: pairs (co, ci) = tid + 256*j; MFMA path: 16x16 blocks b = wave + 4*j
-  constexpr int MAXJ = 16;  // Cout*Cin <= 4096
+  // Cout*Cin <= 8192 (the 128 -> 64 preprocess of darts-gpu.yaml's last cell); MFMA: MBLK 16x16
+  // blocks per wave (4 waves x MBLK x 256), 8 only where needed (more accumulators, fewer waves)
+  constexpr int MAXJ = 32;
   float gacc[MFMA ? 1 : MAXJ];
-  f4 macc[MFMA ? 4 : 1];
+  f4 macc[MFMA ? MBLK : 1];
 #pragma unroll
   for (int j = 0; j < (MFMA ? 1 : MAXJ); ++j) gacc[j] = 0.f;
 #pragma unroll
-  for (int j = 0; j < (MFMA ? 4 : 1); ++j) macc[j] = f4{0, 0, 0, 0};
+  for (int j = 0; j < (MFMA ? MBLK : 1); ++j) macc[j] = f4{0, 0, 0, 0};
   const int npairs = Cout * Cin;
   const int nbi = Cin / 16, nblk = (Cout / 16) * nbi;
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -778,7 +780,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
       if (MFMA) {
         // gW[co][ci] += sum_p dz[co][p] * a[ci][p]  (M = co, N = ci, K = pixels)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < MBLK; ++j) {
           int b = wave + 4 * j;
           if (b < nblk) {
             int cob = (b / nbi) * 16, cib = (b % nbi) * 16;
@@ -860,7 +862,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
     float* gW = a.gW + (size_t)rep_slot() * a.gstride;
     if (MFMA) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < MBLK; ++j) {
         int b = wave + 4 * j;
         if (b < nblk) {
           int cob = (b / nbi) * 16, cib = (b % nbi) * 16;
@@ -1646,9 +1648,10 @@ void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st) {
   int ntiles = a.N * a.Ho * a.Wo / 64;
   dim3 grid(per_edge_blocks(ntiles, b.n), b.n);
   size_t lds = sizeof(float) * (a.Cout * 65 + a.Cin * 65 + 4 * a.Cout + 4);
-  const bool mfma = a.Cin % 16 == 0 && a.Cout % 16 == 0 && (a.Cin / 16) * (a.Cout / 16) <= 16;
-  if (mfma) hipLaunchKernelGGL(pw_bwd_kernel<true>, grid, dim3(256), lds, st, b);
-  else hipLaunchKernelGGL(pw_bwd_kernel<false>, grid, dim3(256), lds, st, b);
+  const int nblk = (a.Cin % 16 == 0 && a.Cout % 16 == 0) ? (a.Cin / 16) * (a.Cout / 16) : 1 << 30;
+  if (nblk <= 16) hipLaunchKernelGGL((pw_bwd_kernel<true, 4>), grid, dim3(256), lds, st, b);
+  else if (nblk <= 32) hipLaunchKernelGGL((pw_bwd_kernel<true, 8>), grid, dim3(256), lds, st, b);
+  else hipLaunchKernelGGL((pw_bwd_kernel<false>), grid, dim3(256), lds, st, b);
 }
 
 

@@ -322,7 +322,7 @@ class DartsNetwork:
                     h //= 2
                 else:
                     ok = ok and tile_ok(C, h, 1)
-                ok = ok and cell["cpp"] * C <= 4096 and cell["cp"] * C <= 4096
+                ok = ok and cell["cpp"] * C <= 8192 and cell["cp"] * C <= 8192
             self._specs[key] = ok
         return ok
 
@@ -381,13 +381,13 @@ class DartsNetwork:
         if reduce:
             w1, w2 = P[name + ".conv1"], P[name + ".conv2"]
             hd = self._hip(x, 2)
-            if hd is not None and w1.shape[0] * w1.shape[1] <= 4096:
+            if hd is not None and w1.shape[0] * w1.shape[1] <= 8192:
                 return hd.factorized_reduce_bn(x, w1, w2, rm, rv, training, self.momentum, self.eps)
             t = ops.factorized_reduce(x, w1, w2)
         else:
             w = P[name + ".conv"]
             hd = self._hip(x, 1)
-            if hd is not None and w.shape[0] * w.shape[1] <= 4096:
+            if hd is not None and w.shape[0] * w.shape[1] <= 8192:
                 return hd.relu_conv_bn(x, w, rm, rv, training, self.momentum, self.eps)
             t = ops.relu_conv1x1(x, w)
         return F.batch_norm(t, rm, rv, None, None, training, self.momentum, self.eps)
