@@ -529,14 +529,17 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
   float* sMean = smem;                                 // [ne][kMaxOps][C]
   float* sInv = sMean + ne * kMaxOps * C;              // [ne][kMaxOps][C]
   float* sW = sInv + ne * kMaxOps * C;                 // [ne][kMaxOps + 1]
-  for (int e = 0; e < ne; ++e) {
+  // every (edge, op, channel) coefficient in one pass: one round of statistic loads per block
+  for (int i = threadIdx.x; i < ne * kMaxOps * C; i += 256) {
+    const int e = i / (kMaxOps * C), k = (i / C) % kMaxOps, c = i % C;
     const CombineFwdArgs& a = bt.e[e];
-    for (int i = threadIdx.x; i < a.nops * C; i += 256) {
-      int k = i / C, c = i % C;
-      bn_coeffs(a.bn[k], c, sMean[(e * kMaxOps + k) * C + c], sInv[(e * kMaxOps + k) * C + c]);
-    }
-    if (threadIdx.x < a.nops) sW[e * (kMaxOps + 1) + threadIdx.x] = a.w ? a.w[a.widx[threadIdx.x]] : 1.f;
-    if (threadIdx.x == 0) sW[e * (kMaxOps + 1) + kMaxOps] = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+    if (k < a.nops) bn_coeffs(a.bn[k], c, sMean[i], sInv[i]);
+  }
+  for (int i = threadIdx.x; i < ne * (kMaxOps + 1); i += 256) {
+    const int e = i / (kMaxOps + 1), k = i % (kMaxOps + 1);
+    const CombineFwdArgs& a = bt.e[e];
+    if (k < a.nops) sW[i] = a.w ? a.w[a.widx[k]] : 1.f;
+    else if (k == kMaxOps) sW[i] = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
   }
   __syncthreads();
   if (blockIdx.x == 0) {
