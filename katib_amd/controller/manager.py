@@ -81,6 +81,7 @@ class TrialRun:
     collector: Dict = field(default_factory=dict)
     path_map: Dict[str, str] = field(default_factory=dict)
     deleted: bool = False
+    scraper: Optional[object] = None  # PrometheusMetric collector (metricscollector/prometheus.py)
 
 
 @dataclass
@@ -286,6 +287,7 @@ class Manager:
             timeout_ms = self.config.amd.poll_interval_ms
         events = self.runtime.poll(timeout_ms)
         with self._lock:
+            self._scrape_prometheus()
             for ev in events:
                 self._on_runtime_event(ev)
             for key in list(self.experiments):
@@ -884,6 +886,16 @@ class Manager:
             d = dst if not os.path.splitext(dst)[1] else os.path.dirname(dst)
             os.makedirs(d, exist_ok=True)
         run.collector = self._collector_cfg(trial, run)
+        prom_env = {}
+        if run.collector.get("kind") == _KIND_CODES[C.COLLECTOR_PROMETHEUS]:
+            from ..metricscollector.prometheus import Scraper
+            from .jobs import free_port
+
+            hg = mc.source.http_get if mc is not None and mc.source is not None else None
+            mpath = (hg.path if hg is not None and hg.path else C.DEFAULT_PROMETHEUS_PATH)
+            port = free_port()  # one port per trial: concurrent trials cannot share the spec's
+            run.scraper = Scraper(port, mpath, run.collector["metric_names"])
+            prom_env = {"KATIB_PROMETHEUS_PORT": str(port), "KATIB_PROMETHEUS_PATH": mpath}
         log_path = os.path.join(run.trial_dir, "metrics.log")
         base_env = {"KATIB_TRIAL_NAME": name, "KATIB_EXPERIMENT_NAME": exp_name, "KATIB_TRIAL_DIR": run.trial_dir,
                     "KATIB_NAMESPACE": ns, "PYTHONUNBUFFERED": "1",
@@ -892,6 +904,7 @@ class Manager:
                     "KATIB_TRIAL_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or "",
                     # trials may run the built-in workloads with `python -m katib_amd.workloads.X`
                     "PYTHONPATH": os.pathsep.join(p for p in (_PKG_ROOT, os.environ.get("PYTHONPATH", "")) if p)}
+        base_env.update(prom_env)
         # each replica gets its share of the trial's devices
         dev_iter = iter(run.devices)
         plan = run.plan
@@ -1066,6 +1079,17 @@ class Manager:
         else:
             msg = ev["message"] or ""
             self._finish_trial(tkey, "Failed", "Error", "exit code %d%s" % (code, (": " + msg) if msg else ""))
+
+    def _scrape_prometheus(self):
+        """PrometheusMetric collector: scrape every running trial whose interval is due."""
+        now = time.time()
+        for tkey, run in self.runs.items():
+            sc = run.scraper
+            if sc is None or run.phase not in ("Launching", "Running") or not sc.due(now):
+                continue
+            logs = sc.scrape(now)
+            if logs:
+                self.store.report(tkey[1], logs)
 
     def _collect_tfevent(self, trial, run):
         from ..metricscollector.tfevent import collect

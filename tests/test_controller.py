@@ -447,3 +447,57 @@ trialTemplate:
         assert len(m.slots.quarantined()) >= 1
     finally:
         m.shutdown()
+
+
+def test_prometheus_collector(manager):
+    """PrometheusMetric: the scheduler scrapes the trial's /metrics endpoint (port from
+    KATIB_PROMETHEUS_PORT) and records every changed sample of the experiment's metrics."""
+    code = textwrap.dedent("""
+        import os, threading, time
+        from http.server import BaseHTTPRequestHandler, HTTPServer
+        state = {"acc": 0.25, "loss": 2.0}
+        class H(BaseHTTPRequestHandler):
+            def log_message(self, *a): pass
+            def do_GET(self):
+                if self.path != os.environ["KATIB_PROMETHEUS_PATH"]:
+                    self.send_response(404); self.end_headers(); return
+                body = ("# HELP acc accuracy\\n# TYPE acc gauge\\nacc %s\\nloss{split=\\"train\\"} %s\\n"
+                        "other_metric 7\\n" % (state["acc"], state["loss"])).encode()
+                self.send_response(200); self.send_header("Content-Length", str(len(body))); self.end_headers()
+                self.wfile.write(body)
+        srv = HTTPServer(("127.0.0.1", int(os.environ["KATIB_PROMETHEUS_PORT"])), H)
+        threading.Thread(target=srv.serve_forever, daemon=True).start()
+        for acc, loss in ((0.5, 1.0), (0.75, 0.5)):
+            time.sleep(0.8)
+            state["acc"], state["loss"] = acc, loss
+        time.sleep(0.8)  # keep the endpoint up for a last scrape
+    """)
+    e = quadratic_yaml(name="prom", command=[PY, "-c", code, "${trialParameters.a}"], parallel=1, max_trials=1,
+                       params=[{"name": "a", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                       extra_spec=yaml.safe_dump({
+                           "objective": {"type": "maximize", "objectiveMetricName": "acc",
+                                         "additionalMetricNames": ["loss"]},
+                           "metricsCollectorSpec": {"collector": {"kind": "PrometheusMetric"}}}))
+    manager.create_experiment(e)
+    done = manager.run_until_complete("prom", timeout=60)
+    assert EC.is_succeeded(done), done.status.conditions
+    ms = {m.name: m for m in done.status.current_optimal_trial.observation.metrics}
+    assert (ms["acc"].min, ms["acc"].max, ms["acc"].latest) == ("0.25", "0.75", "0.75")
+    assert ms["loss"].latest == "0.5"
+    trial = done.status.current_optimal_trial.best_trial_name
+    values = [v for _, n, v in manager.get_observation_log(trial) if n == "acc"]
+    assert values == ["0.25", "0.5", "0.75"]  # one entry per change, not per scrape
+
+
+def test_prometheus_exposition_parser():
+    from katib_amd.metricscollector.prometheus import Scraper, parse_exposition
+
+    text = ("# HELP acc x\n# TYPE acc gauge\nacc 0.5\nacc{split=\"val\"} 0.25 1700000000000\n"
+            "accuracy 9\nloss NaN\nbad line here\nloss +Inf\n")
+    assert parse_exposition(text, ["acc", "loss"]) == [
+        ("acc", "0.5", None), ("acc", "0.25", 1700000000000), ("loss", "NaN", None), ("loss", "+Inf", None)]
+    sc = Scraper(1, "/metrics", ["acc"])
+    first = sc.observe("acc 1\n", 0.0)
+    assert first == [("1970-01-01T00:00:00Z", "acc", "1")]
+    assert sc.observe("acc 1\n", 1.0) == [] and sc.observe("acc 2\n", 1.5)[0][2] == "2"
+    assert sc.observe("acc 2 1700000000250\n", 2.0) == [("2023-11-14T22:13:20.25Z", "acc", "2")]
