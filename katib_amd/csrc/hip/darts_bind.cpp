@@ -135,7 +135,7 @@ void dwpw_fwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, i
     const int TR = 64 / Wo;
     const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
     a.chunk = pick_chunk(C, IR * IW, C * 64 + 4 * C);
-    if (C == 4 || C == 8) {
+    if (C == 4 || C == 8 || C == 16) {
       // dwpw_plane: `chunk` = row bands per image, ~2048 workgroups per launch and >= 4
       // output rows per band, capped so the staged band fits 64 KB of LDS
       int nb = std::max(1, std::min(Ho / 4, 2048 / std::max(N * (int)calls.size(), 1)));
@@ -177,7 +177,7 @@ void pw_fwd(std::vector<py::tuple> calls, int64_t S) {
     if (a.stats)
       TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * z.size(1), "stats [kRep][2Ctot]");
     a.N = N; a.Cin = Cin; a.Cout = Cout; a.CoutTotal = z.size(1); a.co_off = co_off;
-    a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off;
+    a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off; a.relu = 1;
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, Cin); SAME_SHAPE(bt, Cout); SAME_SHAPE(bt, Ho); SAME_SHAPE(bt, Wo);
   }
   launch_pw_fwd(bt, cur_stream());

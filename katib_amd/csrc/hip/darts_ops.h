@@ -47,6 +47,7 @@ struct DwPwFwdArgs {
 struct PwFwdArgs {
   const float* x; const float* pw; float* z; double* stats;  // stats: kRep replicas of [2*CoutTotal]
   int N, Cin, Cout, CoutTotal, co_off, H, W, Ho, Wo, S, off;
+  int relu;  // 1: input = relu(x) (StdConv / FactorizedReduce); 0: identity (pointwise half of a dw-pw stage)
 };
 
 struct PoolFwdArgs {

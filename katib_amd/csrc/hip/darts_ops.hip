@@ -294,14 +294,17 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
 // for a dilated 5x5 on 2-row tiles, a barrier-separated load/compute chain per tile) this
 // reads each input pixel once and has a single barrier before the compute.
 // ------------------------------------------------------------------------------------------------
-template <int K, int DIL, int S, bool PREBN, int C, bool VEC>
+// PW = false (layers wider than 16 channels): depthwise only, d of C-channel group blockIdx.x % (a.C / C);
+// the pointwise then runs as its own GEMM (pw_fwd_wave_kernel)
+template <int K, int DIL, int S, bool PREBN, int C, bool VEC, bool PW = true>
 __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
   const DwPwFwdArgs& a = bt.e[blockIdx.y];
   constexpr int KK = K * K;
   const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, pad = a.pad;
   // workgroup = (image n, band of BR output rows); the band's input rows + halo are staged
   const int nb = a.chunk, BR = (Ho + nb - 1) / nb;  // chunk carries the band count
-  const int n = blockIdx.x / nb, band = blockIdx.x - n * nb;
+  const int G = PW ? 1 : a.C / C, c0 = PW ? 0 : (blockIdx.x % G) * C, nbx = PW ? blockIdx.x : blockIdx.x / G;
+  const int n = nbx / nb, band = nbx - n * nb;
   const int oy0 = band * BR, oy1 = min(Ho, oy0 + BR);
   const int HP = (BR - 1) * S + (K - 1) * DIL + 1, WP = W + 2 * pad, PL = HP * WP;
   const int iyb = oy0 * S - pad;  // input row of staged row 0
@@ -310,12 +313,12 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
   __shared__ float sMean[C], sInv[C], sStat[2 * C];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < C) {
-    if (PREBN) bn_coeffs(a.inbn, tid, sMean[tid], sInv[tid]);
+    if (PREBN) bn_coeffs(a.inbn, c0 + tid, sMean[tid], sInv[tid]);
     sStat[tid] = 0.f;
     sStat[C + tid] = 0.f;
   }
   __syncthreads();
-  const float* xin = a.x + (size_t)n * C * H * W;
+  const float* xin = a.x + ((size_t)n * a.C + c0) * H * W;
   if (VEC) {
     // 16-byte loads over the band's contiguous in-range rows, scattered into the padded plane;
     // the zero border (rows outside [0, H), pad columns) is written separately
@@ -370,7 +373,7 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
 #pragma unroll
   for (int c = 0; c < C; ++c) st1[c] = st2[c] = 0.f;
   const int HWo = Ho * Wo;
-  float* dn = a.d + (size_t)n * C * HWo;
+  float* dn = a.d + ((size_t)n * a.C + c0) * HWo;
   float* zn = a.z + (size_t)n * C * HWo;
   for (int p = oy0 * Wo + tid; p < oy1 * Wo; p += 256) {
     const int oy = p / Wo, ox = p - oy * Wo;
@@ -378,7 +381,7 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const float* src = sIn + c * PL + ((oy - oy0) * S) * WP + ox * S;
-      const float* wk = a.dw + c * KK;  // uniform -> scalar loads
+      const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
       float acc = 0.f;
 #pragma unroll
       for (int ky = 0; ky < K; ++ky)
@@ -387,6 +390,7 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
       d[c] = acc;
       dn[(size_t)c * HWo + p] = acc;
     }
+    if (!PW) continue;
 #pragma unroll
     for (int co = 0; co < C; ++co) {
       float z = 0.f;
@@ -397,7 +401,7 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
       st2[co] += z * z;
     }
   }
-  if (!a.stats) return;
+  if (!PW || !a.stats) return;
   {
     float st[2 * C];  // [sum | sum of squares], reduce-scattered over the wave
 #pragma unroll
@@ -407,6 +411,99 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
   }
   __syncthreads();
   if (tid < 2 * C) atomicAdd(a.stats + rep_slot() * 2 * C + tid, (double)sStat[tid]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// pw_fwd_wave: z[:, co_off + co] = pw . act(x) for Cin, Cout multiples of 16 (<= 64), plus the BN
+// statistics of z. act = relu at (oy*S + off, ox*S + off) (StdConv / FactorizedReduce half) or the
+// identity (a.relu == 0: the pointwise half of a wide dw-pw stage, x = the depthwise output d).
+// One wave per 64-pixel chunk, no LDS and no barrier in the loop:
+//   A[i = co][k = ci] = pw, preloaded in registers for the whole kernel;
+//   B[k = ci][j]      lane (c16, q) loads pixels 4*c16 .. 4*c16+3 of channel k0 + q with one 16-byte
+//                     load; MFMA t in 0..3 takes pixel 4*j + t as column j, so the D fragment a lane
+//                     holds for (co, t = 0..3) is 4 consecutive pixels: one 16-byte store.
+// Statistics stay per lane across chunks and are reduced once per workgroup at the end.
+// ------------------------------------------------------------------------------------------------
+template <int CI, int CO>
+__global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
+  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64, "16-channel blocks");
+  constexpr int BO = CO / 16, KS = CI / 4;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const PwFwdArgs& a = bt.e[blockIdx.y];
+  const int HWo = a.Ho * a.Wo, Wo = a.Wo;
+  const int nchunks = a.N * HWo / 64;  // HWo % 64 == 0 (host-checked)
+  __shared__ float sStat[2 * CO];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, c16 = lane & 15, q = lane >> 4;
+  for (int i = tid; i < 2 * CO; i += 256) sStat[i] = 0.f;
+  __syncthreads();
+  float wA[BO][KS];
+#pragma unroll
+  for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+    for (int k = 0; k < KS; ++k) wA[bo][k] = a.pw[(bo * 16 + c16) * CI + 4 * k + q];
+  const bool flat = !a.relu || (a.S == 1 && a.off == 0 && a.H == a.Ho && a.W == a.Wo);
+  f4 s1[BO], s2[BO];  // per-lane partial sums of z, z^2 for channels bo*16 + 4q + r
+#pragma unroll
+  for (int bo = 0; bo < BO; ++bo) s1[bo] = s2[bo] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int ch = blockIdx.x * 4 + wave; ch < nchunks; ch += gridDim.x * 4) {
+    const int pix0 = ch * 64, n = pix0 / HWo, prem = pix0 - n * HWo;
+    const int pp = prem + 4 * c16;  // this lane's 4 pixels
+    f4 acc[BO][4];
+#pragma unroll
+    for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[bo][t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int ci = 4 * k + q;
+      f4 v;
+      if (flat) {
+        v = *reinterpret_cast<const f4*>(a.x + ((size_t)n * CI + ci) * HWo + pp);
+        if (a.relu) v = f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int p = pp + t, oy = p / Wo, ox = p - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+          v[t] = (iy < a.H && ix < a.W) ? fmaxf(a.x[(((size_t)n * CI + ci) * a.H + iy) * a.W + ix], 0.f) : 0.f;
+        }
+      }
+#pragma unroll
+      for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[bo][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[bo][k], v[t], acc[bo][t], 0, 0, 0);
+    }
+    // D: acc[bo][t][r] = z[co = bo*16 + 4q + r][pixel pp + t]
+#pragma unroll
+    for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f4 z = f4{acc[bo][0][r], acc[bo][1][r], acc[bo][2][r], acc[bo][3][r]};
+        *reinterpret_cast<f4*>(a.z + ((size_t)n * a.CoutTotal + a.co_off + bo * 16 + 4 * q + r) * HWo + pp) = z;
+        s1[bo][r] += (z.x + z.y) + (z.z + z.w);
+        s2[bo][r] += (z.x * z.x + z.y * z.y) + (z.z * z.z + z.w * z.w);
+      }
+  }
+  if (!a.stats) return;
+#pragma unroll
+  for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float u = s1[bo][r], w = s2[bo][r];
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {  // over the 16 lanes c16 sharing channel bo*16 + 4q + r
+        u += __shfl_xor(u, o, 64);
+        w += __shfl_xor(w, o, 64);
+      }
+      if (c16 == 0) {
+        atomicAdd(sStat + bo * 16 + 4 * q + r, u);
+        atomicAdd(sStat + CO + bo * 16 + 4 * q + r, w);
+      }
+    }
+  __syncthreads();
+  for (int i = tid; i < 2 * CO; i += 256) {
+    const int hi = i >= CO;
+    atomicAdd(a.stats + rep_slot() * 2 * a.CoutTotal + hi * a.CoutTotal + a.co_off + (i - hi * CO), (double)sStat[i]);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1037,6 +1134,177 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
   for (int i = tid; i < CI * CO; i += 256) atomicAdd(gW + i, sGW[i]);
 }
 
+// orders a wave's LDS writes before its later LDS reads of other lanes' data (LDS executes one
+// wave's instructions in order, so only the compiler has to be kept from reordering them)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ------------------------------------------------------------------------------------------------
+// pw_bwd_wave: pw_bwd for the 16..64-channel layers of darts-gpu.yaml-sized supernets (Cin, Cout
+// multiples of 16). The tiled kernel above stages a 64-pixel tile per workgroup between two
+// barriers and runs its MFMA chains on one wave when Cin = Cout = 16, so each workgroup walks a
+// serial load -> barrier -> compute chain per tile. Here every WAVE owns whole 64-pixel chunks
+// and never waits for the others until the final weight-gradient reduction:
+//   loads   lane (c = lane & 15, q = lane >> 4) reads 16 consecutive pixels q*16 .. q*16+15 of
+//           channel c of every 16-channel block with 16-byte loads: dz (BN backward on the fly)
+//           and the layer input, straight into MFMA operand registers;
+//   dW      v_mfma_f32_16x16x4f32 with K = pixels: step j feeds pixel q*16 + j of lane group q
+//           as k-index q, so the 16 steps cover the chunk with no data movement;
+//   dd      pw^T dz needs dz with channels on the K axis: the wave writes its dz chunk to a
+//           wave-private LDS tile (no workgroup barrier) and reads it back in B-operand order.
+// ------------------------------------------------------------------------------------------------
+template <int CI, int CO>
+__global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
+  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64, "16-channel blocks");
+  constexpr int BO = CO / 16, BI = CI / 16, RS = 64 + 4;  // LDS tile row stride (floats)
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const PwBwdArgs& a = bt.e[blockIdx.y];
+  const int HWo = a.Ho * a.Wo, Wo = a.Wo;
+  const int nchunks = a.N * HWo / 64;  // HWo % 64 == 0 (host-checked)
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // [4 waves][CO][RS]
+  __shared__ float sC[4 * CO + 1];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int c16 = lane & 15, q = lane >> 4;
+  for (int c = tid; c < CO; c += 256) {
+    bn_coeffs(a.gs.bn, a.co_off + c, sC[c], sC[CO + c]);
+    gs_means(a.gs, a.co_off + c, sC[2 * CO + c], sC[3 * CO + c]);
+  }
+  if (tid == 0) sC[4 * CO] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
+  __syncthreads();
+  const float wk = sC[4 * CO];
+  float mean[BO], inv[BO], m1[BO], m2[BO];
+#pragma unroll
+  for (int bo = 0; bo < BO; ++bo) {
+    const int c = bo * 16 + c16;
+    mean[bo] = sC[c];
+    inv[bo] = sC[CO + c];
+    m1[bo] = sC[2 * CO + c];
+    m2[bo] = sC[3 * CO + c];
+  }
+  const bool want_w = a.gW != nullptr;
+  // contiguous input rows: the dw-pw stage, or a stride-1 StdConv whose input plane is the output plane
+  const bool flat = a.mode == 0 || (a.S == 1 && a.off == 0 && a.H == a.Ho && a.W == a.Wo);
+  const float* src = a.mode == 0 ? a.ain : a.x;
+  float* sT = smem + wave * CO * RS;
+  f4 macc[BO][BI];
+#pragma unroll
+  for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+    for (int bi = 0; bi < BI; ++bi) macc[bo][bi] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int ch = blockIdx.x * 4 + wave; ch < nchunks; ch += gridDim.x * 4) {
+    const int pix0 = ch * 64, n = pix0 / HWo, prem = pix0 - n * HWo;
+    const int pq = prem + q * 16;  // this lane's pixels pq .. pq + 15
+    float dz[BO][16];
+#pragma unroll
+    for (int bo = 0; bo < BO; ++bo) {
+      const size_t gi = ((size_t)n * a.CoutTotal + a.co_off + bo * 16 + c16) * HWo + pq;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f4 zz = *reinterpret_cast<const f4*>(a.gs.z + gi + 4 * t);
+        const f4 gg = *reinterpret_cast<const f4*>(a.gs.g + gi + 4 * t);
+        const f4 v = wk * inv[bo] * (gg - m1[bo] - ((zz - mean[bo]) * inv[bo]) * m2[bo]);
+        dz[bo][4 * t] = v.x;
+        dz[bo][4 * t + 1] = v.y;
+        dz[bo][4 * t + 2] = v.z;
+        dz[bo][4 * t + 3] = v.w;
+      }
+    }
+    if (want_w) {
+      float av[BI][16];
+#pragma unroll
+      for (int bi = 0; bi < BI; ++bi) {
+        const int ci = bi * 16 + c16;
+        if (flat) {
+          const float* s = src + ((size_t)n * CI + ci) * HWo + pq;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            f4 v = *reinterpret_cast<const f4*>(s + 4 * t);
+            if (a.mode != 0) v = f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+            av[bi][4 * t] = v.x;
+            av[bi][4 * t + 1] = v.y;
+            av[bi][4 * t + 2] = v.z;
+            av[bi][4 * t + 3] = v.w;
+          }
+        } else {  // FactorizedReduce half: relu(x) at (oy*S + off, ox*S + off)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int pp = pq + j, oy = pp / Wo, ox = pp - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+            av[bi][j] = (iy < a.H && ix < a.W) ? fmaxf(a.x[(((size_t)n * CI + ci) * a.H + iy) * a.W + ix], 0.f) : 0.f;
+          }
+        }
+      }
+      // gW[co][ci] += sum_p dz[co][p] a[ci][p]: A[i = co][k = p], B[k = p][j = ci]
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+#pragma unroll
+        for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+          for (int bi = 0; bi < BI; ++bi)
+            macc[bo][bi] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[bo][j], av[bi][j], macc[bo][bi], 0, 0, 0);
+    }
+    if (!a.need_dx) continue;
+    // dz chunk -> wave-private LDS tile [co][p]
+    wave_lds_sync();  // the previous chunk's tile reads are done
+#pragma unroll
+    for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        *reinterpret_cast<f4*>(sT + (bo * 16 + c16) * RS + q * 16 + 4 * t) =
+            f4{dz[bo][4 * t], dz[bo][4 * t + 1], dz[bo][4 * t + 2], dz[bo][4 * t + 3]};
+    wave_lds_sync();
+    // dd[ci][p] = sum_co pw[co][ci] dz[co][p]: A[i = ci][k = co] = pw[co][ci], B[k = co][j = p]
+#pragma unroll
+    for (int bi = 0; bi < BI; ++bi) {
+      f4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+      for (int k0 = 0; k0 < CO; k0 += 4) {
+        const float av = a.pw[(k0 + q) * CI + bi * 16 + c16];
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb)
+          acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sT[(k0 + q) * RS + pb * 16 + c16], acc[pb], 0, 0, 0);
+      }
+      // D map: row (ci) = bi*16 + q*4 + r, col (pixel) = pb*16 + c16
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ci = bi * 16 + q * 4 + r;
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          const int pp = prem + pb * 16 + c16;
+          const float v = acc[pb][r];
+          if (a.mode == 0) {
+            a.dd[((size_t)n * CI + ci) * HWo + pp] = v;
+          } else {
+            const int oy = pp / Wo, ox = pp - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
+            if (iy < a.H && ix < a.W) {
+              const size_t xi = (((size_t)n * CI + ci) * a.H + iy) * a.W + ix;
+              if (a.overwrite) a.gx[xi] = a.x[xi] > 0.f ? v : 0.f;
+              else if (a.x[xi] > 0.f) a.gx[xi] += v;
+            }
+          }
+        }
+      }
+    }
+  }
+  if (!want_w) return;
+  // the 4 waves' partial 16x16 blocks -> one LDS sum -> one atomic vector per workgroup
+  __syncthreads();
+  float* sG = smem;  // [CO][CI]
+  for (int i = tid; i < CO * CI; i += 256) sG[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int bo = 0; bo < BO; ++bo)
+#pragma unroll
+    for (int bi = 0; bi < BI; ++bi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(sG + (bo * 16 + q * 4 + r) * CI + bi * 16 + c16, macc[bo][bi][r]);
+  __syncthreads();
+  float* gW = a.gW + (size_t)rep_slot() * a.gstride;
+  for (int i = tid; i < CO * CI; i += 256) atomicAdd(gW + i, sG[i]);
+}
+
 // ------------------------------------------------------------------------------------------------
 // dw_bwd: transposed depthwise. For own output rows [oy0, oy0+TR): dW_dw += dd * act(in);
 // for own input rows [oy0*S, (oy0+TR)*S): ga = sum_taps dw * dd, masked by act'(in).
@@ -1270,7 +1538,10 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
   const DwBwdArgs& a = bt.e[blockIdx.y];
   constexpr int KK = K * K, PAD = (K - 1) / 2 * DIL, PO = (PAD + S - 1) / S, SH = S == 2 ? 1 : 0;
   const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
-  const int n = blockIdx.x / nb, band = blockIdx.x - n * nb;
+  // channel groups: depthwise backward never mixes channels, so wider layers run as a.C / C
+  // independent C-channel groups (blockIdx.x = (image * nb + band) * G + group)
+  const int G = a.C / C, grp = blockIdx.x % G, nbx = blockIdx.x / G, c0 = grp * C;
+  const int n = nbx / nb, band = nbx - n * nb;
   const int BRi = H / nb, iy0 = band * BRi, nrow = BRi;
   const int oyA = (iy0 - PAD) >> SH;                 // floor division (S in {1, 2})
   const int oyB = (iy0 + nrow - 1 + PAD) >> SH;
@@ -1283,7 +1554,7 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
   __shared__ float sMean[C], sInv[C], sRed[2 * C], sGW[C * KK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < C) {
-    if (PREBN) bn_coeffs(a.inbn, tid, sMean[tid], sInv[tid]);
+    if (PREBN) bn_coeffs(a.inbn, c0 + tid, sMean[tid], sInv[tid]);
     sRed[tid] = 0.f;
     sRed[C + tid] = 0.f;
   }
@@ -1291,8 +1562,8 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
   __syncthreads();
   // staging with 16-byte loads (the band's rows are contiguous per channel; W, Wo % 4 == 0):
   // many wide loads in flight per wave, which the one-row-per-wave scalar loop lacked
-  const float* ddn = a.dd + (size_t)n * C * Ho * Wo;
-  const float* xn = a.x + (size_t)n * C * H * W;
+  const float* ddn = a.dd + ((size_t)n * a.C + c0) * Ho * Wo;
+  const float* xn = a.x + ((size_t)n * a.C + c0) * H * W;
   const int va = max(oyA, 0), vb = min(oyB, Ho - 1), vrows = vb - va + 1;  // staged dd rows inside [0, Ho)
   {
     const int q4 = vrows * Wo / 4;  // float4s per channel
@@ -1337,7 +1608,7 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
       *reinterpret_cast<float4*>(sIn + c * NP + o) = v;
     }
     if (accum) {
-      const float* gsrc = a.gout + (size_t)n * C * H * W;
+      const float* gsrc = a.gout + ((size_t)n * a.C + c0) * H * W;
 #pragma unroll 4
       for (int i = tid; i < C * q4; i += 256) {
         const int c = i / q4, o = (i - c * q4) * 4;
@@ -1351,7 +1622,7 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
   float st1[C], st2[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) st1[c] = st2[c] = 0.f;
-  float* gn = a.gout + (size_t)n * C * H * W;
+  float* gn = a.gout + ((size_t)n * a.C + c0) * H * W;
   for (int p = tid; p < ((dbg & 1) ? 0 : NP); p += 256) {
     const int r = p / W, ix = p - r * W, iy = iy0 + r;
     int srow[K], scol[K];
@@ -1366,7 +1637,7 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const float* wk = a.dw + c * KK;  // uniform -> scalar loads
+      const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
       const float* dd = sDD + c * ODR * ODW;
       float ga = 0.f;
 #pragma unroll
@@ -1446,9 +1717,10 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
     }
   }
   __syncthreads();
-  if (PREBN && a.red && tid < 2 * C) atomicAdd(a.red + rep_slot() * 2 * C + tid, (double)sRed[tid]);
+  if (PREBN && a.red && tid < 2 * C)  // red replica layout [sum g: a.C | sum g*y: a.C]
+    atomicAdd(a.red + rep_slot() * 2 * a.C + (tid < C ? c0 + tid : a.C + c0 + tid - C), (double)sRed[tid]);
   if (a.gW)
-    for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + (size_t)rep_slot() * a.gstride + i, sGW[i]);
+    for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + (size_t)rep_slot() * a.gstride + c0 * KK + i, sGW[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1474,15 +1746,60 @@ static void launch_dwpw_plane_t(const DwPwFwdBatch& b, bool prebn, hipStream_t s
   }
 }
 
-// row-band kernel for C = 4 / 8 (the staged band fits 64 KB of LDS by construction)
-static bool plane_ok(const DwPwFwdArgs& a) { return a.C == 4 || a.C == 8; }
+// row-band kernel for C = 4 / 8 / 16 (the staged band fits 64 KB of LDS by construction)
+static bool plane_ok(const DwPwFwdArgs& a) { return a.C == 4 || a.C == 8 || a.C == 16; }
+
+template <int CI, int CO>
+static bool try_pw_fwd_wave(const PwFwdBatch& b, hipStream_t st);
+
+// wide layers (C = 32 / 48 / 64; 16 with KATIB_HIP_DWPW_SPLIT=1): depthwise on 16-channel groups
+// (dwpw_plane_kernel<..., PW = false>), then the pointwise + BN statistics as an MFMA GEMM over d
+template <int K, int DIL, int S>
+static bool try_dwpw_split(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
+  const DwPwFwdArgs& a = b.e[0];
+  static const bool split16 = getenv("KATIB_HIP_DWPW_SPLIT") && atoi(getenv("KATIB_HIP_DWPW_SPLIT")) > 0;
+  if (getenv("KATIB_HIP_DWPW_TILED") || a.C % 16 != 0 || a.C > 64 || (a.C == 16 && !split16) ||
+      (a.Ho * a.Wo) % 64 != 0 || a.W % 4 != 0)
+    return false;
+  for (int i = 0; i < b.n; ++i)
+    if (((uintptr_t)b.e[i].x | (uintptr_t)b.e[i].d | (uintptr_t)b.e[i].z) & 15) return false;
+  constexpr int CG = 16;
+  const int G = a.C / CG;
+  int nb = std::max(1, std::min(a.Ho / 4, 2048 / std::max(a.N * b.n * G, 1)));
+  auto band_bytes = [&](int v) {
+    const int BR = (a.Ho + v - 1) / v;
+    return (size_t)CG * ((BR - 1) * S + (K - 1) * DIL + 1) * (a.W + 2 * a.pad) * sizeof(float);
+  };
+  while (band_bytes(nb) > 65536 && nb < a.Ho) ++nb;
+  DwPwFwdBatch db = b;
+  for (int i = 0; i < b.n; ++i) db.e[i].chunk = nb;
+  dim3 grid(a.N * nb * G, b.n);
+  const size_t lds = band_bytes(nb);
+  if (prebn) hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, true, CG, true, false>), grid, dim3(256), lds, st, db);
+  else hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, false, CG, true, false>), grid, dim3(256), lds, st, db);
+  PwFwdBatch pb{};
+  pb.n = b.n;
+  for (int i = 0; i < b.n; ++i) {
+    const DwPwFwdArgs& e = b.e[i];
+    PwFwdArgs& p = pb.e[i];
+    p.x = e.d; p.pw = e.pw; p.z = e.z; p.stats = e.stats;
+    p.N = e.N; p.Cin = e.C; p.Cout = e.C; p.CoutTotal = e.C; p.co_off = 0;
+    p.H = e.Ho; p.W = e.Wo; p.Ho = e.Ho; p.Wo = e.Wo; p.S = 1; p.off = 0; p.relu = 0;
+  }
+  if (try_pw_fwd_wave<16, 16>(pb, st) || try_pw_fwd_wave<32, 32>(pb, st) || try_pw_fwd_wave<64, 64>(pb, st))
+    return true;
+  launch_pw_fwd(pb, st);  // C = 48: the generic dispatch
+  return true;
+}
 
 template <int K, int DIL, int S>
 static void launch_dwpw_fwd_t(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
   const DwPwFwdArgs& a = b.e[0];
+  if (try_dwpw_split<K, DIL, S>(b, prebn, st)) return;
   if (plane_ok(a)) {
     if (a.C == 4) return launch_dwpw_plane_t<K, DIL, S, 4>(b, prebn, st);
-    return launch_dwpw_plane_t<K, DIL, S, 8>(b, prebn, st);
+    if (a.C == 8) return launch_dwpw_plane_t<K, DIL, S, 8>(b, prebn, st);
+    return launch_dwpw_plane_t<K, DIL, S, 16>(b, prebn, st);
   }
   const int TR = 64 / a.Wo;
   const int IR = (TR - 1) * S + (K - 1) * DIL + 1;
@@ -1502,11 +1819,11 @@ void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, h
 }
 
 // LDS floats of one dw_bwd_plane band (nb bands per image)
-static size_t dw_plane_floats(const DwBwdArgs& a, int K, int DIL, int S, int nb, bool accum) {
+static size_t dw_plane_floats(const DwBwdArgs& a, int K, int DIL, int S, int nb, bool accum, int C) {
   const int PAD = (K - 1) / 2 * DIL, PO = (PAD + S - 1) / S, sh = S == 2 ? 1 : 0, BRi = a.H / nb;
   auto fdiv = [sh](int v) { return v >= 0 ? v >> sh : -((-v + (1 << sh) - 1) >> sh); };
   const int ODR = fdiv(BRi - 1 + PAD) - fdiv(-PAD) + 2;  // +1: odd bands start at odd rows
-  return (size_t)a.C * ODR * (a.Wo + 2 * PO) + (size_t)a.C * BRi * a.W * (accum ? 2 : 1);
+  return (size_t)C * ODR * (a.Wo + 2 * PO) + (size_t)C * BRi * a.W * (accum ? 2 : 1);
 }
 
 template <int K, int DIL, int S, int C>
@@ -1517,11 +1834,12 @@ static void launch_dw_bwd_plane_t(const DwBwdBatch& b, bool prebn, hipStream_t s
   // bands: as few as possible (less halo) while the launch still has ~4 workgroups per CU and a
   // band stays within 40 KB of LDS
   int nb = 1;
+  const int G = a.C / C;  // channel groups per image
   while (nb < 8 && a.H % (2 * nb) == 0 &&
-         (dw_plane_floats(a, K, DIL, S, nb, accum) * 4 > 40 * 1024 || a.N * nb * b.n < 1024))
+         (dw_plane_floats(a, K, DIL, S, nb, accum, C) * 4 > 40 * 1024 || a.N * nb * G * b.n < 1024))
     nb *= 2;
-  const size_t lds = sizeof(float) * dw_plane_floats(a, K, DIL, S, nb, accum);
-  dim3 grid(a.N * nb, b.n);
+  const size_t lds = sizeof(float) * dw_plane_floats(a, K, DIL, S, nb, accum, C);
+  dim3 grid(a.N * nb * G, b.n);
   static const int dbg = getenv("KATIB_HIP_DWB_DBG") ? atoi(getenv("KATIB_HIP_DWB_DBG")) : 0;  // timing probes
   if (prebn) hipLaunchKernelGGL((dw_bwd_plane_kernel<K, DIL, S, true, C>), grid, dim3(256), lds, st, b, nb, dbg);
   else hipLaunchKernelGGL((dw_bwd_plane_kernel<K, DIL, S, false, C>), grid, dim3(256), lds, st, b, nb, dbg);
@@ -1537,7 +1855,7 @@ static bool aligned16(const DwBwdBatch& b) {
 static bool dw_plane_ok(const DwBwdBatch& b, int K, int DIL, int S) {
   if (getenv("KATIB_HIP_DW_BWD_TILED")) return false;
   const DwBwdArgs& a = b.e[0];
-  return (a.C == 4 || a.C == 8 || a.C == 16) && a.H == a.Ho * S && a.W == a.Wo * S &&
+  return (a.C == 4 || a.C == 8 || (a.C % 16 == 0 && a.C <= kMaxC)) && a.H == a.Ho * S && a.W == a.Wo * S &&
          a.pad == (K - 1) / 2 * DIL && a.Wo % 4 == 0 && aligned16(b);
 }
 
@@ -1567,8 +1885,27 @@ void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipSt
 #undef DISPATCH
 }
 
+template <int CI, int CO>
+static bool try_pw_fwd_wave(const PwFwdBatch& b, hipStream_t st) {
+  const PwFwdArgs& a = b.e[0];
+  if (a.Cin != CI || a.Cout != CO || (a.Ho * a.Wo) % 64 != 0 || getenv("KATIB_HIP_PW_FWD_TILED")) return false;
+  for (int e = 0; e < b.n; ++e) {  // 16-byte loads (flat input) and stores
+    const PwFwdArgs& x = b.e[e];
+    const bool flat = !x.relu || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);
+    if ((((uintptr_t)x.z) | (flat ? (uintptr_t)x.x : 0)) & 15) return false;
+  }
+  const int waves = a.N * a.Ho * a.Wo / 64;
+  const int per_edge = std::max(1, std::min((waves + 3) / 4, max_blocks() / std::max(b.n, 1)));
+  hipLaunchKernelGGL((pw_fwd_wave_kernel<CI, CO>), dim3(per_edge, b.n), dim3(256), 0, st, b);
+  return true;
+}
+
 void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st) {
   const PwFwdArgs& a = b.e[0];
+  if (try_pw_fwd_wave<48, 16>(b, st) || try_pw_fwd_wave<48, 32>(b, st) || try_pw_fwd_wave<64, 32>(b, st) ||
+      try_pw_fwd_wave<32, 16>(b, st) || try_pw_fwd_wave<16, 16>(b, st) || try_pw_fwd_wave<32, 32>(b, st) ||
+      try_pw_fwd_wave<64, 64>(b, st))
+    return;
   size_t lds = sizeof(float) * (a.Cin * 64 + 2 * a.Cout);
   dim3 grid(per_edge_blocks(a.N * a.Ho * a.Wo / 64, b.n), b.n);
   hipLaunchKernelGGL(pw_fwd_kernel, grid, dim3(256), lds, st, b);
@@ -1641,12 +1978,34 @@ static bool try_pw_bwd_px(const PwBwdBatch& b, hipStream_t st) {
   return true;
 }
 
+template <int CI, int CO>
+static bool try_pw_bwd_wave(const PwBwdBatch& b, hipStream_t st) {
+  const PwBwdArgs& a = b.e[0];
+  if (a.Cin != CI || a.Cout != CO || (a.Ho * a.Wo) % 64 != 0 || getenv("KATIB_HIP_PW_BWD_TILED")) return false;
+  for (int e = 0; e < b.n; ++e) {  // 16-byte operand loads
+    const PwBwdArgs& x = b.e[e];
+    const bool flat = x.mode == 0 || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);
+    const uintptr_t bits = (uintptr_t)x.gs.z | (uintptr_t)x.gs.g | (uintptr_t)(flat ? (x.mode == 0 ? x.ain : x.x) : nullptr);
+    if (bits & 15) return false;
+  }
+  const int waves = a.N * a.Ho * a.Wo / 64;
+  const int per_edge = std::max(1, std::min((waves + 3) / 4, max_blocks() / std::max(b.n, 1)));
+  const size_t lds = sizeof(float) * 4 * CO * (64 + 4);
+  hipLaunchKernelGGL((pw_bwd_wave_kernel<CI, CO>), dim3(per_edge, b.n), dim3(256), lds, st, b);
+  return true;
+}
+
 void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st) {
   const PwBwdArgs& a = b.e[0];
   // narrow layers: pixel-per-thread kernel (see pw_bwd_px_kernel)
   if (try_pw_bwd_px<4, 4>(b, st) || try_pw_bwd_px<8, 8>(b, st) || try_pw_bwd_px<4, 8>(b, st) ||
       try_pw_bwd_px<8, 4>(b, st) || try_pw_bwd_px<12, 8>(b, st) || try_pw_bwd_px<2, 2>(b, st) ||
       try_pw_bwd_px<4, 2>(b, st) || try_pw_bwd_px<2, 4>(b, st))
+    return;
+  // 16..64-channel layers: wave-per-chunk MFMA kernel (see pw_bwd_wave_kernel)
+  if (try_pw_bwd_wave<16, 16>(b, st) || try_pw_bwd_wave<32, 32>(b, st) || try_pw_bwd_wave<64, 64>(b, st) ||
+      try_pw_bwd_wave<48, 16>(b, st) || try_pw_bwd_wave<48, 32>(b, st) || try_pw_bwd_wave<64, 32>(b, st) ||
+      try_pw_bwd_wave<32, 16>(b, st))
     return;
   int ntiles = a.N * a.Ho * a.Wo / 64;
   dim3 grid(per_edge_blocks(ntiles, b.n), b.n);
