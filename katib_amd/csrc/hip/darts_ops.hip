@@ -423,11 +423,14 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
 //                     load; MFMA t in 0..3 takes pixel 4*j + t as column j, so the D fragment a lane
 //                     holds for (co, t = 0..3) is 4 consecutive pixels: one 16-byte store.
 // Statistics stay per lane across chunks and are reduced once per workgroup at the end.
+// NS > 1 (small planes, too few chunks to fill the chip): work item = (chunk, output-block group
+// of CO / NS channels); the grid stride is a multiple of NS, so a wave keeps one group (and its
+// weights and statistics) for all its items.
 // ------------------------------------------------------------------------------------------------
-template <int CI, int CO>
+template <int CI, int CO, int NS = 1>
 __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
-  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64, "16-channel blocks");
-  constexpr int BO = CO / 16, KS = CI / 4;
+  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64 && (CO / 16) % NS == 0, "16-channel blocks");
+  constexpr int BO = CO / 16 / NS, KS = CI / 4;
   typedef float f4 __attribute__((ext_vector_type(4)));
   const PwFwdArgs& a = bt.e[blockIdx.y];
   const int HWo = a.Ho * a.Wo, Wo = a.Wo;
@@ -436,17 +439,18 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, c16 = lane & 15, q = lane >> 4;
   for (int i = tid; i < 2 * CO; i += 256) sStat[i] = 0.f;
   __syncthreads();
+  const int grp = (blockIdx.x * 4 + wave) % NS, cb0 = grp * BO * 16;  // first output channel of the group
   float wA[BO][KS];
 #pragma unroll
   for (int bo = 0; bo < BO; ++bo)
 #pragma unroll
-    for (int k = 0; k < KS; ++k) wA[bo][k] = a.pw[(bo * 16 + c16) * CI + 4 * k + q];
+    for (int k = 0; k < KS; ++k) wA[bo][k] = a.pw[(cb0 + bo * 16 + c16) * CI + 4 * k + q];
   const bool flat = !a.relu || (a.S == 1 && a.off == 0 && a.H == a.Ho && a.W == a.Wo);
   f4 s1[BO], s2[BO];  // per-lane partial sums of z, z^2 for channels bo*16 + 4q + r
 #pragma unroll
   for (int bo = 0; bo < BO; ++bo) s1[bo] = s2[bo] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int ch = blockIdx.x * 4 + wave; ch < nchunks; ch += gridDim.x * 4) {
-    const int pix0 = ch * 64, n = pix0 / HWo, prem = pix0 - n * HWo;
+  for (int w = blockIdx.x * 4 + wave; w < nchunks * NS; w += gridDim.x * 4) {
+    const int pix0 = (w / NS) * 64, n = pix0 / HWo, prem = pix0 - n * HWo;
     const int pp = prem + 4 * c16;  // this lane's 4 pixels
     f4 acc[BO][4];
 #pragma unroll
@@ -478,7 +482,7 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const f4 z = f4{acc[bo][0][r], acc[bo][1][r], acc[bo][2][r], acc[bo][3][r]};
-        *reinterpret_cast<f4*>(a.z + ((size_t)n * a.CoutTotal + a.co_off + bo * 16 + 4 * q + r) * HWo + pp) = z;
+        *reinterpret_cast<f4*>(a.z + ((size_t)n * a.CoutTotal + a.co_off + cb0 + bo * 16 + 4 * q + r) * HWo + pp) = z;
         s1[bo][r] += (z.x + z.y) + (z.z + z.w);
         s2[bo][r] += (z.x * z.x + z.y * z.y) + (z.z * z.z + z.w * z.w);
       }
@@ -495,8 +499,8 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
         w += __shfl_xor(w, o, 64);
       }
       if (c16 == 0) {
-        atomicAdd(sStat + bo * 16 + 4 * q + r, u);
-        atomicAdd(sStat + CO + bo * 16 + 4 * q + r, w);
+        atomicAdd(sStat + cb0 + bo * 16 + 4 * q + r, u);
+        atomicAdd(sStat + CO + cb0 + bo * 16 + 4 * q + r, w);
       }
     }
   __syncthreads();
@@ -1156,10 +1160,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   dd      pw^T dz needs dz with channels on the K axis: the wave writes its dz chunk to a
 //           wave-private LDS tile (no workgroup barrier) and reads it back in B-operand order.
 // ------------------------------------------------------------------------------------------------
-template <int CI, int CO>
+// NS > 1 (small planes): work item = (chunk, group of CI / NS input channels): the wave forms dz for
+// every output channel but the weight gradients and dd of its input-channel group only.
+template <int CI, int CO, int NS = 1>
 __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
-  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64, "16-channel blocks");
-  constexpr int BO = CO / 16, BI = CI / 16, RS = 64 + 4;  // LDS tile row stride (floats)
+  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64 && (CI / 16) % NS == 0, "16-channel blocks");
+  constexpr int BO = CO / 16, BI = CI / 16 / NS, RS = 64 + 4;  // LDS tile row stride (floats)
   typedef float f4 __attribute__((ext_vector_type(4)));
   const PwBwdArgs& a = bt.e[blockIdx.y];
   const int HWo = a.Ho * a.Wo, Wo = a.Wo;
@@ -1189,13 +1195,14 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
   const bool flat = a.mode == 0 || (a.S == 1 && a.off == 0 && a.H == a.Ho && a.W == a.Wo);
   const float* src = a.mode == 0 ? a.ain : a.x;
   float* sT = smem + wave * CO * RS;
+  const int ci0 = ((blockIdx.x * 4 + wave) % NS) * BI * 16;  // the wave's input-channel group (fixed: stride % NS == 0)
   f4 macc[BO][BI];
 #pragma unroll
   for (int bo = 0; bo < BO; ++bo)
 #pragma unroll
     for (int bi = 0; bi < BI; ++bi) macc[bo][bi] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int ch = blockIdx.x * 4 + wave; ch < nchunks; ch += gridDim.x * 4) {
-    const int pix0 = ch * 64, n = pix0 / HWo, prem = pix0 - n * HWo;
+  for (int w = blockIdx.x * 4 + wave; w < nchunks * NS; w += gridDim.x * 4) {
+    const int pix0 = (w / NS) * 64, n = pix0 / HWo, prem = pix0 - n * HWo;
     const int pq = prem + q * 16;  // this lane's pixels pq .. pq + 15
     float dz[BO][16];
 #pragma unroll
@@ -1216,7 +1223,7 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
       float av[BI][16];
 #pragma unroll
       for (int bi = 0; bi < BI; ++bi) {
-        const int ci = bi * 16 + c16;
+        const int ci = ci0 + bi * 16 + c16;
         if (flat) {
           const float* s = src + ((size_t)n * CI + ci) * HWo + pq;
 #pragma unroll
@@ -1261,7 +1268,7 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
       f4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
       for (int k0 = 0; k0 < CO; k0 += 4) {
-        const float av = a.pw[(k0 + q) * CI + bi * 16 + c16];
+        const float av = a.pw[(k0 + q) * CI + ci0 + bi * 16 + c16];
 #pragma unroll
         for (int pb = 0; pb < 4; ++pb)
           acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sT[(k0 + q) * RS + pb * 16 + c16], acc[pb], 0, 0, 0);
@@ -1269,7 +1276,7 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
       // D map: row (ci) = bi*16 + q*4 + r, col (pixel) = pb*16 + c16
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ci = bi * 16 + q * 4 + r;
+        const int ci = ci0 + bi * 16 + q * 4 + r;
 #pragma unroll
         for (int pb = 0; pb < 4; ++pb) {
           const int pp = prem + pb * 16 + c16;
@@ -1299,7 +1306,7 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
 #pragma unroll
     for (int bi = 0; bi < BI; ++bi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(sG + (bo * 16 + q * 4 + r) * CI + bi * 16 + c16, macc[bo][bi][r]);
+      for (int r = 0; r < 4; ++r) atomicAdd(sG + (bo * 16 + q * 4 + r) * CI + ci0 + bi * 16 + c16, macc[bo][bi][r]);
   __syncthreads();
   float* gW = a.gW + (size_t)rep_slot() * a.gstride;
   for (int i = tid; i < CO * CI; i += 256) atomicAdd(gW + i, sG[i]);
@@ -1752,18 +1759,31 @@ static bool plane_ok(const DwPwFwdArgs& a) { return a.C == 4 || a.C == 8 || a.C 
 template <int CI, int CO>
 static bool try_pw_fwd_wave(const PwFwdBatch& b, hipStream_t st);
 
-// wide layers (C = 32 / 48 / 64; 16 with KATIB_HIP_DWPW_SPLIT=1): depthwise on 16-channel groups
-// (dwpw_plane_kernel<..., PW = false>), then the pointwise + BN statistics as an MFMA GEMM over d
+template <int K, int DIL, int S, int CG>
+static bool try_dwpw_split_g(const DwPwFwdBatch& b, bool prebn, hipStream_t st, bool split16);
+
+// layers of 16..64 channels: depthwise on channel groups (dwpw_plane_kernel<..., PW = false>), then
+// the pointwise + BN statistics as an MFMA GEMM over d (pw_fwd_wave_kernel). At C = 16 this measured
+// faster than the fused plane kernel (50.7 vs 52.5 ms per darts-gpu.yaml step); KATIB_HIP_DWPW_SPLIT=0
+// keeps the fused kernel there.
 template <int K, int DIL, int S>
 static bool try_dwpw_split(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
   const DwPwFwdArgs& a = b.e[0];
-  static const bool split16 = getenv("KATIB_HIP_DWPW_SPLIT") && atoi(getenv("KATIB_HIP_DWPW_SPLIT")) > 0;
+  static const bool split16 = !getenv("KATIB_HIP_DWPW_SPLIT") || atoi(getenv("KATIB_HIP_DWPW_SPLIT")) > 0;
+  static const int grp = getenv("KATIB_HIP_DW_GROUP") ? atoi(getenv("KATIB_HIP_DW_GROUP")) : 8;
+  if (grp == 4) return try_dwpw_split_g<K, DIL, S, 4>(b, prebn, st, split16);
+  if (grp == 8) return try_dwpw_split_g<K, DIL, S, 8>(b, prebn, st, split16);
+  return try_dwpw_split_g<K, DIL, S, 16>(b, prebn, st, split16);
+}
+
+template <int K, int DIL, int S, int CG>
+static bool try_dwpw_split_g(const DwPwFwdBatch& b, bool prebn, hipStream_t st, bool split16) {
+  const DwPwFwdArgs& a = b.e[0];
   if (getenv("KATIB_HIP_DWPW_TILED") || a.C % 16 != 0 || a.C > 64 || (a.C == 16 && !split16) ||
       (a.Ho * a.Wo) % 64 != 0 || a.W % 4 != 0)
     return false;
   for (int i = 0; i < b.n; ++i)
     if (((uintptr_t)b.e[i].x | (uintptr_t)b.e[i].d | (uintptr_t)b.e[i].z) & 15) return false;
-  constexpr int CG = 16;
   const int G = a.C / CG;
   int nb = std::max(1, std::min(a.Ho / 4, 2048 / std::max(a.N * b.n * G, 1)));
   auto band_bytes = [&](int v) {
@@ -1863,8 +1883,11 @@ template <int K, int DIL, int S>
 static void launch_dw_bwd_t(const DwBwdBatch& b, bool prebn, hipStream_t st) {
   const DwBwdArgs& a = b.e[0];
   if (dw_plane_ok(b, K, DIL, S)) {
-    if (a.C == 4) return launch_dw_bwd_plane_t<K, DIL, S, 4>(b, prebn, st);
-    if (a.C == 8) return launch_dw_bwd_plane_t<K, DIL, S, 8>(b, prebn, st);
+    // wide layers run in channel groups of KATIB_HIP_DWB_GROUP (4, 8 or 16) channels: 8 measured
+    // 48.2 vs 50.8 ms per darts-gpu.yaml step against 16 (half the LDS per band: fewer, taller bands)
+    static const int grp = getenv("KATIB_HIP_DWB_GROUP") ? atoi(getenv("KATIB_HIP_DWB_GROUP")) : 8;
+    if (a.C == 4 || grp == 4) return launch_dw_bwd_plane_t<K, DIL, S, 4>(b, prebn, st);
+    if (a.C == 8 || grp == 8) return launch_dw_bwd_plane_t<K, DIL, S, 8>(b, prebn, st);
     return launch_dw_bwd_plane_t<K, DIL, S, 16>(b, prebn, st);
   }
   const int TR = 64 / a.Wo;
@@ -1888,15 +1911,24 @@ void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipSt
 template <int CI, int CO>
 static bool try_pw_fwd_wave(const PwFwdBatch& b, hipStream_t st) {
   const PwFwdArgs& a = b.e[0];
+  constexpr int BO = CO / 16;
   if (a.Cin != CI || a.Cout != CO || (a.Ho * a.Wo) % 64 != 0 || getenv("KATIB_HIP_PW_FWD_TILED")) return false;
   for (int e = 0; e < b.n; ++e) {  // 16-byte loads (flat input) and stores
     const PwFwdArgs& x = b.e[e];
     const bool flat = !x.relu || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);
     if ((((uintptr_t)x.z) | (flat ? (uintptr_t)x.x : 0)) & 15) return false;
   }
-  const int waves = a.N * a.Ho * a.Wo / 64;
-  const int per_edge = std::max(1, std::min((waves + 3) / 4, max_blocks() / std::max(b.n, 1)));
-  hipLaunchKernelGGL((pw_fwd_wave_kernel<CI, CO>), dim3(per_edge, b.n), dim3(256), 0, st, b);
+  const int chunks = a.N * a.Ho * a.Wo / 64;
+  // split the output channels over waves while the launch has fewer than ~4 waves per SIMD
+  int ns = 1;
+  while (BO % (2 * ns) == 0 && chunks * ns * b.n < 4096) ns *= 2;
+  const int per_edge = std::max(1, std::min((chunks * ns + 3) / 4, max_blocks() / std::max(b.n, 1)));
+  const dim3 grid(per_edge, b.n);
+  if (ns == 1) hipLaunchKernelGGL((pw_fwd_wave_kernel<CI, CO, 1>), grid, dim3(256), 0, st, b);
+  else if constexpr (BO % 2 == 0) {
+    if (ns == 2) hipLaunchKernelGGL((pw_fwd_wave_kernel<CI, CO, 2>), grid, dim3(256), 0, st, b);
+    else if constexpr (BO % 4 == 0) hipLaunchKernelGGL((pw_fwd_wave_kernel<CI, CO, 4>), grid, dim3(256), 0, st, b);
+  }
   return true;
 }
 
@@ -1988,10 +2020,19 @@ static bool try_pw_bwd_wave(const PwBwdBatch& b, hipStream_t st) {
     const uintptr_t bits = (uintptr_t)x.gs.z | (uintptr_t)x.gs.g | (uintptr_t)(flat ? (x.mode == 0 ? x.ain : x.x) : nullptr);
     if (bits & 15) return false;
   }
-  const int waves = a.N * a.Ho * a.Wo / 64;
-  const int per_edge = std::max(1, std::min((waves + 3) / 4, max_blocks() / std::max(b.n, 1)));
+  constexpr int BI = CI / 16;
+  const int chunks = a.N * a.Ho * a.Wo / 64;
+  // split the input channels over waves while the launch has fewer than ~4 waves per SIMD
+  int ns = 1;
+  while (BI % (2 * ns) == 0 && chunks * ns * b.n < 4096) ns *= 2;
+  const int per_edge = std::max(1, std::min((chunks * ns + 3) / 4, max_blocks() / std::max(b.n, 1)));
   const size_t lds = sizeof(float) * 4 * CO * (64 + 4);
-  hipLaunchKernelGGL((pw_bwd_wave_kernel<CI, CO>), dim3(per_edge, b.n), dim3(256), lds, st, b);
+  const dim3 grid(per_edge, b.n);
+  if (ns == 1) hipLaunchKernelGGL((pw_bwd_wave_kernel<CI, CO, 1>), grid, dim3(256), lds, st, b);
+  else if constexpr (BI % 2 == 0) {
+    if (ns == 2) hipLaunchKernelGGL((pw_bwd_wave_kernel<CI, CO, 2>), grid, dim3(256), lds, st, b);
+    else if constexpr (BI % 4 == 0) hipLaunchKernelGGL((pw_bwd_wave_kernel<CI, CO, 4>), grid, dim3(256), lds, st, b);
+  }
   return true;
 }
 

@@ -10,6 +10,12 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_darts.py -x -q --timeout 12
   -p no:cacheprovider >> $L 2>&1 || exit $?
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 >> $L 2>&1 || exit $?
 timeout -k 10 300 python bench.py --config default --steps 10 --warmup 3 >> $L 2>&1 || exit $?
+# A/B: the default config under experiment switches, ';'-separated (e.g. "KATIB_HIP_DWB_GROUP=8;KATIB_HIP_DW_GROUP=8")
+IFS=';' read -ra EXPS <<< "${DARTS_EXP_ENV:-}"
+for e in "${EXPS[@]}"; do
+  echo "exp: $e" >> $L
+  timeout -k 10 300 env $e python bench.py --config default --steps 10 --warmup 3 >> $L 2>&1 || exit $?
+done
 rm -rf gpurun_out/prof_darts_default
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_darts_default -o run -- \
   python3 bench.py --config default --steps 5 --warmup 2 >> $L 2>&1 || exit 1
