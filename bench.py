@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--capture", type=int, default=1)
     ap.add_argument("--ops", default=os.environ.get("KATIB_AMD_DARTS_OPS", "hip"))
     ap.add_argument("--valid-batches", type=int, default=10)
+    ap.add_argument("--full-search", type=int, default=-1,
+                    help="also run the whole search (epochs x (steps/epoch train steps + validation)) and report "
+                         "its measured wall clock next to the projection (-1: on for the b5 config)")
     args = ap.parse_args()
 
     import torch
@@ -117,6 +120,25 @@ def main():
     steps_per_epoch = math.ceil((n_train // 2) / (bs * comm.world_size))
     epoch_s = steps_per_epoch * ms_step / 1000.0 + steps_per_epoch * ms_valid / 1000.0
     wall = cfg["epochs"] * epoch_s
+
+    # cross-check of the projection: the whole search, end to end (train steps + per-epoch validation)
+    full_s = None
+    if args.full_search > 0 or (args.full_search < 0 and args.config == "b5"):
+        sync()
+        comm.barrier()
+        sync()
+        t2 = time.perf_counter()
+        for _ in range(cfg["epochs"]):
+            for i in range(steps_per_epoch):
+                (tx, ty), (vx, vy) = batches[i % len(batches)]
+                search.step(tx, ty, vx, vy)
+            for i in range(steps_per_epoch):
+                vx, vy = vbatches[i % len(vbatches)]
+                search.evaluate(vx, vy)
+        sync()
+        comm.barrier()
+        sync()
+        full_s = comm.allreduce_max(time.perf_counter() - t2)
     if comm.rank == 0:
         out = {
             "metric": "darts_cifar10_search_wall_clock_s",
@@ -140,6 +162,7 @@ def main():
                        "allreduce": ("xgmi-oneshot" if comm.xgmi is not None else "rccl") if comm.distributed else None,
                        "second_order": True},
             "ms_valid_batch": round(ms_valid, 4),
+            "measured_search_wall_s": round(full_s, 3) if full_s is not None else None,
             "train_images_per_s": round(bs * comm.world_size * 1000.0 / ms_step, 1),
             "final_loss": round(loss, 4),
             "baseline_b5_s": B5_SECONDS,

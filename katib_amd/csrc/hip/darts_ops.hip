@@ -427,6 +427,16 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
 // of CO / NS channels); the grid stride is a multiple of NS, so a wave keeps one group (and its
 // weights and statistics) for all its items.
 // ------------------------------------------------------------------------------------------------
+// relu(x) at output pixels p, p + 1 of a stride-2 FactorizedReduce half (input (2oy + off, 2ox + off)):
+// one 16-byte load of x[2oy + off][2ox .. 2ox + 3] holds both (p even and its row inside the plane,
+// H = 2 Ho, W = 2 Wo, W % 4 == 0, x 16-byte aligned: the kernels check this as `fr2`)
+__device__ __forceinline__ void fr2_pair(const float* plane, int W, int Wo, int off, int p, float& v0, float& v1) {
+  const int oy = p / Wo, ox = p - oy * Wo;
+  const float4 v = *reinterpret_cast<const float4*>(plane + (size_t)(2 * oy + off) * W + 2 * ox);
+  v0 = fmaxf(off ? v.y : v.x, 0.f);
+  v1 = fmaxf(off ? v.w : v.z, 0.f);
+}
+
 template <int CI, int CO, int NS = 1>
 __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
   static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64 && (CO / 16) % NS == 0, "16-channel blocks");
@@ -446,6 +456,8 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
 #pragma unroll
     for (int k = 0; k < KS; ++k) wA[bo][k] = a.pw[(cb0 + bo * 16 + c16) * CI + 4 * k + q];
   const bool flat = !a.relu || (a.S == 1 && a.off == 0 && a.H == a.Ho && a.W == a.Wo);
+  const bool fr2 = a.S == 2 && a.H == 2 * a.Ho && a.W == 2 * a.Wo && a.W % 4 == 0 && a.off <= 1 &&
+                   ((uintptr_t)a.x & 15) == 0;
   f4 s1[BO], s2[BO];  // per-lane partial sums of z, z^2 for channels bo*16 + 4q + r
 #pragma unroll
   for (int bo = 0; bo < BO; ++bo) s1[bo] = s2[bo] = f4{0.f, 0.f, 0.f, 0.f};
@@ -464,6 +476,12 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
       if (flat) {
         v = *reinterpret_cast<const f4*>(a.x + ((size_t)n * CI + ci) * HWo + pp);
         if (a.relu) v = f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+      } else if (fr2) {
+        const float* plane = a.x + ((size_t)n * CI + ci) * a.H * a.W;
+        float v0, v1, v2, v3;
+        fr2_pair(plane, a.W, Wo, a.off, pp, v0, v1);
+        fr2_pair(plane, a.W, Wo, a.off, pp + 2, v2, v3);
+        v = f4{v0, v1, v2, v3};
       } else {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -1193,6 +1211,8 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
   const bool want_w = a.gW != nullptr;
   // contiguous input rows: the dw-pw stage, or a stride-1 StdConv whose input plane is the output plane
   const bool flat = a.mode == 0 || (a.S == 1 && a.off == 0 && a.H == a.Ho && a.W == a.Wo);
+  const bool fr2 = a.mode != 0 && a.S == 2 && a.H == 2 * a.Ho && a.W == 2 * a.Wo && a.W % 4 == 0 && a.off <= 1 &&
+                   ((uintptr_t)a.x & 15) == 0;
   const float* src = a.mode == 0 ? a.ain : a.x;
   float* sT = smem + wave * CO * RS;
   const int ci0 = ((blockIdx.x * 4 + wave) % NS) * BI * 16;  // the wave's input-channel group (fixed: stride % NS == 0)
@@ -1235,6 +1255,10 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
             av[bi][4 * t + 2] = v.z;
             av[bi][4 * t + 3] = v.w;
           }
+        } else if (fr2) {
+          const float* plane = a.x + ((size_t)n * CI + ci) * a.H * a.W;
+#pragma unroll
+          for (int j = 0; j < 16; j += 2) fr2_pair(plane, a.W, Wo, a.off, pq + j, av[bi][j], av[bi][j + 1]);
         } else {  // FactorizedReduce half: relu(x) at (oy*S + off, ox*S + off)
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
