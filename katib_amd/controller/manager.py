@@ -41,11 +41,12 @@ from ..api.models import (V1beta1AlgorithmSetting, V1beta1EarlyStoppingRule, V1b
                           V1beta1ParameterAssignment, V1beta1Suggestion, V1beta1SuggestionSpec,
                           V1beta1SuggestionStatus, V1beta1Trial, V1beta1TrialAssignment, V1beta1TrialSpec,
                           V1beta1TrialStatus, V1ObjectMeta, now)
-from ..api.validation import ValidationError, is_restartable, validate_experiment
+from ..api.validation import ValidationError, validate_experiment
 from ..rpc import api_pb2 as api
 from ..utils.prometheus import Registry
 from ..utils.tracing import Tracer
 from . import gjson
+from . import status_engine as SE
 from .config import KatibConfig
 from .converters import comparison_from_pb, convert_experiment, convert_trials
 from .jobs import JobSpecError, LaunchPlan, job_status, make_plan, map_paths, path_mapping
@@ -369,13 +370,14 @@ class Manager:
         if EC.is_completed(exp):
             if exp.spec.resume_policy in (C.RESUME_NEVER, C.RESUME_FROM_VOLUME):
                 self._cleanup_suggestion(exp)
-            trials = exp.status.trials or 0
-            if (is_restartable(exp) and exp.spec.max_trial_count is not None and exp.spec.max_trial_count > trials) \
-                    or (exp.spec.max_trial_count is None and trials != 0 and is_restartable(exp)):
+            action = SE.plan_restart(EC.is_completed_reason(exp, C.EXPERIMENT_MAX_TRIALS_REACHED_REASON),
+                                     exp.spec.resume_policy, exp.spec.max_trial_count, exp.status.trials or 0,
+                                     EC.has_running_trials(exp))
+            if action == "restart":
                 EC.mark_restarting(exp, C.EXPERIMENT_RESTARTING_REASON, "Experiment is restarted")
                 if exp.spec.resume_policy == C.RESUME_FROM_VOLUME:
                     self._restart_suggestion(exp)
-            elif not EC.has_running_trials(exp):
+            elif action == "none":
                 return
         if not EC.is_created(exp):
             if exp.status.start_time is None:
@@ -398,68 +400,16 @@ class Manager:
             self._reconcile_trials(key, exp, trials)
 
     def _objective_value(self, trial) -> str:
-        """getObjectiveMetricValue (status_util.go:151-183)."""
-        obs = trial.status.observation if trial.status else None
-        if obs is None:
-            return C.UNAVAILABLE_METRIC_VALUE
-        name = trial.spec.objective.objective_metric_name
-        strat = None
-        for s in trial.spec.objective.metric_strategies or []:
-            if s.name == name:
-                strat = s.value
-                break
-        for m in obs.metrics or []:
-            if m.name == name:
-                if strat == C.STRATEGY_MIN:
-                    return m.latest if m.min == C.UNAVAILABLE_METRIC_VALUE else m.min
-                if strat == C.STRATEGY_MAX:
-                    return m.latest if m.max == C.UNAVAILABLE_METRIC_VALUE else m.max
-                if strat == C.STRATEGY_LATEST:
-                    return m.latest
-        return C.UNAVAILABLE_METRIC_VALUE
+        """getObjectiveMetricValue (status_util.go:151-183), native status engine."""
+        return SE.objective_value(trial)
 
     def _update_trials_summary(self, exp, trials) -> bool:
-        """updateTrialsSummary (status_util.go:57-148)."""
+        """updateTrialsSummary (status_util.go:57-148): bucketing, optimal trial and goal
+        are decided by the native status engine (csrc/native/status_engine.cpp)."""
         st = exp.status
-        lists = {k: [] for k in ("killed", "failed", "succeeded", "early", "running", "mu", "pending")}
-        best_idx, best_val, goal_reached = -1, None, False
         obj = exp.spec.objective
-        for i, t in enumerate(trials):
-            n = t.metadata.name
-            if TC.is_killed(t):
-                lists["killed"].append(n)
-            elif TC.is_failed(t):
-                lists["failed"].append(n)
-            elif TC.is_succeeded(t):
-                lists["succeeded"].append(n)
-            elif TC.is_early_stopped(t):
-                lists["early"].append(n)
-            elif TC.is_running(t):
-                lists["running"].append(n)
-            elif TC.is_metrics_unavailable(t):
-                lists["mu"].append(n)
-            else:
-                lists["pending"].append(n)
-            sval = self._objective_value(t)
-            if sval == C.UNAVAILABLE_METRIC_VALUE:
-                continue
-            try:
-                v = float(sval)
-            except ValueError:
-                best_idx = i  # string metric: latest trial is best
-                continue
-            if best_idx == -1 or best_val is None:
-                best_val, best_idx = v, i
-            if obj.type == C.OBJECTIVE_MINIMIZE:
-                if v < best_val:
-                    best_val, best_idx = v, i
-                if obj.goal is not None and best_val <= obj.goal:
-                    goal_reached = True
-            elif obj.type == C.OBJECTIVE_MAXIMIZE:
-                if v > best_val:
-                    best_val, best_idx = v, i
-                if obj.goal is not None and best_val >= obj.goal:
-                    goal_reached = True
+        buckets, best_idx, goal_reached = SE.summarize(trials, obj.type, obj.goal)
+        lists = SE.bucket_names(trials, buckets)
         st.trials = len(trials)
         st.killed_trial_list = lists["killed"] or None
         st.failed_trial_list = lists["failed"] or None
@@ -484,55 +434,41 @@ class Manager:
         return goal_reached
 
     def _update_condition(self, exp, goal_reached: bool, suggestion_done: bool):
-        """UpdateExperimentStatusCondition (status_util.go:187-235)."""
+        """UpdateExperimentStatusCondition (status_util.go:187-235); the outcome comes from
+        the native status engine."""
         st = exp.status
-        completed = (st.trials_succeeded or 0) + (st.trials_failed or 0) + (st.trials_killed or 0) + \
-            (st.trials_early_stopped or 0) + (st.trial_metrics_unavailable or 0)
-        failed = (st.trials_failed or 0) + (st.trial_metrics_unavailable or 0)
-        active = (st.trials_pending or 0) + (st.trials_running or 0)
         ns = exp.metadata.namespace
-        if goal_reached:
-            EC.mark_succeeded(exp, C.EXPERIMENT_GOAL_REACHED_REASON,
-                              "Experiment has succeeded because Objective goal has reached")
-            st.completion_time = now()
-            self.metrics.inc("katib_experiment_succeeded_total", namespace=ns)
+        outcome = SE.decide_condition(st, goal_reached, suggestion_done, exp.spec.max_failed_trial_count,
+                                      exp.spec.max_trial_count)
+        if outcome == "running":
+            EC.mark_running(exp, C.EXPERIMENT_RUNNING_REASON, "Experiment is running")
             return
-        if exp.spec.max_failed_trial_count is not None and failed != 0 and failed >= exp.spec.max_failed_trial_count:
+        if outcome == "max_failed":
             EC.mark_failed(exp, C.EXPERIMENT_FAILED_REASON, "Experiment has failed because max failed count has reached")
             st.completion_time = now()
             self.metrics.inc("katib_experiment_failed_total", namespace=ns)
             return
-        if exp.spec.max_trial_count is not None and completed >= exp.spec.max_trial_count:
-            EC.mark_succeeded(exp, C.EXPERIMENT_MAX_TRIALS_REACHED_REASON,
-                              "Experiment has succeeded because max trial count has reached")
-            st.completion_time = now()
-            self.metrics.inc("katib_experiment_succeeded_total", namespace=ns)
-            return
-        if suggestion_done and active == 0:
-            EC.mark_succeeded(exp, C.EXPERIMENT_SUGGESTION_END_REACHED_REASON,
-                              "Experiment has succeeded because suggestion service has reached the end")
-            st.completion_time = now()
-            self.metrics.inc("katib_experiment_succeeded_total", namespace=ns)
-            return
-        EC.mark_running(exp, C.EXPERIMENT_RUNNING_REASON, "Experiment is running")
+        reason, msg = {
+            "goal": (C.EXPERIMENT_GOAL_REACHED_REASON, "Experiment has succeeded because Objective goal has reached"),
+            "max_trials": (C.EXPERIMENT_MAX_TRIALS_REACHED_REASON,
+                           "Experiment has succeeded because max trial count has reached"),
+            "suggestion_end": (C.EXPERIMENT_SUGGESTION_END_REACHED_REASON,
+                               "Experiment has succeeded because suggestion service has reached the end"),
+        }[outcome]
+        EC.mark_succeeded(exp, reason, msg)
+        st.completion_time = now()
+        self.metrics.inc("katib_experiment_succeeded_total", namespace=ns)
 
     def _reconcile_trials(self, key, exp, trials):
-        """ReconcileTrials (experiment_controller.go:274-330)."""
-        st = exp.status
-        parallel = exp.spec.parallel_trial_count
-        active = (st.trials_pending or 0) + (st.trials_running or 0)
-        completed = (st.trials_succeeded or 0) + (st.trials_failed or 0) + (st.trials_killed or 0) + \
-            (st.trials_early_stopped or 0)
-        if active > parallel:
-            self._delete_newest_trials(key, exp, trials, active - parallel)
-        elif active < parallel:
-            if exp.spec.max_trial_count is None:
-                required = parallel
-            else:
-                required = min(exp.spec.max_trial_count - completed, parallel)
-            add = max(required - active, 0)
-            if add > 0:
-                self._create_trials(key, exp, trials, add)
+        """ReconcileTrials (experiment_controller.go:274-330); the admission plan (deletions,
+        additions, suggestion demand) comes from the native status engine."""
+        es_no_obs = sum(1 for t in trials if not TC.is_observation_available(t) and TC.is_early_stopped(t))
+        delete, add, requests = SE.plan_admission(exp.status, exp.spec.parallel_trial_count,
+                                                  exp.spec.max_trial_count, len(trials), es_no_obs)
+        if delete > 0:
+            self._delete_newest_trials(key, exp, trials, delete)
+        elif add > 0:
+            self._create_trials(key, exp, trials, add, requests)
 
     def _delete_newest_trials(self, key, exp, trials, count):
         """deleteTrials (experiment_controller.go:362-442): newest first, then prune the suggestion."""
@@ -548,11 +484,10 @@ class Manager:
             sug.status.suggestions = keep
             sug.status.suggestion_count = len(keep)
 
-    def _create_trials(self, key, exp, trials, add):
-        """createTrials + ReconcileSuggestions (experiment_controller.go:332-360, 445-493)."""
+    def _create_trials(self, key, exp, trials, add, requests):
+        """createTrials + ReconcileSuggestions (experiment_controller.go:332-360, 445-493);
+        ``requests`` = len(trials) + add - early-stopped trials without an observation."""
         names = {t.metadata.name for t in trials}
-        incomplete_es = sum(1 for t in trials if not TC.is_observation_available(t) and TC.is_early_stopped(t))
-        requests = len(trials) + add - incomplete_es
         sug = self._get_or_create_suggestion(key, exp, requests)
         if sug is None:
             return

@@ -2,11 +2,13 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <optional>
 #include <regex>
 
 #include "metrics_parser.hpp"
 #include "obs_store.hpp"
 #include "samplers.hpp"
+#include "status_engine.hpp"
 #include "timeutil.hpp"
 #include "trial_runtime.hpp"
 
@@ -73,6 +75,14 @@ py::dict event_dict(const Event& e) {
   d["metrics_error"] = e.metrics_error;
   d["message"] = e.message;
   return d;
+}
+
+// (pending, running, succeeded, failed, killed, early_stopped, metrics_unavailable)
+using CountsTuple = std::tuple<int, int, int, int, int, int, int>;
+StatusCounts counts_from(const CountsTuple& t) {
+  StatusCounts c;
+  std::tie(c.pending, c.running, c.succeeded, c.failed, c.killed, c.early_stopped, c.metrics_unavailable) = t;
+  return c;
 }
 
 }  // namespace
@@ -268,4 +278,66 @@ PYBIND11_MODULE(_native, m) {
         return tpe_sample(td, xs, losses, s, seed);
       },
       py::arg("dims"), py::arg("xs"), py::arg("losses"), py::arg("settings"), py::arg("seed") = 0);
+
+  // ---- experiment status engine (status_engine.hpp) ----
+  // trials: [(name, condition_mask, has_metric, min, max, latest, strategy)]
+  m.def(
+      "summarize_trials",
+      [](const std::vector<std::tuple<std::string, uint32_t, bool, std::string, std::string, std::string, int>>& rows,
+         int objective_type, std::optional<double> goal) {
+        std::vector<TrialFacts> facts;
+        facts.reserve(rows.size());
+        for (const auto& r : rows) {
+          TrialFacts f;
+          std::tie(f.name, f.conditions, f.has_metric, f.min, f.max, f.latest, std::ignore) = r;
+          f.strategy = static_cast<MetricStrategy>(std::get<6>(r));
+          facts.push_back(std::move(f));
+        }
+        TrialsSummary s;
+        {
+          py::gil_scoped_release nogil;
+          s = summarize_trials(facts, static_cast<ObjectiveType>(objective_type), goal.has_value(),
+                               goal.value_or(0.0));
+        }
+        std::vector<std::vector<int>> buckets(s.buckets.begin(), s.buckets.end());
+        return py::make_tuple(buckets, s.best, s.goal_reached);
+      },
+      py::arg("trials"), py::arg("objective_type"), py::arg("goal") = py::none());
+  m.def("objective_value", [](bool has_metric, const std::string& mn, const std::string& mx, const std::string& latest,
+                              int strategy) {
+    TrialFacts f;
+    f.has_metric = has_metric;
+    f.min = mn;
+    f.max = mx;
+    f.latest = latest;
+    f.strategy = static_cast<MetricStrategy>(strategy);
+    return objective_value(f);
+  });
+  m.def(
+      "decide_condition",
+      [](const CountsTuple& c, bool goal_reached, bool suggestion_done, std::optional<int> max_failed,
+         std::optional<int> max_trials) {
+        return static_cast<int>(decide_condition(counts_from(c), goal_reached, suggestion_done, max_failed.has_value(),
+                                                 max_failed.value_or(0), max_trials.has_value(),
+                                                 max_trials.value_or(0)));
+      },
+      py::arg("counts"), py::arg("goal_reached"), py::arg("suggestion_done"), py::arg("max_failed") = py::none(),
+      py::arg("max_trials") = py::none());
+  m.def(
+      "plan_admission",
+      [](const CountsTuple& c, int parallel, std::optional<int> max_trials, int n_trials, int es_without_obs) {
+        AdmissionPlan p = plan_admission(counts_from(c), parallel, max_trials.has_value(), max_trials.value_or(0),
+                                         n_trials, es_without_obs);
+        return py::make_tuple(p.delete_count, p.add_count, p.requests);
+      },
+      py::arg("counts"), py::arg("parallel"), py::arg("max_trials"), py::arg("n_trials"),
+      py::arg("early_stopped_without_observation"));
+  m.def(
+      "plan_restart",
+      [](bool succeeded_by_max_trials, int policy, std::optional<int> max_trials, int trials, bool has_running) {
+        return static_cast<int>(plan_restart(succeeded_by_max_trials, static_cast<ResumePolicy>(policy),
+                                             max_trials.has_value(), max_trials.value_or(0), trials, has_running));
+      },
+      py::arg("succeeded_by_max_trials"), py::arg("resume_policy"), py::arg("max_trials"), py::arg("trials"),
+      py::arg("has_running_trials"));
 }

@@ -22,6 +22,7 @@
 #include "../metrics_parser.hpp"
 #include "../obs_store.hpp"
 #include "../samplers.hpp"
+#include "../status_engine.hpp"
 #include "../trial_runtime.hpp"
 
 using namespace katib;
@@ -191,7 +192,27 @@ static void test_runtime() {
   rmdir(dir);
 }
 
+static void test_status_engine() {
+  std::vector<TrialFacts> ts(4);
+  ts[0].name = "a"; ts[0].conditions = kCondCreated | kCondSucceeded; ts[0].has_metric = true;
+  ts[0].min = ts[0].max = ts[0].latest = "0.4"; ts[0].strategy = MetricStrategy::Min;
+  ts[1] = ts[0]; ts[1].name = "b"; ts[1].min = "0.2";
+  ts[2].name = "c"; ts[2].conditions = kCondCreated | kCondRunning;
+  ts[3].name = "d"; ts[3].conditions = kCondKilled | kCondFailed;
+  TrialsSummary s = summarize_trials(ts, ObjectiveType::Minimize, true, 0.25);
+  CHECK(s.best == 1 && s.goal_reached);
+  StatusCounts c = counts_of(s);
+  CHECK(c.succeeded == 2 && c.running == 1 && c.killed == 1 && c.failed == 0);
+  CHECK(decide_condition(c, false, false, true, 1, true, 10) == ConditionOutcome::Running);
+  c.metrics_unavailable = 1;
+  CHECK(decide_condition(c, false, false, true, 1, true, 10) == ConditionOutcome::MaxFailedReached);
+  AdmissionPlan p = plan_admission(c, 3, true, 10, 5, 0);
+  CHECK(p.delete_count == 0 && p.add_count == 2 && p.requests == 7);
+  CHECK(plan_restart(true, ResumePolicy::LongRunning, true, 12, 10, false) == RestartAction::Restart);
+}
+
 int main() {
+  test_status_engine();
   test_store_concurrent();
   test_parser();
   test_samplers();
