@@ -466,6 +466,7 @@ void register_mlp(py::module& m);  // mlp_bind.cpp
 void register_stem(py::module& m);  // stem_bind.cpp
 void register_enas(py::module& m);  // enas_bind.cpp
 void register_dwconv(py::module& m);  // dwconv_bind.cpp
+void register_darts_optim(py::module& m);  // darts_optim_bind.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, transformer, xGMI all-reduce)";
@@ -490,4 +491,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_dwconv(m);
   register_mlp(m);
   register_stem(m);
+  register_darts_optim(m);
 }

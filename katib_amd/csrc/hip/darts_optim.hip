@@ -1,0 +1,162 @@
+// DARTS search-step optimizer kernels - see darts_optim.h.
+#include <algorithm>
+
+#include "darts_optim.h"
+
+namespace katib_hip {
+namespace optim {
+namespace {
+
+constexpr int kWave = 64;
+
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// Fixed-order reduction of the sumsq partials by wave 0, broadcast through LDS.
+__device__ inline double total_of(const double* parts, int nparts) {
+  __shared__ double sh;
+  if (threadIdx.x < kWave) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxParts / kWave; ++k) {
+      const int i = threadIdx.x + k * kWave;
+      if (i < nparts) v += parts[i];
+    }
+    v = wave_sum(v);
+    if (threadIdx.x == 0) sh = v;
+  }
+  __syncthreads();
+  return sh;
+}
+
+int grid_for(int n) { return std::max(1, std::min((n + kThreads - 1) / kThreads, 1024)); }
+
+__global__ void __launch_bounds__(kThreads) sumsq_kernel(const float* __restrict__ x, int n,
+                                                         double* __restrict__ parts) {
+  __shared__ double sh[kThreads / kWave];
+  double acc = 0.0;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const double v = x[i];
+    acc += v * v;
+  }
+  acc = wave_sum(acc);
+  const int lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
+  if (lane == 0) sh[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kThreads / kWave; ++k) s += sh[k];
+    parts[blockIdx.x] = s;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) virtual_step_kernel(VirtualStepArgs a) {
+  const float lr = *a.lr;
+  const int stride = gridDim.x * kThreads;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < a.n; i += stride) {
+    const float w = a.w[i];
+    // v = (mu * m + g) + wd * w;  w' = w + (-lr) * v   (architect.py:30-47 operation order)
+    const float v = __fadd_rn(__fadd_rn(__fmul_rn(a.mom[i], a.mu), a.g[i]), __fmul_rn(w, a.wd));
+    a.wv[i] = __fadd_rn(__fmul_rn(v, -lr), w);
+  }
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < a.n_zero_w; i += stride) a.zero_w[i] = 0.0f;
+  if (blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < a.na; i += kThreads) {
+      a.av[i] = a.a[i];
+      a.zero_a[i] = 0.0f;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) hessian_kernel(HessianArgs a) {
+  float eps;
+  if (a.phase == 0) {
+    const float norm = static_cast<float>(sqrt(total_of(a.parts, a.nparts)));
+    eps = __fdiv_rn(0.01f, norm);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.eps = eps;
+  } else {
+    eps = *a.eps;
+  }
+  const float scale = a.phase == 1 ? -__fmul_rn(2.0f, eps) : eps;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < a.n; i += gridDim.x * kThreads)
+    a.w[i] = __fadd_rn(a.w[i], __fmul_rn(a.d[i], scale));
+  if (blockIdx.x == 0) {
+    if (a.phase == 0) {
+      for (int i = threadIdx.x; i < a.na; i += kThreads) a.ga[i] = 0.0f;
+    } else if (a.phase == 1) {
+      for (int i = threadIdx.x; i < a.na; i += kThreads) {
+        a.gap[i] = a.ga[i];
+        a.ga[i] = 0.0f;
+      }
+    } else {
+      const float lr = *a.lr, two_eps = __fmul_rn(2.0f, eps);
+      for (int i = threadIdx.x; i < a.na; i += kThreads) {
+        const float h = __fdiv_rn(__fsub_rn(a.gap[i], a.ga[i]), two_eps);
+        a.alpha_grad[i] = __fsub_rn(a.gav[i], __fmul_rn(h, lr));
+      }
+    }
+  }
+}
+
+// single workgroup (the step counter is read by every thread, then advanced once)
+__global__ void __launch_bounds__(kThreads) adam_kernel(AdamArgs a) {
+  const float t = *a.t + 1.0f;
+  __syncthreads();
+  if (threadIdx.x == 0) *a.t = t;
+  const float bc1 = 1.0f - powf(a.b1, t), bc2 = 1.0f - powf(a.b2, t);
+  const float sbc2 = sqrtf(bc2), step = a.lr / bc1;
+  for (int i = threadIdx.x; i < a.n; i += kThreads) {
+    const float g = a.grad[i] + a.wd * a.a[i];
+    const float m = a.b1 * a.m[i] + (1.0f - a.b1) * g;
+    const float v = a.b2 * a.v[i] + (1.0f - a.b2) * g * g;
+    a.m[i] = m;
+    a.v[i] = v;
+    a.a[i] -= m / (sqrtf(v) / sbc2 + a.eps) * step;
+  }
+  for (int i = threadIdx.x; i < a.nzero; i += kThreads) a.zero[i] = 0.0f;
+}
+
+__global__ void __launch_bounds__(kThreads) sgd_clip_kernel(SgdArgs a) {
+  const float total = static_cast<float>(sqrt(total_of(a.parts, a.nparts)));
+  const float coef = fminf(__fdiv_rn(a.clip, total + 1e-6f), 1.0f);
+  const float lr = *a.lr;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < a.n; i += gridDim.x * kThreads) {
+    const float g = __fmul_rn(a.g[i], coef);
+    const float w = a.w[i];
+    a.g[i] = g;
+    const float m = __fadd_rn(__fmul_rn(a.mom[i], a.mu), __fadd_rn(g, __fmul_rn(w, a.wd)));
+    a.mom[i] = m;
+    a.w[i] = __fsub_rn(w, __fmul_rn(m, lr));
+  }
+}
+
+}  // namespace
+
+int sumsq_parts(int n) { return std::max(1, std::min((n + kThreads * 8 - 1) / (kThreads * 8), kMaxParts)); }
+
+void launch_sumsq(const float* x, int n, double* parts, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(sumsq_parts(n)), dim3(kThreads), 0, st, x, n, parts);
+}
+
+void launch_virtual_step(const VirtualStepArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(virtual_step_kernel, dim3(grid_for(std::max(a.n, a.n_zero_w))), dim3(kThreads), 0, st, a);
+}
+
+void launch_hessian(const HessianArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(hessian_kernel, dim3(grid_for(a.n)), dim3(kThreads), 0, st, a);
+}
+
+void launch_adam(const AdamArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(adam_kernel, dim3(1), dim3(kThreads), 0, st, a);
+}
+
+void launch_sgd_clip(const SgdArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(sgd_clip_kernel, dim3(grid_for(a.n)), dim3(kThreads), 0, st, a);
+}
+
+}  // namespace optim
+}  // namespace katib_hip

@@ -156,6 +156,37 @@ def test_search_step_matches_torch(capture):
     _close(Ah, At, "alpha", rtol=5e-2, atol=5e-5)
 
 
+def test_evaluate_graph_matches_eager():
+    """The HIP-graph validation forward (DartsSearch.evaluate with capture) equals the eager
+    HIP forward and the torch-oracle forward on the same weights, across batch shapes and
+    after the weights change between replays."""
+    from katib_amd.models.darts import DartsLayout
+    from katib_amd.models.darts_search import DartsSearch
+    from katib_amd.ops import darts as dops
+
+    dev = torch.device("cuda", 0)
+    layout = DartsLayout(ALL, init_channels=4, num_layers=2, num_nodes=3, stem_multiplier=1)
+    gen = torch.Generator(device=dev).manual_seed(5)
+    tx = torch.randn(16, 3, 32, 32, device=dev, generator=gen)
+    ty = torch.randint(0, 10, (16,), device=dev, generator=gen)
+    dops.set_backend("hip")
+    s = DartsSearch(layout, dev, capture=True)
+    s.step(tx, ty, tx, ty)  # non-trivial running BN statistics
+    for n in (16, 32, 16):
+        vx = torch.randn(n, 3, 32, 32, device=dev, generator=gen)
+        vy = torch.randint(0, 10, (n,), device=dev, generator=gen)
+        got = [float(t) for t in s.evaluate(vx, vy)]
+        want = [float(t) for t in s._evaluate(vx, vy)]
+        dops.set_backend("torch")
+        oracle = [float(t) for t in s._evaluate(vx, vy)]
+        dops.set_backend("hip")
+        assert abs(got[0] - want[0]) < 1e-5 * max(1.0, abs(want[0])) and got[1:] == want[1:]
+        assert abs(got[0] - oracle[0]) < 1e-3 * max(1.0, abs(oracle[0]))
+        s.step(tx, ty, tx, ty)  # weights move; the captured graph must read the live buffers
+    assert len(s._eval_graphs) == 2
+    dops.set_backend("torch")
+
+
 @pytest.mark.parametrize("C,cell_idx,node", [(4, 0, 1), (8, 1, 1), (16, 0, 2), (8, 1, 2)])
 def test_mixed_node_matches_torch(C, cell_idx, node):
     """All edges of a node in one edge-batched Function (mixed strides in reduction cells)."""
