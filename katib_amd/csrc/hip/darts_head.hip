@@ -1,0 +1,119 @@
+// Fused DARTS head: gap + classifier + cross-entropy, forward and backward - see darts_head.h.
+#include <cmath>
+
+#include "darts_head.h"
+#include "darts_ops.h"  // kRep (weight-gradient replica rows)
+
+namespace katib_hip {
+namespace head {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWave = 64;
+constexpr int kWaves = kThreads / kWave;
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// one workgroup per sample; wave w pools channels w, w+4, ... with its lanes over the pixels
+__global__ void __launch_bounds__(kThreads) head_fwd_kernel(FwdArgs a) {
+  __shared__ float sp[kMaxC];
+  __shared__ float sl[kMaxK];
+  const int n = blockIdx.x, lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
+  const float inv_hw = 1.0f / a.HW;
+  const float* xn = a.x + (size_t)n * a.C * a.HW;
+  for (int c = wid; c < a.C; c += kWaves) {
+    float s = 0.0f;
+    for (int p = lane; p < a.HW; p += kWave) s += xn[(size_t)c * a.HW + p];
+    s = wave_sum(s) * inv_hw;
+    if (lane == 0) {
+      sp[c] = s;
+      a.pooled[(size_t)n * a.C + c] = s;
+    }
+  }
+  __syncthreads();
+  for (int k = wid; k < a.K; k += kWaves) {
+    float s = 0.0f;
+    for (int c = lane; c < a.C; c += kWave) s += sp[c] * a.w[(size_t)k * a.C + c];
+    s = wave_sum(s);
+    if (lane == 0) {
+      s += a.b[k];
+      sl[k] = s;
+      a.logits[(size_t)n * a.K + k] = s;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = sl[0];
+    for (int k = 1; k < a.K; ++k) m = fmaxf(m, sl[k]);
+    float se = 0.0f;
+    for (int k = 0; k < a.K; ++k) se += expf(sl[k] - m);
+    const float lse = m + logf(se);
+    const int64_t t = a.y[n];
+    const bool ok = t >= 0 && t < a.K;  // out-of-range label -> NaN loss, no out-of-bounds read
+    a.loss_n[n] = ok ? lse - sl[t] : NAN;
+    const float inv_n = 1.0f / a.N;
+    for (int k = 0; k < a.K; ++k)
+      a.dl[(size_t)n * a.K + k] = (expf(sl[k] - lse) - (k == t ? 1.0f : 0.0f)) * inv_n;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) head_loss_kernel(const float* __restrict__ loss_n, int N,
+                                                             float* __restrict__ loss) {
+  __shared__ float sh[kWaves];
+  float s = 0.0f;
+  for (int i = threadIdx.x; i < N; i += kThreads) s += loss_n[i];
+  s = wave_sum(s);
+  if (threadIdx.x % kWave == 0) sh[threadIdx.x / kWave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.0f;
+    for (int i = 0; i < kWaves; ++i) t += sh[i];
+    *loss = t / N;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) head_bwd_kernel(BwdArgs a) {
+  __shared__ float sd[kMaxK];
+  const int n = blockIdx.x, lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
+  const float g = *a.gout;
+  if (threadIdx.x < a.K) sd[threadIdx.x] = g * a.dl[(size_t)n * a.K + threadIdx.x];
+  __syncthreads();
+  if (a.dx != nullptr) {
+    const float inv_hw = 1.0f / a.HW;
+    float* dxn = a.dx + (size_t)n * a.C * a.HW;
+    for (int c = wid; c < a.C; c += kWaves) {
+      float d = 0.0f;
+      for (int k = 0; k < a.K; ++k) d += sd[k] * a.w[(size_t)k * a.C + c];
+      d *= inv_hw;
+      for (int p = lane; p < a.HW; p += kWave) dxn[(size_t)c * a.HW + p] = d;
+    }
+  }
+  const int rep = n % kRep;
+  if (a.gw != nullptr) {
+    const float* pn = a.pooled + (size_t)n * a.C;
+    float* gw = a.gw + (size_t)rep * a.gw_stride;
+    for (int i = threadIdx.x; i < a.K * a.C; i += kThreads) atomicAdd(gw + i, sd[i / a.C] * pn[i % a.C]);
+  }
+  if (a.gb != nullptr && threadIdx.x < a.K) atomicAdd(a.gb + (size_t)rep * a.gb_stride + threadIdx.x, sd[threadIdx.x]);
+}
+
+}  // namespace
+
+void launch_fwd(const FwdArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(a.N), dim3(kThreads), 0, st, a);
+}
+
+void launch_loss(const float* loss_n, int N, float* loss, hipStream_t st) {
+  hipLaunchKernelGGL(head_loss_kernel, dim3(1), dim3(kThreads), 0, st, loss_n, N, loss);
+}
+
+void launch_bwd(const BwdArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(a.N), dim3(kThreads), 0, st, a);
+}
+
+}  // namespace head
+}  // namespace katib_hip

@@ -351,7 +351,22 @@ class DartsNetwork:
             self._specs[key] = spec
         return spec
 
-    def _forward_cells(self, hd, x, P, normal, reduce, bn, training):
+    def forward_loss(self, x, y, P: Dict[str, torch.Tensor], normal, reduce, bn: BNState, training=True):
+        """(cross-entropy loss, logits). On the whole-cell HIP path the head - global average
+        pool, classifier, log-softmax + NLL and their backward - is one fused HIP Function
+        (hip_darts.head_loss); the returned logits carry no gradient there."""
+        hd = self.ops.hip_module() if self.ops.hip_enabled(x) else None
+        if hd is not None and self._hip_cells(hd, x) and hasattr(hd, "head_loss"):
+            s1 = self._forward_cells(hd, x, P, normal, reduce, bn, training, features=True)
+            if hd.head_supported(s1, P["classifier.weight"], y):
+                return hd.head_loss(s1, P["classifier.weight"], P["classifier.bias"], y)
+            out = F.adaptive_avg_pool2d(s1, 1).flatten(1)
+            logits = F.linear(out, P["classifier.weight"], P["classifier.bias"])
+        else:
+            logits = self.forward(x, P, normal, reduce, bn, training)
+        return F.cross_entropy(logits, y), logits
+
+    def _forward_cells(self, hd, x, P, normal, reduce, bn, training, features=False):
         L = self.layout
         an = normal if torch.is_tensor(normal) else torch.cat(list(normal), 0)
         wn = F.softmax(an, dim=-1)
@@ -371,6 +386,8 @@ class DartsNetwork:
             out = hd.cell_forward(spec, s0, s1, wr if cell["reduction"] else wn, params, bn.get, training,
                                   self.momentum, self.eps)
             s0, s1 = s1, out
+        if features:
+            return s1
         out = F.adaptive_avg_pool2d(s1, 1).flatten(1)
         return F.linear(out, P["classifier.weight"], P["classifier.bias"])
 

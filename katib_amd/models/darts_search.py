@@ -140,8 +140,7 @@ class DartsSearch:
 
     # ------------------------------------------------------------------ pieces
     def _loss(self, x, y, P, an, ar, bn):
-        logits = self.net.forward(x, P, an, ar, bn, training=True)
-        return F.cross_entropy(logits, y), logits
+        return self.net.forward_loss(x, y, P, an, ar, bn, training=True)
 
     def _fold(self, rep):
         if self.hd is not None:
@@ -351,8 +350,8 @@ class DartsSearch:
     # ------------------------------------------------------------------ eval / genotype
     @torch.no_grad()
     def _evaluate(self, x, y):
-        logits = self.net.forward(x, self.layout.views(self.W), *self._arch(self.Aw), self.bn, training=False)
-        loss = F.cross_entropy(logits, y)
+        loss, logits = self.net.forward_loss(x, y, self.layout.views(self.W), *self._arch(self.Aw), self.bn,
+                                             training=False)
         top1, top5 = accuracy(logits, y)
         return loss, top1, top5
 

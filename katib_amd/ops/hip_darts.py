@@ -775,3 +775,59 @@ def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 def stem_conv(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return _StemConv.apply(x, w)
+
+
+# --------------------------------------------------------------------------------- head
+class _Head(torch.autograd.Function):
+    """Global average pool -> classifier -> cross-entropy (mean) as the fused HIP head
+    (``csrc/hip/darts_head.hip``; reference ``model.py:156-161`` + ``nn.CrossEntropyLoss``):
+    forward = per-sample workgroups + one loss reduction, backward = one launch writing the
+    feature gradient and accumulating the classifier gradients into their replica rows."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, y):
+        x = x.contiguous()
+        N, C = x.shape[:2]
+        K = w.shape[0]
+        dev = x.device
+        pooled = torch.empty(N, C, device=dev)
+        logits = torch.empty(N, K, device=dev)
+        dl = torch.empty(N, K, device=dev)
+        loss_n = torch.empty(N, device=dev)
+        loss = torch.empty((), device=dev)
+        _K.head_fwd(x, w, b, y, pooled, logits, dl, loss_n)
+        _K.head_loss(loss_n, loss)
+        ctx.save_for_backward(dl, pooled, w, b)
+        ctx.xshape = x.shape
+        ctx.mark_non_differentiable(logits)
+        ctx.set_materialize_grads(False)
+        return loss, logits
+
+    @staticmethod
+    def backward(ctx, gloss, _glogits):
+        dl, pooled, w, b = ctx.saved_tensors
+        grads = [None, None, None, None]
+        if gloss is None:
+            return tuple(grads)
+        need = ctx.needs_input_grad
+        dev = dl.device
+        x_like = torch.empty((), device=dev).expand(ctx.xshape)
+        dx = torch.empty(ctx.xshape, device=dev) if need[0] else None
+        sinks = _Sinks()
+        gw, sw = sinks.get(w, 1) if need[1] else (None, 0)
+        gb, sb = sinks.get(b, 2) if need[2] else (None, 0)
+        _K.head_bwd(x_like, dl, pooled, w, gloss.reshape(()).contiguous().float(), dx, gw, sw, gb, sb)
+        grads[0] = dx
+        sinks.finish(grads)
+        return tuple(grads)
+
+
+def head_supported(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and w.dtype == torch.float32
+            and w.dim() == 2 and w.shape[1] == x.shape[1] and x.shape[1] <= 1024 and w.shape[0] <= 64
+            and y.dtype == torch.int64 and y.dim() == 1 and y.shape[0] == x.shape[0])
+
+
+def head_loss(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor):
+    """(mean cross-entropy, logits) of ``linear(gap(x))`` against ``y``; logits carry no grad."""
+    return _Head.apply(x, w, b, y.contiguous())

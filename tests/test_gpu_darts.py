@@ -156,6 +156,49 @@ def test_search_step_matches_torch(capture):
     _close(Ah, At, "alpha", rtol=5e-2, atol=5e-5)
 
 
+@pytest.mark.parametrize("N,C,H,K,registered", [(128, 48, 8, 10, False), (128, 256, 8, 10, True),
+                                                 (7, 33, 5, 3, False), (64, 1024, 2, 64, True)])
+def test_fused_head_matches_torch(N, C, H, K, registered):
+    """hip_darts.head_loss (gap + linear + cross-entropy, fused forward/backward) against the
+    fp32 PyTorch formula; weight grads through a registered replicated buffer and through the
+    temporary-replica fallback."""
+    from katib_amd.ops import hip_darts as hd
+
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(N + C)
+    x = torch.randn(N, C, H, H, device=dev, generator=gen)
+    y = torch.randint(0, K, (N,), device=dev, generator=gen)
+    w0 = 0.1 * torch.randn(K, C, device=dev, generator=gen)
+    b0 = 0.1 * torch.randn(K, device=dev, generator=gen)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w0, b0))
+    logits_r = torch.nn.functional.linear(xr.mean((2, 3)), wr, br)
+    loss_r = torch.nn.functional.cross_entropy(logits_r, y)
+    (3.0 * loss_r).backward()
+    if registered:
+        rep = torch.zeros(hd.REP, K * C + K, device=dev)
+        hd.register_grad_replicas(rep)
+        w = rep.new_zeros(K * C + K)[:K * C].view(K, C).copy_(w0).requires_grad_(True)
+        b = torch.empty(K, device=dev).copy_(b0).requires_grad_(True)
+        w.grad = rep[0, :K * C].view(K, C)
+        b.grad = rep[0, K * C:]
+    else:
+        w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+    xh = x.clone().requires_grad_(True)
+    loss, logits = hd.head_loss(xh, w, b, y)
+    assert not logits.requires_grad
+    (3.0 * loss).backward()
+    _close(logits, logits_r.detach(), "logits", rtol=1e-5, atol=1e-5)
+    assert abs(float(loss) - float(loss_r)) < 1e-5 * max(1.0, abs(float(loss_r)))
+    _close(xh.grad, xr.grad, "dx", rtol=1e-4, atol=1e-7)
+    if registered:
+        hd.fold(rep)
+        gw, gb = rep[0, :K * C].view(K, C), rep[0, K * C:]
+    else:
+        gw, gb = w.grad, b.grad
+    _close(gw, wr.grad, "dW", rtol=1e-4, atol=1e-6)
+    _close(gb, br.grad, "db", rtol=1e-4, atol=1e-6)
+
+
 def test_evaluate_graph_matches_eager():
     """The HIP-graph validation forward (DartsSearch.evaluate with capture) equals the eager
     HIP forward and the torch-oracle forward on the same weights, across batch shapes and
