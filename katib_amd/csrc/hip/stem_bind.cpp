@@ -3,6 +3,9 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include <optional>
+
+#include "darts_ops.h"
 #include "stem_conv.h"
 
 namespace py = pybind11;
@@ -52,9 +55,71 @@ void wgrad(const Tensor& x, const Tensor& dy, const Tensor& partial, const Tenso
                    Cout, H, W, chunks, stream());
 }
 
+void chk64(const Tensor& t, const char* name, int64_t min_numel) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kDouble && t.is_contiguous() && t.numel() >= min_numel, name,
+              " must be a contiguous float64 GPU tensor with >= ", min_numel, " elements");
+}
+
+// y = conv(x, w) and BN statistics into stats[kRep][2*Cout] (must be zeroed by the caller)
+void fwd_stats(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& stats) {
+  check_shapes(x, w);
+  chk(y, "y");
+  const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = w.size(0);
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(1) == Cout && y.size(2) == H && y.size(3) == W,
+              "stem: y must be [N][Cout][H][W]");
+  chk64(stats, "stats", (int64_t)katib_hip::kRep * 2 * Cout);
+  TORCH_CHECK(stats.device() == x.device(), "stem: stats on the device of x");
+  S_::launch_fwd_stats(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), stats.data_ptr<double>(), N,
+                       Cin, Cout, H, W, stream());
+}
+
+// weight gradient through the affine BN backward (dy = gradient of the BN output)
+void wgrad_bn(const Tensor& x, const Tensor& dy, const Tensor& z, const Tensor& red, const Tensor& stats,
+              const Tensor& gamma, double eps, std::optional<Tensor> dgamma, std::optional<Tensor> dbeta,
+              const Tensor& partial, const Tensor& dw) {
+  check_shapes(x, dw);
+  chk(dy, "dy");
+  chk(z, "z");
+  chk(partial, "partial");
+  chk(gamma, "gamma");
+  const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = dw.size(0);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == N && dy.size(1) == Cout && dy.size(2) == H && dy.size(3) == W,
+              "stem: dy must be [N][Cout][H][W]");
+  TORCH_CHECK(z.sizes() == dy.sizes(), "stem: z must match dy");
+  TORCH_CHECK(gamma.numel() == Cout, "stem: gamma must have Cout elements");
+  chk64(red, "red", 2 * Cout);
+  chk64(stats, "stats", 2 * Cout);
+  TORCH_CHECK(partial.dim() == 2 && partial.size(1) == Cout * Cin * 9, "stem: partial must be [chunks][Cout*Cin*9]");
+  const int chunks = partial.size(0);
+  TORCH_CHECK(chunks >= 1 && chunks <= 65535 && chunks <= (int64_t)N * H * W, "stem: bad chunk count");
+  S_::BnBwd bn{};
+  bn.z = z.data_ptr<float>();
+  bn.red = red.data_ptr<double>();
+  bn.stats = stats.data_ptr<double>();
+  bn.gamma = gamma.data_ptr<float>();
+  bn.inv_count = static_cast<float>(1.0 / ((double)N * H * W));
+  bn.eps = static_cast<float>(eps);
+  if (dgamma) {
+    chk(*dgamma, "dgamma");
+    TORCH_CHECK(dgamma->numel() == Cout, "stem: dgamma must have Cout elements");
+    bn.dgamma = dgamma->data_ptr<float>();
+  }
+  if (dbeta) {
+    chk(*dbeta, "dbeta");
+    TORCH_CHECK(dbeta->numel() == Cout, "stem: dbeta must have Cout elements");
+    bn.dbeta = dbeta->data_ptr<float>();
+  }
+  for (const Tensor* t : {&dy, &z, &red, &stats, &gamma, &partial})
+    TORCH_CHECK(t->device() == x.device(), "stem: operands on one device");
+  S_::launch_wgrad_bn(x.data_ptr<float>(), dy.data_ptr<float>(), bn, partial.data_ptr<float>(), dw.data_ptr<float>(),
+                      N, Cin, Cout, H, W, chunks, stream());
+}
+
 }  // namespace
 
 void register_stem(py::module& m) {
+  m.def("stem_conv_fwd_stats", &fwd_stats, "stem conv forward + BN statistics into kRep fp64 replicas");
+  m.def("stem_conv_wgrad_bn", &wgrad_bn, "stem conv weight gradient through the affine BN backward");
   m.def("stem_conv_fwd", &fwd, "direct 3x3 stem conv forward (fp32 NCHW)");
   m.def("stem_conv_wgrad", &wgrad, "stem conv weight gradient (chunk partials + fixed-order sum)");
 }

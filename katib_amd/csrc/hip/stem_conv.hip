@@ -13,6 +13,7 @@
 //            4 waves, and a second launch (one wave per weight) sums the chunk partials in a fixed order
 //            (deterministic, no float atomics).
 // The input image never needs a gradient, so there is no data-gradient kernel.
+#include "darts_ops.h"  // kRep
 #include "stem_conv.h"
 
 namespace katib_hip {
@@ -62,21 +63,85 @@ __global__ __launch_bounds__(kThreads) void stem_fwd_kernel(const float* __restr
   }
 }
 
+__device__ __forceinline__ float wsum64(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// forward + BN statistics: every thread of the grid takes part in the per-channel wave sums
+// (out-of-range pixels contribute zeros), waves fold into LDS, the workgroup into replica
+// blockIdx.x % kRep of stats[kRep][2*Cout] = (sum, sum of squares).
 template <int CIN>
+__global__ __launch_bounds__(kThreads) void stem_fwd_stats_kernel(const float* __restrict__ x,
+                                                                   const float* __restrict__ wt,
+                                                                   float* __restrict__ y, double* __restrict__ stats,
+                                                                   int N, int Cout, int H, int W) {
+  __shared__ float ws[kMaxCout * CIN * 9];
+  __shared__ float st[2 * kMaxCout];
+  for (int i = threadIdx.x; i < Cout * CIN * 9; i += kThreads) ws[i] = wt[i];
+  for (int i = threadIdx.x; i < 2 * Cout; i += kThreads) st[i] = 0.f;
+  __syncthreads();
+  const int HW = H * W;
+  const int p = blockIdx.x * kThreads + threadIdx.x;
+  const bool valid = p < N * HW;
+  const int q = valid ? p : 0;
+  const int n = q / HW, r = q - n * HW, h = r / W, w = r - (r / W) * W;
+  float v[CIN * 9];
+  load_patch<CIN>(x, n, h, w, H, W, v);
+  float* out = y + (size_t)n * Cout * HW + r;
+  const int lane = threadIdx.x & 63;
+  for (int co = 0; co < Cout; ++co) {
+    const float* wc = ws + co * CIN * 9;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < CIN * 9; ++k) acc = fmaf(wc[k], v[k], acc);
+    if (valid) out[(size_t)co * HW] = acc;
+    const float a = valid ? acc : 0.f;
+    const float s1 = wsum64(a), s2 = wsum64(a * a);
+    if (lane == 0) {
+      atomicAdd(&st[co], s1);
+      atomicAdd(&st[Cout + co], s2);
+    }
+  }
+  __syncthreads();
+  double* rep = stats + (size_t)(blockIdx.x % kRep) * 2 * Cout;
+  for (int i = threadIdx.x; i < 2 * Cout; i += kThreads) atomicAdd(rep + i, (double)st[i]);
+}
+
+template <int CIN, bool BN>
 __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const float* __restrict__ x,
-                                                               const float* __restrict__ dy,
+                                                               const float* __restrict__ dy, BnBwd bn,
                                                                float* __restrict__ partial, int N, int Cout, int H,
                                                                int W, int per_chunk) {
   constexpr int K = CIN * 9;
   __shared__ float red[kThreads / 64][K];
   const int co = blockIdx.y, HW = H * W, P = N * HW;
   const int p0 = blockIdx.x * per_chunk, p1 = min(P, p0 + per_chunk);
+  // BN backward coefficients: dz = k1 * (dy - m1 - zhat * m2), zhat = (z - mean) * istd
+  float mean = 0.f, istd = 0.f, k1 = 1.f, m1 = 0.f, m2 = 0.f;
+  if (BN) {
+    const double m = bn.stats[co] * (double)bn.inv_count;
+    double var = bn.stats[Cout + co] * (double)bn.inv_count - m * m;
+    if (var < 0) var = 0;
+    mean = (float)m;
+    istd = rsqrtf((float)var + bn.eps);
+    k1 = bn.gamma[co] * istd;
+    m1 = (float)(bn.red[co] * (double)bn.inv_count);
+    m2 = (float)(bn.red[Cout + co] * (double)bn.inv_count);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (bn.dgamma) bn.dgamma[co] += (float)bn.red[Cout + co];
+      if (bn.dbeta) bn.dbeta[co] += (float)bn.red[co];
+    }
+  }
   float acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0.f;
   for (int p = p0 + threadIdx.x; p < p1; p += kThreads) {
     const int n = p / HW, r = p - n * HW, h = r / W, w = r - (r / W) * W;
-    const float d = dy[((size_t)n * Cout + co) * HW + r];
+    const size_t idx = ((size_t)n * Cout + co) * HW + r;
+    float d = dy[idx];
+    if (BN) d = k1 * (d - m1 - (bn.z[idx] - mean) * istd * m2);
     float v[K];
     load_patch<CIN>(x, n, h, w, H, W, v);
 #pragma unroll
@@ -121,18 +186,42 @@ void launch_fwd(const float* x, const float* w, float* y, int N, int Cin, int Co
     hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(blocks), dim3(kThreads), 0, s, x, w, y, N, Cout, H, W);
 }
 
-void launch_wgrad(const float* x, const float* dy, float* partial, float* dw, int N, int Cin, int Cout, int H, int W,
-                  int chunks, hipStream_t s) {
+namespace {
+
+template <bool BN>
+void wgrad_impl(const float* x, const float* dy, const BnBwd& bn, float* partial, float* dw, int N, int Cin, int Cout,
+                int H, int W, int chunks, hipStream_t s) {
   const int P = N * H * W;
   const int per_chunk = (P + chunks - 1) / chunks;
   if (Cin == 3)
-    hipLaunchKernelGGL(stem_wgrad_kernel<3>, dim3(chunks, Cout), dim3(kThreads), 0, s, x, dy, partial, N, Cout, H, W,
-                       per_chunk);
+    hipLaunchKernelGGL((stem_wgrad_kernel<3, BN>), dim3(chunks, Cout), dim3(kThreads), 0, s, x, dy, bn, partial, N,
+                       Cout, H, W, per_chunk);
   else
-    hipLaunchKernelGGL(stem_wgrad_kernel<1>, dim3(chunks, Cout), dim3(kThreads), 0, s, x, dy, partial, N, Cout, H, W,
-                       per_chunk);
+    hipLaunchKernelGGL((stem_wgrad_kernel<1, BN>), dim3(chunks, Cout), dim3(kThreads), 0, s, x, dy, bn, partial, N,
+                       Cout, H, W, per_chunk);
   const int n = Cout * Cin * 9;
   hipLaunchKernelGGL(chunk_sum_kernel, dim3(n), dim3(64), 0, s, partial, dw, n, chunks);
+}
+
+}  // namespace
+
+void launch_wgrad(const float* x, const float* dy, float* partial, float* dw, int N, int Cin, int Cout, int H, int W,
+                  int chunks, hipStream_t s) {
+  wgrad_impl<false>(x, dy, BnBwd{}, partial, dw, N, Cin, Cout, H, W, chunks, s);
+}
+
+void launch_wgrad_bn(const float* x, const float* dy, const BnBwd& bn, float* partial, float* dw, int N, int Cin,
+                     int Cout, int H, int W, int chunks, hipStream_t s) {
+  wgrad_impl<true>(x, dy, bn, partial, dw, N, Cin, Cout, H, W, chunks, s);
+}
+
+void launch_fwd_stats(const float* x, const float* w, float* y, double* stats, int N, int Cin, int Cout, int H, int W,
+                      hipStream_t s) {
+  const int blocks = (N * H * W + kThreads - 1) / kThreads;
+  if (Cin == 3)
+    hipLaunchKernelGGL(stem_fwd_stats_kernel<3>, dim3(blocks), dim3(kThreads), 0, s, x, w, y, stats, N, Cout, H, W);
+  else
+    hipLaunchKernelGGL(stem_fwd_stats_kernel<1>, dim3(blocks), dim3(kThreads), 0, s, x, w, y, stats, N, Cout, H, W);
 }
 
 }  // namespace stem

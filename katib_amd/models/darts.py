@@ -374,11 +374,20 @@ class DartsNetwork:
         if L.has_reduce:
             ar = reduce if torch.is_tensor(reduce) else torch.cat(list(reduce), 0)
             wr = F.softmax(ar, dim=-1)
-        if hd.stem_supported(x, P["stem.conv"]):
-            s = hd.stem_conv(x, P["stem.conv"])
+        if hd.stem_supported(x, P["stem.conv"]) and training and hasattr(hd, "stem_conv_bn"):
+            rm, rv = bn.get("stem.bn")
+            s = hd.stem_conv_bn(x, P["stem.conv"], P["stem.bn.weight"], P["stem.bn.bias"], rm, rv, self.momentum,
+                                self.eps)
+        elif hd.stem_supported(x, P["stem.conv"]) and not torch.is_grad_enabled() and hasattr(hd, "stem_bn_eval"):
+            rm, rv = bn.get("stem.bn")
+            s = hd.stem_bn_eval(hd.stem_conv(x, P["stem.conv"]), P["stem.bn.weight"], P["stem.bn.bias"], rm, rv,
+                                self.eps)
         else:
-            s = F.conv2d(x, P["stem.conv"], padding=1)
-        s = self._bn(s, "stem.bn", bn, training, P["stem.bn.weight"], P["stem.bn.bias"])
+            if hd.stem_supported(x, P["stem.conv"]):
+                s = hd.stem_conv(x, P["stem.conv"])
+            else:
+                s = F.conv2d(x, P["stem.conv"], padding=1)
+            s = self._bn(s, "stem.bn", bn, training, P["stem.bn.weight"], P["stem.bn.bias"])
         s0 = s1 = s
         for ci, cell in enumerate(L.cells):
             spec = self._cell_spec(hd, ci)

@@ -760,6 +760,80 @@ class _StemConv(torch.autograd.Function):
         return gx, gw
 
 
+class _StemConvBN(torch.autograd.Function):
+    """Stem Conv2d(Cin, C, 3, padding=1, bias=False) + BatchNorm2d(C) (affine, batch statistics)
+    on the stem kernels (reference ``model.py:90-93``): the conv accumulates the BN statistics
+    in its epilogue, one fold + one combine_fwd launch apply the normalisation (running stats
+    updated in the same launch); the backward is one BN-backward reduction + fold, then the weight
+    gradient kernel forms the conv-output gradient on the fly and adds d gamma / d beta."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, rm, rv, momentum, eps):
+        x, w = x.contiguous(), w.contiguous()
+        N, _, H, W = x.shape
+        C = w.shape[0]
+        stats = zeros64(REP * 2 * C, x.device)
+        z = torch.empty(N, C, H, W, device=x.device, dtype=x.dtype)
+        _K.stem_conv_fwd_stats(x, w, z, stats)
+        _fold64([(stats, 2 * C, 2 * C)])
+        bn = _bn(stats, rm, rv, N * H * W, True, eps, C)
+        out = torch.empty_like(z)
+        _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], gamma, beta, out, momentum, True, False)
+        ctx.bn, ctx.eps, ctx.stats = bn, eps, stats
+        ctx.save_for_backward(x, w, gamma, beta, z)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w, gamma, beta, z = ctx.saved_tensors
+        bn, eps, stats = ctx.bn, ctx.eps, ctx.stats
+        ctx.bn = ctx.stats = None
+        dout = dout.contiguous()
+        C = w.shape[0]
+        nred = 2 * C + 1
+        red = zeros64(REP * nred, x.device)
+        _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
+        _fold64([(red, nred, nred)])
+        need = ctx.needs_input_grad
+        grads = [None] * 8
+        sinks = _Sinks()
+        gg, _ = sinks.get(gamma, 2) if need[2] else (None, 0)
+        gb, _ = sinks.get(beta, 3) if need[3] else (None, 0)
+        if need[1] or need[2] or need[3]:
+            chunks = stem_chunks(x, C)
+            partial = torch.empty(chunks, w.numel(), device=x.device, dtype=torch.float32)
+            gw = torch.empty_like(w)
+            _K.stem_conv_wgrad_bn(x, dout, z, red, stats, gamma, eps, gg, gb, partial, gw)
+            grads[1] = gw if need[1] else None
+        if need[0]:  # never for the input image; plain formula for completeness
+            m = stats[:C] / z[:, 0].numel()
+            var = (stats[C:2 * C] / z[:, 0].numel() - m * m).clamp_min(0)
+            istd = torch.rsqrt(var.float() + eps).view(1, C, 1, 1)
+            zhat = (z - m.float().view(1, C, 1, 1)) * istd
+            m1 = (red[:C] / z[:, 0].numel()).float().view(1, C, 1, 1)
+            m2 = (red[C:2 * C] / z[:, 0].numel()).float().view(1, C, 1, 1)
+            dz = gamma.view(1, C, 1, 1) * istd * (dout - m1 - zhat * m2)
+            grads[0] = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1)
+        sinks.finish(grads)
+        return tuple(grads)
+
+
+def stem_conv_bn(x, w, gamma, beta, rm, rv, momentum=0.1, eps=1e-5):
+    """Training-mode stem conv + BatchNorm (batch statistics, running stats updated)."""
+    return _StemConvBN.apply(x, w, gamma, beta, rm, rv, momentum, eps)
+
+
+@torch.no_grad()
+def stem_bn_eval(z, gamma, beta, rm, rv, eps=1e-5):
+    """Inference BatchNorm of the stem output with the running statistics (one combine_fwd)."""
+    z = z.contiguous()
+    N, C, H, W = z.shape
+    out = torch.empty_like(z)
+    _K.combine_fwd([([z], [_bn(None, rm, rv, N * H * W, False, eps, C)], [0], None, -1, None, [])], gamma, beta, out,
+                   0.0, False, False)
+    return out
+
+
 def stem_chunks(x: torch.Tensor, cout: int) -> int:
     """Pixel chunks of the weight-gradient grid: >= ~512 workgroups over (chunk, Cout),
     each thread covering a handful of pixels."""

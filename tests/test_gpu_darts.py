@@ -6,6 +6,7 @@ layers, eval mode, and a full second-order search step (eager and HIP-graph).
 """
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
@@ -197,6 +198,39 @@ def test_fused_head_matches_torch(N, C, H, K, registered):
         gw, gb = w.grad, b.grad
     _close(gw, wr.grad, "dW", rtol=1e-4, atol=1e-6)
     _close(gb, br.grad, "db", rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,Cout,H", [(128, 4, 32), (128, 48, 32), (5, 7, 9)])
+def test_stem_conv_bn_matches_torch(N, Cout, H):
+    """hip_darts.stem_conv_bn (conv + BN statistics epilogue, combine BN apply, fused BN backward
+    in the weight-gradient kernel) and stem_bn_eval against conv2d + batch_norm in fp32."""
+    from katib_amd.ops import hip_darts as hd
+
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(N * Cout + H)
+    x = torch.randn(N, 3, H, H, device=dev, generator=gen)
+    w0 = 0.3 * torch.randn(Cout, 3, 3, 3, device=dev, generator=gen)
+    g0 = 1.0 + 0.1 * torch.randn(Cout, device=dev, generator=gen)
+    b0 = 0.1 * torch.randn(Cout, device=dev, generator=gen)
+    R = torch.randn(N, Cout, H, H, device=dev, generator=gen)
+    rm_r, rv_r = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    wr, gr, br = (t.clone().requires_grad_(True) for t in (w0, g0, b0))
+    out_r = F.batch_norm(F.conv2d(x, wr, padding=1), rm_r, rv_r, gr, br, True, 0.1, 1e-5)
+    (out_r * R).sum().backward()
+    rm, rv = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    w, g, b = (t.clone().requires_grad_(True) for t in (w0, g0, b0))
+    out = hd.stem_conv_bn(x, w, g, b, rm, rv, 0.1, 1e-5)
+    (out * R).sum().backward()
+    _close(out, out_r.detach(), "out", rtol=1e-4, atol=1e-5)
+    _close(rm, rm_r, "running_mean", rtol=1e-5, atol=1e-6)
+    _close(rv, rv_r, "running_var", rtol=1e-5, atol=1e-6)
+    _close(w.grad, wr.grad, "dW", rtol=1e-3, atol=1e-4)
+    _close(g.grad, gr.grad, "dgamma", rtol=1e-4, atol=1e-4)
+    _close(b.grad, br.grad, "dbeta", rtol=1e-4, atol=1e-4)
+    with torch.no_grad():
+        ev = hd.stem_bn_eval(hd.stem_conv(x, w0), g0, b0, rm, rv, 1e-5)
+        ev_r = F.batch_norm(F.conv2d(x, w0, padding=1), rm, rv, g0, b0, False, 0.1, 1e-5)
+    _close(ev, ev_r, "eval", rtol=1e-4, atol=1e-5)
 
 
 def test_evaluate_graph_matches_eager():
