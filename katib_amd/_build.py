@@ -81,14 +81,17 @@ def hip_target() -> str:
     return os.path.join(PKG_DIR, "_hipkern" + EXT_SUFFIX)
 
 
-def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950") -> str:
-    """Compile every ``csrc/hip/*.hip`` kernel file + the torch binding into one .so."""
+def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", defines=(), out: str = "",
+              build_dir: str = "") -> str:
+    """Compile every ``csrc/hip/*.hip`` kernel file + the torch binding into one .so.
+    ``defines`` / ``out`` / ``build_dir`` build a tuning variant elsewhere (e.g.
+    ``defines=["KATIB_HIP_REP=8"]``), loadable with ``KATIB_AMD_HIPKERN=<path>``."""
     import torch
     from torch.utils import cpp_extension as ce
 
     srcs = sorted(glob.glob(os.path.join(HIP_SRC, "*.hip"))) + sorted(glob.glob(os.path.join(HIP_SRC, "*.cpp")))
     deps = srcs + sorted(glob.glob(os.path.join(HIP_SRC, "*.h")))
-    out = hip_target()
+    out = out or hip_target()
     if not srcs:
         return ""
     if not force and not _newer(out, deps):
@@ -98,12 +101,12 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950") 
     torch_inc = ce.include_paths()  # torch + torch/csrc/api
     py_inc = sysconfig.get_paths()["include"]
     torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
-    build_dir = os.path.join(PKG_DIR, "csrc", "hip", "build")
+    build_dir = build_dir or os.path.join(PKG_DIR, "csrc", "hip", "build")
     os.makedirs(build_dir, exist_ok=True)
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={arch}", "-D__HIP_PLATFORM_AMD__=1",
               "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_hipkern", "-DTORCH_API_INCLUDE_EXTENSION_H",
               "-D_GLIBCXX_USE_CXX11_ABI=" + str(int(torch._C._GLIBCXX_USE_CXX11_ABI)),
-              "-fno-gpu-rdc", "-Wno-unused-result", "-Wno-deprecated-declarations"]
+              "-fno-gpu-rdc", "-Wno-unused-result", "-Wno-deprecated-declarations"] + ["-D" + d for d in defines]
     inc = [f"-I{p}" for p in torch_inc + [py_inc, HIP_SRC]]
     objs, cmds = [], []
     headers = sorted(glob.glob(os.path.join(HIP_SRC, "*.h")))

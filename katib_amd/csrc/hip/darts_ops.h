@@ -11,7 +11,10 @@ constexpr int kMaxC = 256;
 // execute memory-side and same-address adds serialise, so bounding the adders per address
 // (grid / kRep) keeps every flush short. Consumers sum the replicas (bn_moments / prologues);
 // weight-gradient replicas are folded once per backward pass (fold_rows).
-constexpr int kRep = 32;
+#ifndef KATIB_HIP_REP
+#define KATIB_HIP_REP 32
+#endif
+constexpr int kRep = KATIB_HIP_REP;
 
 struct BNRef {              // where a BN layer's normalisation statistics come from
   const double* sums;       // training: replica r at sums + r*rstride: [2*C] = (sum, sum of squares)

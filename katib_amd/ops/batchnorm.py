@@ -21,6 +21,8 @@ from __future__ import annotations
 import importlib
 
 import torch
+
+from .. import _hipload
 import torch.nn as nn
 import torch.nn.functional as F
 
@@ -31,7 +33,7 @@ def kernels():
     global _K
     if _K is None:
         try:
-            _K = importlib.import_module("katib_amd._hipkern")
+            _K = _hipload.hipkern()
         except ImportError as e:
             raise ImportError("katib_amd._hipkern is not built (run __graft_entry__.build()): %s" % e)
     return _K

@@ -40,8 +40,10 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
+from .. import _hipload
+
 try:
-    _K = importlib.import_module("katib_amd._hipkern")
+    _K = _hipload.hipkern()
 except ImportError as e:  # pragma: no cover - machines without the build
     raise ImportError("katib_amd._hipkern is not built (run __graft_entry__.build()): %s" % e)
 
@@ -775,7 +777,7 @@ class _StemConvBN(torch.autograd.Function):
         stats = zeros64(REP * 2 * C, x.device)
         z = torch.empty(N, C, H, W, device=x.device, dtype=x.dtype)
         _K.stem_conv_fwd_stats(x, w, z, stats)
-        _fold64([(stats, 2 * C, 2 * C)])
+        _K.fold_f64([(stats, 2 * C, 2 * C)])  # always folded: the weight-gradient kernel reads replica 0
         bn = _bn(stats, rm, rv, N * H * W, True, eps, C)
         out = torch.empty_like(z)
         _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], gamma, beta, out, momentum, True, False)
@@ -793,7 +795,7 @@ class _StemConvBN(torch.autograd.Function):
         nred = 2 * C + 1
         red = zeros64(REP * nred, x.device)
         _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
-        _fold64([(red, nred, nred)])
+        _K.fold_f64([(red, nred, nred)])
         need = ctx.needs_input_grad
         grads = [None] * 8
         sinks = _Sinks()

@@ -30,6 +30,8 @@ import importlib
 import math
 
 import torch
+
+from .. import _hipload
 import torch.nn.functional as F
 
 LOG2E = 1.4426950408889634
@@ -37,7 +39,7 @@ LOG2E = 1.4426950408889634
 
 def _kern():
     try:
-        return importlib.import_module("katib_amd._hipkern")
+        return _hipload.hipkern()
     except ImportError as e:
         raise ImportError("katib_amd._hipkern is not built (run __graft_entry__.build()): %s" % e)
 

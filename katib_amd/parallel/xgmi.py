@@ -22,12 +22,14 @@ import os
 from typing import Optional
 
 import torch
+
+from .. import _hipload
 import torch.distributed as dist
 
 
 def _kern():
     try:
-        return importlib.import_module("katib_amd._hipkern")
+        return _hipload.hipkern()
     except ImportError as e:  # pragma: no cover - GPU boxes always carry the in-tree build
         raise ImportError("katib_amd._hipkern is not built (run __graft_entry__.build()): %s" % e)
 
