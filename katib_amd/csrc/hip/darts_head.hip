@@ -11,6 +11,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWave = 64;
 constexpr int kWaves = kThreads / kWave;
+constexpr int kU = 8;  // channels / classes per wave with loads in flight together
 
 __device__ inline float wave_sum(float v) {
 #pragma unroll
@@ -25,24 +26,61 @@ __global__ void __launch_bounds__(kThreads) head_fwd_kernel(FwdArgs a) {
   const int n = blockIdx.x, lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
   const float inv_hw = 1.0f / a.HW;
   const float* xn = a.x + (size_t)n * a.C * a.HW;
-  for (int c = wid; c < a.C; c += kWaves) {
-    float s = 0.0f;
-    for (int p = lane; p < a.HW; p += kWave) s += xn[(size_t)c * a.HW + p];
-    s = wave_sum(s) * inv_hw;
-    if (lane == 0) {
-      sp[c] = s;
-      a.pooled[(size_t)n * a.C + c] = s;
+  // kU channels per wave in flight: all loads issue before the first reduction (the chain of
+  // one load -> wave sum per channel was latency-bound)
+  for (int c0 = wid; c0 < a.C; c0 += kWaves * kU) {
+    float s[kU];
+    if (a.HW <= kWave) {  // one pixel per lane: straight-line loads
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int c = c0 + u * kWaves;
+        s[u] = (c < a.C && lane < a.HW) ? xn[(size_t)c * a.HW + lane] : 0.0f;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int c = c0 + u * kWaves;
+        float v = 0.0f;
+        if (c < a.C)
+          for (int p = lane; p < a.HW; p += kWave) v += xn[(size_t)c * a.HW + p];
+        s[u] = v;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int c = c0 + u * kWaves;
+      const float v = wave_sum(s[u]) * inv_hw;
+      if (lane == 0 && c < a.C) {
+        sp[c] = v;
+        a.pooled[(size_t)n * a.C + c] = v;
+      }
     }
   }
   __syncthreads();
-  for (int k = wid; k < a.K; k += kWaves) {
-    float s = 0.0f;
-    for (int c = lane; c < a.C; c += kWave) s += sp[c] * a.w[(size_t)k * a.C + c];
-    s = wave_sum(s);
-    if (lane == 0) {
-      s += a.b[k];
-      sl[k] = s;
-      a.logits[(size_t)n * a.K + k] = s;
+  for (int k0 = wid; k0 < a.K; k0 += kWaves * kU) {
+    float s[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int k = k0 + u * kWaves;
+      float v = 0.0f;
+      if (k < a.K) {
+        if (a.C <= kWave) {
+          v = lane < a.C ? sp[lane] * a.w[(size_t)k * a.C + lane] : 0.0f;
+        } else {
+          for (int c = lane; c < a.C; c += kWave) v += sp[c] * a.w[(size_t)k * a.C + c];
+        }
+      }
+      s[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int k = k0 + u * kWaves;
+      const float v = wave_sum(s[u]);
+      if (lane == 0 && k < a.K) {
+        const float l = v + a.b[k];
+        sl[k] = l;
+        a.logits[(size_t)n * a.K + k] = l;
+      }
     }
   }
   __syncthreads();
