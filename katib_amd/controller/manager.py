@@ -1002,13 +1002,16 @@ class Manager:
         code = ev["exit_code"]
         if run.collector.get("kind") == 2:
             self._collect_tfevent(trial, run)
-        if ev["early_stopped"] or code == 0 or (ev["worker"] >= 0 and code == 3 and run.early_stopped):
+        outcome = SE.classify_exit(bool(ev["early_stopped"]), code, ev["worker"] >= 0, bool(run.early_stopped),
+                                   bool(ev["deadline_exceeded"]), TC.is_killed(trial), run.attempt,
+                                   run.plan.backoff_limit)
+        if outcome == "succeeded":
             self._finish_trial(tkey, "Succeeded", "", "")
-        elif ev["deadline_exceeded"]:
+        elif outcome == "deadline_exceeded":
             self._finish_trial(tkey, "Failed", "DeadlineExceeded", "Job was active longer than specified deadline")
-        elif TC.is_killed(trial):
+        elif outcome == "killed":
             run.phase = "Failed"
-        elif run.attempt <= run.plan.backoff_limit:
+        elif outcome == "retry":
             run.phase = "Pending"  # retry (Job backoffLimit)
             self.store.remove(tkey[1])
         else:
@@ -1058,37 +1061,31 @@ class Manager:
         status = job_status(kind, phase, reason, message)
         st = gjson.deployed_job_status(status, trial.spec.success_condition or "",
                                        trial.spec.failure_condition or "", trial_running=True) or {}
-        failed, succeeded = st.get("condition") == "Failed", st.get("condition") == "Succeeded"
+        cond = st.get("condition")
         ns = tkey[0]
-        if failed:
-            if not TC.is_failed(trial) and not TC.is_early_stopped(trial):
-                TC.mark_failed(trial, "%s. Job reason: %s" % (C.TRIAL_FAILED_REASON, reason) if reason
-                               else C.TRIAL_FAILED_REASON,
-                               "Trial has failed. Job message: %s" % message if message else "Trial has failed")
-                trial.status.completion_time = now()
-                self._event(trial, "Normal", C.JOB_FAILED_REASON, "Job %s has failed. %s %s"
-                            % (trial.metadata.name, message, reason))
-                self.metrics.inc("katib_trial_failed_total", namespace=ns)
-                self._completed += 1
-        elif succeeded:
+        if cond == "Succeeded":
             self._update_observation(trial)
-            if TC.is_observation_available(trial) and not TC.is_succeeded(trial):
-                if not TC.is_early_stopped(trial):
-                    TC.mark_succeeded(trial, C.CONDITION_TRUE, C.TRIAL_SUCCEEDED_REASON, "Trial has succeeded")
-                    self._event(trial, "Normal", C.JOB_SUCCEEDED_REASON, "Job %s has succeeded" % trial.metadata.name)
-                    self.metrics.inc("katib_trial_succeeded_total", namespace=ns)
-                trial.status.completion_time = now()
-                self._completed += 1
-            elif not TC.is_metrics_unavailable(trial) and not TC.is_early_stopped(trial):
-                TC.mark_metrics_unavailable(trial, C.TRIAL_METRICS_UNAVAILABLE_REASON, "Metrics are not available")
-                trial.status.completion_time = now()
-                self._event(trial, "Warning", C.JOB_METRICS_UNAVAILABLE_REASON,
-                            "Metrics are not available for Job %s" % trial.metadata.name)
-                self.metrics.inc("katib_trial_metrics_unavailable_total", namespace=ns)
-                self._completed += 1
-            elif TC.is_early_stopped(trial):
-                trial.status.completion_time = now()
-                self._completed += 1
+        # the condition change is decided by the native trial state machine
+        action = SE.trial_transition(cond, trial, cond == "Succeeded" and TC.is_observation_available(trial))
+        if action == "mark_failed":
+            TC.mark_failed(trial, "%s. Job reason: %s" % (C.TRIAL_FAILED_REASON, reason) if reason
+                           else C.TRIAL_FAILED_REASON,
+                           "Trial has failed. Job message: %s" % message if message else "Trial has failed")
+            self._event(trial, "Normal", C.JOB_FAILED_REASON, "Job %s has failed. %s %s"
+                        % (trial.metadata.name, message, reason))
+            self.metrics.inc("katib_trial_failed_total", namespace=ns)
+        elif action == "mark_succeeded":
+            TC.mark_succeeded(trial, C.CONDITION_TRUE, C.TRIAL_SUCCEEDED_REASON, "Trial has succeeded")
+            self._event(trial, "Normal", C.JOB_SUCCEEDED_REASON, "Job %s has succeeded" % trial.metadata.name)
+            self.metrics.inc("katib_trial_succeeded_total", namespace=ns)
+        elif action == "mark_metrics_unavailable":
+            TC.mark_metrics_unavailable(trial, C.TRIAL_METRICS_UNAVAILABLE_REASON, "Metrics are not available")
+            self._event(trial, "Warning", C.JOB_METRICS_UNAVAILABLE_REASON,
+                        "Metrics are not available for Job %s" % trial.metadata.name)
+            self.metrics.inc("katib_trial_metrics_unavailable_total", namespace=ns)
+        if action != "none":
+            trial.status.completion_time = now()
+            self._completed += 1
         if not trial.spec.retain_run:
             # the Job is deleted once the trial completed (trial_controller.go:297-306)
             self._event(trial, "Normal", C.JOB_DELETED_REASON, "Job %s has been deleted" % trial.metadata.name)

@@ -3,8 +3,9 @@
 controller - trial bucketing and optimal-trial selection (status_util.go:57-183),
 the experiment completion check (status_util.go:187-235), parallel admission and
 suggestion demand (experiment_controller.go:274-330, 445-493) and the restart rule
-(experiment_controller.go:187-212) - run in C++; this module only flattens the
-objects into plain tuples and maps the results back.
+(experiment_controller.go:187-212), plus the trial state machine - what a finished process
+means for its trial and the resulting condition change (trial_controller_util.go:42-122) -
+run in C++; this module only flattens the objects into plain tuples and maps the results back.
 """
 
 from __future__ import annotations
@@ -31,6 +32,9 @@ _RESUME = {C.RESUME_NEVER: 0, C.RESUME_LONG_RUNNING: 1, C.RESUME_FROM_VOLUME: 2}
 BUCKETS = ("killed", "failed", "succeeded", "early", "running", "mu", "pending")
 OUTCOMES = ("running", "goal", "max_failed", "max_trials", "suggestion_end")
 RESTART = ("none", "restart", "keep_going")
+EXIT = ("succeeded", "deadline_exceeded", "killed", "retry", "failed")
+TRANSITIONS = ("none", "mark_failed", "mark_succeeded", "complete_observed", "mark_metrics_unavailable",
+               "complete_early_stopped")
 
 
 def _s(v) -> str:
@@ -101,9 +105,22 @@ def plan_restart(succeeded_by_max_trials: bool, resume_policy: Optional[str], ma
                                               trials, has_running_trials)]
 
 
+def classify_exit(early_stopped: bool, exit_code: int, warm_worker: bool, run_early_stopped: bool,
+                  deadline_exceeded: bool, trial_killed: bool, attempt: int, backoff_limit: int) -> str:
+    """What a finished primary process means for its trial (local Job controller + backoffLimit)."""
+    return EXIT[native.load().classify_exit(early_stopped, exit_code, warm_worker, run_early_stopped,
+                                            deadline_exceeded, trial_killed, attempt, backoff_limit)]
+
+
+def trial_transition(job_condition: str, trial, observation_available: bool) -> str:
+    """UpdateTrialStatusCondition's decision for a job in ``job_condition`` (Running/Succeeded/Failed)."""
+    job = {"Succeeded": 1, "Failed": 2}.get(job_condition, 0)
+    return TRANSITIONS[native.load().trial_transition(job, condition_mask(trial), observation_available)]
+
+
 def bucket_names(trials: Sequence, buckets) -> dict:
     return {k: [trials[i].metadata.name for i in idx] for k, idx in buckets.items()}
 
 
 __all__: List[str] = ["summarize", "decide_condition", "plan_admission", "plan_restart", "objective_value",
-                      "trial_facts", "condition_mask", "BUCKETS", "OUTCOMES"]
+                      "trial_facts", "condition_mask", "classify_exit", "trial_transition", "BUCKETS", "OUTCOMES"]

@@ -439,7 +439,7 @@ __device__ __forceinline__ void fr2_pair(const float* plane, int W, int Wo, int 
 
 template <int CI, int CO, int NS = 1>
 __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
-  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64 && (CO / 16) % NS == 0, "16-channel blocks");
+  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 128 && CO <= 64 && (CO / 16) % NS == 0, "16-channel blocks");
   constexpr int BO = CO / 16 / NS, KS = CI / 4;
   typedef float f4 __attribute__((ext_vector_type(4)));
   const PwFwdArgs& a = bt.e[blockIdx.y];
@@ -1182,7 +1182,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // every output channel but the weight gradients and dd of its input-channel group only.
 template <int CI, int CO, int NS = 1>
 __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
-  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 64 && CO <= 64 && (CI / 16) % NS == 0, "16-channel blocks");
+  static_assert(CI % 16 == 0 && CO % 16 == 0 && CI <= 128 && CO <= 64 && (CI / 16) % NS == 0, "16-channel blocks");
   constexpr int BO = CO / 16, BI = CI / 16 / NS, RS = 64 + 4;  // LDS tile row stride (floats)
   typedef float f4 __attribute__((ext_vector_type(4)));
   const PwBwdArgs& a = bt.e[blockIdx.y];
@@ -1960,7 +1960,7 @@ void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st) {
   const PwFwdArgs& a = b.e[0];
   if (try_pw_fwd_wave<48, 16>(b, st) || try_pw_fwd_wave<48, 32>(b, st) || try_pw_fwd_wave<64, 32>(b, st) ||
       try_pw_fwd_wave<32, 16>(b, st) || try_pw_fwd_wave<16, 16>(b, st) || try_pw_fwd_wave<32, 32>(b, st) ||
-      try_pw_fwd_wave<64, 64>(b, st))
+      try_pw_fwd_wave<64, 64>(b, st) || try_pw_fwd_wave<128, 64>(b, st))  // 128 -> 64: last-cell preprocess
     return;
   size_t lds = sizeof(float) * (a.Cin * 64 + 2 * a.Cout);
   dim3 grid(per_edge_blocks(a.N * a.Ho * a.Wo / 64, b.n), b.n);
@@ -2070,7 +2070,7 @@ void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st) {
   // 16..64-channel layers: wave-per-chunk MFMA kernel (see pw_bwd_wave_kernel)
   if (try_pw_bwd_wave<16, 16>(b, st) || try_pw_bwd_wave<32, 32>(b, st) || try_pw_bwd_wave<64, 64>(b, st) ||
       try_pw_bwd_wave<48, 16>(b, st) || try_pw_bwd_wave<48, 32>(b, st) || try_pw_bwd_wave<64, 32>(b, st) ||
-      try_pw_bwd_wave<32, 16>(b, st))
+      try_pw_bwd_wave<32, 16>(b, st) || try_pw_bwd_wave<128, 64>(b, st))
     return;
   int ntiles = a.N * a.Ho * a.Wo / 64;
   dim3 grid(per_edge_blocks(ntiles, b.n), b.n);

@@ -333,6 +333,29 @@ PYBIND11_MODULE(_native, m) {
       py::arg("counts"), py::arg("parallel"), py::arg("max_trials"), py::arg("n_trials"),
       py::arg("early_stopped_without_observation"));
   m.def(
+      "classify_exit",
+      [](bool early_stopped, int exit_code, bool warm_worker, bool run_early_stopped, bool deadline_exceeded,
+         bool trial_killed, int attempt, int backoff_limit) {
+        ExitFacts f;
+        f.early_stopped = early_stopped;
+        f.exit_code = exit_code;
+        f.warm_worker = warm_worker;
+        f.run_early_stopped = run_early_stopped;
+        f.deadline_exceeded = deadline_exceeded;
+        f.trial_killed = trial_killed;
+        f.attempt = attempt;
+        f.backoff_limit = backoff_limit;
+        return static_cast<int>(classify_exit(f));
+      },
+      py::arg("early_stopped"), py::arg("exit_code"), py::arg("warm_worker"), py::arg("run_early_stopped"),
+      py::arg("deadline_exceeded"), py::arg("trial_killed"), py::arg("attempt"), py::arg("backoff_limit"));
+  m.def(
+      "trial_transition",
+      [](int job, uint32_t conditions, bool observation_available) {
+        return static_cast<int>(trial_transition(job, conditions, observation_available));
+      },
+      py::arg("job"), py::arg("conditions"), py::arg("observation_available"));
+  m.def(
       "plan_restart",
       [](bool succeeded_by_max_trials, int policy, std::optional<int> max_trials, int trials, bool has_running) {
         return static_cast<int>(plan_restart(succeeded_by_max_trials, static_cast<ResumePolicy>(policy),

@@ -116,6 +116,28 @@ AdmissionPlan plan_admission(const StatusCounts& c, int parallel, bool has_max_t
   return p;
 }
 
+ExitOutcome classify_exit(const ExitFacts& f) {
+  if (f.early_stopped || f.exit_code == 0 || (f.warm_worker && f.exit_code == 3 && f.run_early_stopped))
+    return ExitOutcome::Succeeded;
+  if (f.deadline_exceeded) return ExitOutcome::DeadlineExceeded;
+  if (f.trial_killed) return ExitOutcome::Killed;
+  if (f.attempt <= f.backoff_limit) return ExitOutcome::Retry;
+  return ExitOutcome::Failed;
+}
+
+TrialTransition trial_transition(int job, uint32_t c, bool observation_available) {
+  const bool failed = c & kCondFailed, succeeded = c & kCondSucceeded, early = c & kCondEarlyStopped,
+             mu = c & kCondMetricsUnavailable;
+  if (job == 2) return (!failed && !early) ? TrialTransition::MarkFailed : TrialTransition::None;
+  if (job != 1) return TrialTransition::None;
+  // the reference's if / else-if chain, with the local early-stop handling
+  if (observation_available && !succeeded)
+    return early ? TrialTransition::CompleteObserved : TrialTransition::MarkSucceeded;
+  if (!mu && !early) return TrialTransition::MarkMetricsUnavailable;
+  if (early) return TrialTransition::CompleteEarlyStopped;
+  return TrialTransition::None;
+}
+
 RestartAction plan_restart(bool succeeded_by_max_trials, ResumePolicy policy, bool has_max_trials, int max_trials,
                            int trials, bool has_running_trials) {
   const bool restartable =

@@ -94,6 +94,40 @@ enum class RestartAction : int {
   KeepGoing,    // completed but trials still running: reconcile them
 };
 
+// ---- trial state machine (trial controller) ----
+// What a finished primary process means for its trial (manager.py _on_runtime_event, the
+// local analogue of the Job controller + backoffLimit feeding trial_controller.go:263-310).
+enum class ExitOutcome : int {
+  Succeeded = 0,     // job status Succeeded (exit 0, or early-stopped by the collector)
+  DeadlineExceeded,  // job Failed, reason DeadlineExceeded (activeDeadlineSeconds)
+  Killed,            // the trial was killed: keep the Killed condition, job phase Failed
+  Retry,             // back to Pending (attempt <= backoffLimit)
+  Failed,            // job Failed, reason Error
+};
+struct ExitFacts {
+  bool early_stopped = false;       // the collector's stop rules fired
+  int exit_code = 0;
+  bool warm_worker = false;         // ran inside a warm worker (exit code 3 = stopped by signal)
+  bool run_early_stopped = false;   // an early stop was requested for this run
+  bool deadline_exceeded = false;
+  bool trial_killed = false;
+  int attempt = 0;
+  int backoff_limit = 0;
+};
+ExitOutcome classify_exit(const ExitFacts& f);
+
+// UpdateTrialStatusCondition (trial_controller_util.go:42-122): the condition change for a
+// trial whose job reached `job` (0 running, 1 succeeded, 2 failed).
+enum class TrialTransition : int {
+  None = 0,
+  MarkFailed,              // Failed + completion time + event + counter
+  MarkSucceeded,           // Succeeded (observation available)
+  CompleteObserved,        // observation available but already EarlyStopped: completion time only
+  MarkMetricsUnavailable,  // succeeded job without the objective metric
+  CompleteEarlyStopped,    // early-stopped trial without an observation: completion time only
+};
+TrialTransition trial_transition(int job, uint32_t conditions, bool observation_available);
+
 TrialBucket classify(uint32_t conditions);
 std::string objective_value(const TrialFacts& t);
 TrialsSummary summarize_trials(const std::vector<TrialFacts>& trials, ObjectiveType type, bool has_goal,

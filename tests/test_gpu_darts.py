@@ -129,6 +129,38 @@ def test_preprocess_matches_torch(reduce):
         _close(a, b, name_, rtol=1e-3, atol=1e-4)
 
 
+def test_wide_preprocess_128_to_64_matches_torch():
+    """darts-gpu.yaml's last reduction cell: StdConv 128 -> 64 at 16x16 (pw_fwd_wave / pw_bwd_wave
+    <128, 64> instantiations)."""
+    from katib_amd.models.darts import DartsNetwork
+    from katib_amd.ops import darts as dops
+
+    layout, W, dev, BNState = _setup(16, L=3, N=4)
+    cell = layout.cells[2]
+    assert cell["cp"] == 128 and cell["C"] == 64
+    gen = torch.Generator(device=dev).manual_seed(9)
+    x = torch.randn(16, 128, 16, 16, device=dev, generator=gen)
+    results = []
+    for backend in ("torch", "hip"):
+        dops.set_backend(backend)
+        net = DartsNetwork(layout)
+        Wl = W.clone()
+        gW = torch.zeros_like(Wl)
+        P, G = layout.views(Wl), layout.views(gW)
+        for k, v in P.items():
+            v.requires_grad_(True)
+            v.grad = G[k]
+        bn = BNState(layout, dev)
+        xl = x.clone().requires_grad_(True)
+        out = net.preprocess(xl, "cells.2.pre1", False, P, bn, True)
+        R = torch.randn(out.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(8))
+        (out * R).sum().backward(inputs=[xl] + list(P.values()))
+        results.append((out.detach(), xl.grad, gW, bn.mean.clone(), bn.var.clone()))
+    dops.set_backend("torch")
+    for name_, a, b in zip(["out", "dx", "dW", "rm", "rv"], results[1], results[0]):
+        _close(a, b, name_, rtol=1e-3, atol=1e-4)
+
+
 @pytest.mark.parametrize("capture", [False, True])
 def test_search_step_matches_torch(capture):
     from katib_amd.models.darts import DartsLayout

@@ -159,3 +159,34 @@ def test_adapter_flattens_objects():
     assert names["succeeded"] == ["a", "b"] and names["running"] == ["c"] and names["pending"] == ["d"]
     assert best == 1 and goal
     assert SE.objective_value(ts[0]) == "0.4" and SE.objective_value(ts[2]) == UNAV
+
+
+@pytest.mark.parametrize("facts,want", [
+    # (early_stopped, exit_code, warm_worker, run_early_stopped, deadline, killed, attempt, backoff)
+    ((False, 0, False, False, False, False, 1, 0), 0),
+    ((True, 143, False, True, False, False, 1, 0), 0),  # collector stop rules fired
+    ((False, 3, True, True, False, False, 1, 0), 0),  # warm worker stopped by the early-stop signal
+    ((False, 3, False, True, False, False, 1, 0), 4),  # exit code 3 only counts inside warm workers
+    ((False, 1, False, False, True, False, 1, 0), 1),  # activeDeadlineSeconds
+    ((False, 137, False, False, False, True, 1, 0), 2),  # killed trial keeps its Killed condition
+    ((False, 1, False, False, False, False, 1, 2), 3),  # attempt <= backoffLimit: retry
+    ((False, 1, False, False, False, False, 3, 2), 4),
+])
+def test_classify_exit(facts, want):
+    assert N.classify_exit(*facts) == want
+
+
+@pytest.mark.parametrize("job,mask,obs,want", [
+    (0, CREATED | RUNNING, False, 0),
+    (2, CREATED | RUNNING, False, 1),
+    (2, CREATED | FAILED, False, 0),  # already failed
+    (2, CREATED | ES, False, 0),  # early-stopped trials never fail
+    (1, CREATED | RUNNING, True, 2),
+    (1, CREATED | ES, True, 3),  # early-stopped with an observation: completion only
+    (1, CREATED | RUNNING, False, 4),  # no objective metric
+    (1, CREATED | MU, False, 0),
+    (1, CREATED | ES, False, 5),
+    (1, CREATED | SUCCEEDED, True, 4),  # the reference's else-if on an already-succeeded trial
+])
+def test_trial_transition(job, mask, obs, want):
+    assert N.trial_transition(job, mask, obs) == want
