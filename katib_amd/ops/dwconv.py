@@ -7,7 +7,11 @@ op_library.py:22-155``: Keras ``DepthwiseConv2D`` / ``SeparableConv2D`` with
 channels-last like the rest of the child network, weights are the fp32 master parameters
 (``[C*DM, 1, K, K]``, output channel ``o`` reads input channel ``o // DM`` as in Keras and
 ``groups=C`` in PyTorch), accumulation is fp32. The weight gradient is summed from
-per-workgroup partials without atomics (deterministic).
+per-workgroup partials without atomics (deterministic). Channel counts that are not a
+multiple of 8 (the 3-channel image input of a child whose first op is a (separable)
+depthwise convolution) are zero-padded to 8 channels around the kernels, so no child op
+falls back to MIOpen's grouped convolution (whose solvers, measured on MI355X, corrupt
+the HIP-graph-captured train step: ``profiles/enas_child_capture_bisect_r02.log``).
 """
 
 from __future__ import annotations
@@ -27,7 +31,7 @@ def supported(x: torch.Tensor, weight: torch.Tensor, groups: int, stride: int) -
     C = x.shape[1]
     K = weight.shape[-1]
     dm = weight.shape[0] // max(C, 1)
-    return (x.is_cuda and x.dim() == 4 and groups == C and C % 8 == 0 and weight.shape[0] == C * dm
+    return (x.is_cuda and x.dim() == 4 and groups == C and weight.shape[0] == C * dm
             and dm in (1, 2) and K in (3, 5, 7) and weight.shape[-2] == K and stride in (1, 2))
 
 
@@ -74,4 +78,12 @@ def depthwise_same(x: torch.Tensor, weight: torch.Tensor, bias, stride: int) -> 
     """Keras ``padding='same'`` depthwise convolution (bf16 NHWC in / out)."""
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
-    return _DwFn.apply(x, weight, bias, int(stride))
+    C = x.shape[1]
+    if C % 8 == 0:
+        return _DwFn.apply(x, weight, bias, int(stride))
+    # zero channels C..C8-1: output channel o = c*DM + j, so the real outputs are the first C*DM
+    c8, dm = (C + 7) // 8 * 8, weight.shape[0] // C
+    xp = torch.nn.functional.pad(x, (0, 0, 0, 0, 0, c8 - C))
+    wp = torch.nn.functional.pad(weight, (0, 0, 0, 0, 0, 0, 0, (c8 - C) * dm))
+    bp = torch.nn.functional.pad(bias, (0, (c8 - C) * dm)) if bias is not None else None
+    return _DwFn.apply(xp, wp, bp, int(stride))[:, :C * dm]

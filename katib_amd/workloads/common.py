@@ -81,9 +81,24 @@ def markov_tokens(n_tokens: int, vocab: int = 50257, seed: int = 0, dev=None, fa
 class CapturedStep:
     """Capture ``fn()`` (a full train step reading static input buffers) into a HIP
     graph after ``warmup`` eager runs on a side stream; replay afterwards. Falls back
-    to eager execution on CPU or when ``enabled`` is False."""
+    to eager execution on CPU or when ``enabled`` is False.
 
-    def __init__(self, fn: Callable[[], torch.Tensor], enabled: bool = True, warmup: int = 3):
+    ``no_miopen``: run the step (warmup, capture and eager) with MIOpen disabled, so a
+    convolution / batch-norm fallback takes PyTorch's native kernels. Measured on MI355X
+    (``profiles/enas_child_capture_probe_r02.log``): with MIOpen's grouped convolution inside
+    the captured ENAS child step, one replay turned finite weights NaN at a deterministic
+    step while an eager rerun of the same step from a snapshot stayed finite; the step only
+    broke once eager allocations between replays (validation passes, snapshots) grew the
+    memory pool - memory the captured MIOpen nodes reference outside the graph's pool."""
+
+    def __init__(self, fn: Callable[[], torch.Tensor], enabled: bool = True, warmup: int = 3,
+                 no_miopen: bool = False):
+        if no_miopen:
+            inner = fn
+
+            def fn():
+                with torch.backends.cudnn.flags(enabled=False):
+                    return inner()
         self.fn = fn
         self.enabled = enabled and torch.cuda.is_available()
         self.warmup = warmup

@@ -21,6 +21,9 @@ SHAPES = [
     (2, 48, 15, 15, 3, 2, 2),   # odd size: asymmetric 'same' padding
     (2, 16, 8, 8, 7, 2, 1),
     (3, 96, 17, 9, 5, 1, 1),    # non-square, odd
+    (4, 3, 32, 32, 3, 1, 1),    # 3-channel image input: channels zero-padded to 8 around the kernel
+    (2, 3, 32, 32, 5, 2, 2),
+    (2, 12, 9, 9, 3, 1, 2),
 ]
 
 
