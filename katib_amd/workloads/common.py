@@ -84,12 +84,8 @@ class CapturedStep:
     to eager execution on CPU or when ``enabled`` is False.
 
     ``no_miopen``: run the step (warmup, capture and eager) with MIOpen disabled, so a
-    convolution / batch-norm fallback takes PyTorch's native kernels. Measured on MI355X
-    (``profiles/enas_child_capture_probe_r02.log``): with MIOpen's grouped convolution inside
-    the captured ENAS child step, one replay turned finite weights NaN at a deterministic
-    step while an eager rerun of the same step from a snapshot stayed finite; the step only
-    broke once eager allocations between replays (validation passes, snapshots) grew the
-    memory pool - memory the captured MIOpen nodes reference outside the graph's pool."""
+    convolution / batch-norm fallback takes PyTorch's native kernels instead of MIOpen
+    solvers inside a captured graph."""
 
     def __init__(self, fn: Callable[[], torch.Tensor], enabled: bool = True, warmup: int = 3,
                  no_miopen: bool = False):

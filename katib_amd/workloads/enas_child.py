@@ -15,11 +15,9 @@ batches of 128, printing ``Training-Accuracy``, ``Training-Loss``,
 MI355X specifics: channels-last bf16 convolutions on the hand-written implicit-GEMM
 MFMA kernels (``ops/conv.py``; TF 'same' padding handled inside the kernel's gather),
 depthwise convolutions on the NHWC depthwise kernels (``ops/dwconv.py``; the 3-channel
-image input is zero-padded to 8 channels there instead of falling back to MIOpen's grouped
-convolution, which broke the captured step: ``profiles/enas_child_capture_*_r02.log``),
-batch norm on the NHWC bf16 HIP kernels (``ops/batchnorm.py``, channel counts that are
-multiples of 8), the train step captured as a HIP graph (MIOpen disabled inside it, so any
-remaining fallback runs PyTorch's native kernels), synthetic CIFAR-10-shaped data in HBM, and data parallelism
+image input is zero-padded to 8 channels there, so no op falls back to MIOpen), batch norm
+on the NHWC bf16 HIP kernels (``ops/batchnorm.py``, channel counts that are multiples of
+8), synthetic CIFAR-10-shaped data in HBM, and data parallelism
 over the trial's GPUs (``WORLD_SIZE`` ranks, RCCL all-reduce of the flat gradient)
 in place of ``tf.distribute.MirroredStrategy``.
 """
@@ -180,7 +178,11 @@ def parse_args(argv):
     p.add_argument("--batch-size", type=int, default=128)
     p.add_argument("--num-train", type=int, default=50000)
     p.add_argument("--num-valid", type=int, default=10000)
-    p.add_argument("--capture", type=int, default=1)
+    # eager by default: measured on MI355X the eager step is faster (28.4 s vs 31.7 s for 3
+    # epochs) and the HIP-graph-captured step turns NaN at a deterministic replay once eager
+    # work runs between replays (profiles/enas_child_capture_{bisect,probe,fix}_r02.log;
+    # open issue, scripts/enas_repro.py reproduces it)
+    p.add_argument("--capture", type=int, default=0)
     p.add_argument("--seed", type=int, default=0)
     return p.parse_args(argv)
 
