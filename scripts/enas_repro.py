@@ -10,7 +10,7 @@ argv: "<capture>[:variant]" with variant in
             re-run eagerly from a snapshot of the state before it, with forward/backward hooks
             naming the first module whose output / input gradient is non-finite
 variants combine with '+': samestream (warmup and capture on one persistent side stream),
-blas (rocBLAS instead of hipBLASLt), nocache (autocast cache_enabled=False)"""
+blas (rocBLAS instead of hipBLASLt), nocache (autocast cache_enabled=False), nodrop (no dropout)"""
 import functools
 import json
 import os
@@ -62,6 +62,8 @@ def _probe_call(self):
     if self.graph is None:
         return _base[0](self)
     env = _closure(self.fn)
+    if "inner" in env:  # CapturedStep(no_miopen=True) wraps the step
+        env = _closure(env["inner"])
     model, opt, acc = env["model"], env["opt"], env["acc_buf"]
     self.nstep = getattr(self, "nstep", 0) + 1
     l0 = float(acc[0])
@@ -117,7 +119,8 @@ import math  # noqa: E402
 
 cfg = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "enas_repro_arch.json")))
 orig = dict(bn=hbn.BatchNorm2d.forward, conv=hconv.supported, dw=hdw.supported, adam=torch.optim.Adam,
-            autocast=torch.autocast, blas=torch.backends.cuda.preferred_blas_library())
+            autocast=torch.autocast, blas=torch.backends.cuda.preferred_blas_library(),
+            drop=torch.nn.Dropout.forward)
 
 
 class _AdamForeach(torch.optim.Adam):
@@ -137,6 +140,7 @@ for spec in sys.argv[1:] or ["1", "0"]:
     torch.backends.cuda.preferred_blas_library("cublas" if "blas" in parts else orig["blas"])
     enas_child.torch.autocast = (functools.partial(orig["autocast"], cache_enabled=False) if "nocache" in parts
                                  else orig["autocast"])
+    torch.nn.Dropout.forward = (lambda self, x: x) if "nodrop" in parts else orig["drop"]
     if variant == "torchbn":
         hbn.BatchNorm2d.forward = lambda self, x, residual=None, relu=False: torch.nn.BatchNorm2d.forward(self, x)
     elif variant == "noconv":
