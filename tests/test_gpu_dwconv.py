@@ -85,3 +85,30 @@ def test_enas_child_ops_use_hip_depthwise(monkeypatch):
         y.float().sum().backward()
         assert y.shape[1] == op.cout and y.shape[2] == op.hw
     assert len(calls) == 2
+
+
+def test_enas_child_has_no_miopen_convolution(monkeypatch):
+    """Every convolution of a child whose first op is a separable conv on the 3-channel image
+    (the repro architecture) runs on the HIP kernels: nn.Conv2d.forward is never reached."""
+    import json
+    import os
+
+    import torch.nn as nn
+    from katib_amd.workloads.enas_child import ChildNet
+
+    def refuse(self, x):
+        raise AssertionError("MIOpen / PyTorch conv fallback reached: %s" % (tuple(self.weight.shape),))
+
+    monkeypatch.setattr(nn.Conv2d, "forward", refuse)
+    cfg = json.load(open(os.path.join(os.path.dirname(__file__), "..", "scripts", "enas_repro_arch.json")))
+    arch = cfg["architecture"]
+    arch = json.loads(arch) if isinstance(arch, str) else arch
+    nn_config = json.loads(cfg["nn_config"].replace("'", '"'))
+    dev = torch.device("cuda", 0)
+    net = ChildNet(arch, nn_config).to(dev).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 32, 32, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = net(x)
+    y.float().sum().backward()
+    torch.cuda.synchronize()
+    assert y.shape == (4, 10) and torch.isfinite(y.float()).all()
