@@ -141,13 +141,13 @@ for spec in sys.argv[1:] or ["1", "0"]:
     enas_child.torch.autocast = (functools.partial(orig["autocast"], cache_enabled=False) if "nocache" in parts
                                  else orig["autocast"])
     torch.nn.Dropout.forward = (lambda self, x: x) if "nodrop" in parts else orig["drop"]
-    if variant == "torchbn":
+    if "torchbn" in parts:
         hbn.BatchNorm2d.forward = lambda self, x, residual=None, relu=False: torch.nn.BatchNorm2d.forward(self, x)
-    elif variant == "noconv":
+    if "noconv" in parts:
         hconv.supported = lambda *a, **k: False
-    elif variant == "nodw":
+    if "nodw" in parts:
         hdw.supported = lambda *a, **k: False
-    elif variant == "adamfe":
+    if "adamfe" in parts:
         enas_child.torch.optim.Adam = _AdamForeach
     extra = ["--num-valid=0"] if variant == "noeval" else []
     try:
