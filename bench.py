@@ -3,13 +3,25 @@
 
 Runs the flagship workload - one full DARTS search step (second-order architect:
 5 forward + 5 backward passes, Adam on alphas, clipped SGD on weights) - on N
-GPUs of one node, one process per GPU (torchrun env; RCCL all-reduce of the
-flat gradient buffers). Times exactly ``--steps`` steps after ``--warmup``
-untimed steps, bracketed by barrier + synchronize, MAX over ranks, then projects
-the reference's end-to-end search: ``epochs x (steps/epoch x step time +
-validation pass)`` with the B5 config (C=4, L=2, N=3, stem x1, 6 primitives +
-none, batch 128 per GPU, 25k/25k split, 2 epochs) unless ``--config default``
-(darts-gpu.yaml: C=16, L=3, N=4, stem x3).
+GPUs of one node, one process per GPU (torchrun env; one-shot xGMI / RCCL
+all-reduce of the flat gradient buffers inside the captured step). Times exactly
+``--steps`` steps after ``--warmup`` untimed steps, bracketed by barrier +
+synchronize, MAX over ranks, then projects the reference's end-to-end search:
+``epochs x (steps/epoch x step time + validation pass)`` with the B5 config (C=4,
+L=2, N=3, stem x1, 6 primitives + none, 25k/25k split, 2 epochs) unless
+``--config default`` (darts-gpu.yaml: C=16, L=3, N=4, stem x3).
+
+Scaling: ``--scaling strong`` (default) keeps B5's global batch of 128 at every N,
+each rank taking 128/N rows, so every N runs the same search (196 steps per epoch);
+``--scaling weak`` keeps 128 rows per GPU (global batch 128 N: a different search,
+labelled as such).
+
+The same JSON line also carries
+* ``trials_per_hour``: BASELINE config 2 end to end through the scheduler (TPE over the
+  MNIST MLP, one trial per GPU at a time over all N GPUs, warm workers), run by rank 0
+  in a child process *before* any rank touches the GPU (``bench_trials.py``);
+* ``torch_eager_ms_per_step``: the same search step on the PyTorch op backend launched
+  eagerly (MIOpen / hipBLASLt / PyTorch kernels, no HIP graph), a same-node comparator.
 
 Lower is better; vs_baseline = value / 282 s (B5, 1x NVIDIA GPU, end to end).
 Data: synthetic CIFAR-10-shaped tensors resident in HBM, random-init weights.
@@ -21,6 +33,7 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -39,7 +52,10 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="b5", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=128, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=128, help="global batch (strong) / per-GPU batch (weak)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--trials", type=int, default=3, help="trials per GPU of the trials/hour experiment (0: skip)")
+    ap.add_argument("--comparator-steps", type=int, default=5, help="torch-eager comparator steps (0: skip)")
     ap.add_argument("--capture", type=int, default=1)
     ap.add_argument("--ops", default=os.environ.get("KATIB_AMD_DARTS_OPS", "hip"))
     ap.add_argument("--valid-batches", type=int, default=10)
@@ -47,6 +63,12 @@ def main():
                     help="also run the whole search (epochs x (steps/epoch train steps + validation)) and report "
                          "its measured wall clock next to the projection (-1: on for the b5 config)")
     args = ap.parse_args()
+
+    # trials/hour (BASELINE config 2) first, from rank 0, before this process touches the GPU:
+    # the scheduler's warm workers then own every GPU while the experiment runs
+    tph = None
+    if args.trials > 0 and int(os.environ.get("RANK", "0")) == 0:
+        tph = trials_per_hour(args.gpus, args.trials)
 
     import torch
 
@@ -76,7 +98,10 @@ def main():
     n_train = 50000
     ds = cifar10(dev, n=n_train)
     train, valid = ds.subset(0, n_train // 2), ds.subset(n_train // 2, n_train)
-    bs = args.batch
+    if args.scaling == "strong":
+        bs = max(1, args.batch // comm.world_size)  # global batch stays args.batch
+    else:
+        bs = args.batch
     tb = train.batches(bs, seed=0, shard=comm.rank, num_shards=comm.world_size, drop_last=True)
     vb = valid.batches(bs, seed=1, shard=comm.rank, num_shards=comm.world_size, drop_last=True)
     batches = []
@@ -139,6 +164,27 @@ def main():
         comm.barrier()
         sync()
         full_s = comm.allreduce_max(time.perf_counter() - t2)
+
+    # same-node comparator: the PyTorch op backend, eager (no graph), same config and batch
+    torch_ms = None
+    if args.comparator_steps > 0 and dev.type == "cuda":
+        dops.set_backend("torch")
+        ref = DartsSearch(layout, dev, comm, capture=False)
+        for i in range(2):
+            (tx, ty), (vx, vy) = batches[i % len(batches)]
+            ref.step(tx, ty, vx, vy)
+        sync()
+        comm.barrier()
+        sync()
+        t3 = time.perf_counter()
+        for i in range(args.comparator_steps):
+            (tx, ty), (vx, vy) = batches[i % len(batches)]
+            ref.step(tx, ty, vx, vy)
+        sync()
+        comm.barrier()
+        sync()
+        torch_ms = comm.allreduce_max((time.perf_counter() - t3) * 1000.0 / args.comparator_steps)
+        dops.set_backend(args.ops)
     if comm.rank == 0:
         out = {
             "metric": "darts_cifar10_search_wall_clock_s",
@@ -149,14 +195,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": False,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": round(wall / B5_SECONDS, 5) if args.config == "b5" else None,
             "dtype": "fp32",
             "data": "synthetic (CIFAR-10-shaped, device-resident); random-init weights",
             "config": {"model": "darts-cnn-cifar10 supernet (%s: C=%d, L=%d, N=%d, stem x%d, 6 primitives + none)"
                                 % (args.config, cfg["init_channels"], cfg["num_layers"], cfg["num_nodes"],
                                    cfg["stem_multiplier"]),
-                       "global_batch": bs * comm.world_size, "seq_len": None,
+                       "global_batch": bs * comm.world_size, "per_gpu_batch": bs, "seq_len": None,
                        "parallelism": "dp%d" % comm.world_size, "epochs": cfg["epochs"],
                        "steps_per_epoch": steps_per_epoch, "ops": args.ops, "hip_graph": bool(search.capture),
                        "allreduce": ("xgmi-oneshot" if comm.xgmi is not None else "rccl") if comm.distributed else None,
@@ -166,9 +212,40 @@ def main():
             "train_images_per_s": round(bs * comm.world_size * 1000.0 / ms_step, 1),
             "final_loss": round(loss, 4),
             "baseline_b5_s": B5_SECONDS,
+            "torch_eager_ms_per_step": round(torch_ms, 3) if torch_ms is not None else None,
+            "speedup_vs_torch_eager": round(torch_ms / ms_step, 2) if torch_ms else None,
+            "trials_per_hour": tph,
         }
         print(json.dumps(out), flush=True)
     comm.destroy()
+
+
+def trials_per_hour(gpus: int, per_gpu: int):
+    """BASELINE config 2 (TPE over the MNIST MLP, examples/hp-tuning/tpe-mnist-mlp.yaml) end to
+    end through the in-process scheduler: parallelTrialCount = one trial per GPU,
+    ``per_gpu`` trials per GPU, 3 epochs of 60k rows each. Completed trials per hour of wall
+    clock from experiment creation to completion (includes warm-worker start). B1, the
+    reference's 36.3 trials/h, is a 12-trial random search at parallelTrialCount=3 on a K8s
+    CPU cluster (docs/workflow-design.md:41-164): same kind of experiment, not the same
+    trial program (the reference's MXNet MLP image is not in the reference tree)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    cmd = [sys.executable, os.path.join(here, "bench_trials.py"), "--trials", str(per_gpu * gpus), "--parallel",
+           str(gpus), "--gpus", str(gpus), "--slots-per-gpu", "1", "--epochs", "3"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not line:
+            print("trials/hour experiment failed: %s" % (r.stderr[-2000:],), file=sys.stderr)
+            return None
+        res = json.loads(line[-1])
+    except (subprocess.TimeoutExpired, ValueError) as e:
+        print("trials/hour experiment failed: %s" % e, file=sys.stderr)
+        return None
+    return {"value": res["value"], "unit": "trials/h", "n_gpus": gpus, "vs_b1": res["vs_baseline"],
+            "wall_s": res["wall_s"], "trials_completed": res["trials_completed"],
+            "trials_succeeded": res["trials_succeeded"], "best_validation_accuracy": res["best_validation_accuracy"],
+            "config": "tpe-mnist-mlp: %d trials, parallel %d (1 per GPU), 3 epochs x 60k, warm workers"
+                      % (res["trials_completed"], gpus), "b1_trials_per_hour": 36.3}
 
 
 if __name__ == "__main__":

@@ -50,7 +50,8 @@ def main():
     e = load_experiment(os.path.join(os.path.dirname(os.path.abspath(__file__)), "examples", "hp-tuning",
                                      "tpe-mnist-mlp.yaml"))
     e.spec.max_trial_count = args.trials
-    e.spec.parallel_trial_count = args.parallel
+    e.spec.parallel_trial_count = min(args.parallel, args.trials)
+    e.spec.max_failed_trial_count = min(e.spec.max_failed_trial_count or 0, args.trials)
     e.spec.objective.goal = None
     e.spec.algorithm.algorithm_name = args.algorithm
     if args.algorithm != "tpe":

@@ -47,6 +47,9 @@ class AmdConfig:
     fault_quarantine_threshold: int = 3
     poll_interval_ms: int = 20
     map_collector_paths: bool = True
+    # a Job / LocalProcess trial with amd.com/gpu: N > 1 runs as N rank processes ("ranks", one
+    # process per GPU with the torchrun env) or as one process seeing all N GPUs ("single")
+    multi_gpu_launch: str = "ranks"
 
 
 @dataclass

@@ -16,6 +16,18 @@ object. Supported kinds:
   primary-pod semantics (``inject_webhook.go:143-148``).
 * ``LocalProcess`` (native kind, ``apiVersion: katib-amd.io/v1``): ``command`` for
   a subprocess or ``entrypoint: module:function`` to run in a warm GPU worker.
+
+A ``Job`` / ``LocalProcess`` trial that asks for N > 1 GPUs runs as N *rank* processes
+(one process per GPU, the MI355X way to drive several GPUs) with the torchrun env
+(``RANK``, ``WORLD_SIZE``, ``LOCAL_RANK``, ``LOCAL_WORLD_SIZE``, ``MASTER_ADDR``,
+``MASTER_PORT``); rank 0 is the primary whose output the metrics collector parses, the
+way the reference collects from the primary pod only. This replaces the reference's
+one-process-over-all-GPUs trials (the ENAS child's ``MirroredStrategy``,
+``examples/v1beta1/trial-images/enas-cnn-cifar10/RunTrial.py:54-63``). A program that
+drives every GPU itself opts out with the container env ``KATIB_AMD_LAUNCH=single`` (or
+``amd.multi_gpu_launch: single`` in the KatibConfig). Every rank - and every replica of a
+training-operator job - sees the trial's whole device list and picks
+``LOCAL_RANK % device_count`` (``parallel/comm.py``).
 * ``Function``: SDK ``tune()`` objective source executed in a warm worker.
 
 The job status handed to the GJSON success/failure conditions is synthesised in
@@ -64,6 +76,7 @@ class LaunchPlan:
     replicas: List[ReplicaPlan] = field(default_factory=list)
     deadline: float = 0.0
     backoff_limit: int = 0
+    share_devices: bool = False  # every replica sees all the trial's devices (rank plans, training jobs)
 
     @property
     def primary(self) -> ReplicaPlan:
@@ -126,7 +139,39 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Optional[Dict[str, str]] = None) -> LaunchPlan:
+LAUNCH_MODES = ("ranks", "single")
+
+
+def rank_env(rank: int, world: int, port: int) -> Dict[str, str]:
+    """torchrun-style env of one rank of a single-node job."""
+    return {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world), "RANK": str(rank),
+            "LOCAL_RANK": str(rank), "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "NODE_RANK": "0"}
+
+
+def _ranked(plan: LaunchPlan, base: ReplicaPlan, mode: str) -> LaunchPlan:
+    """Expand a single-process replica that asks for N > 1 GPUs into N rank processes."""
+    mode = base.env.get("KATIB_AMD_LAUNCH", mode)
+    if mode not in LAUNCH_MODES:
+        raise JobSpecError("KATIB_AMD_LAUNCH must be one of %s, got %r" % ("/".join(LAUNCH_MODES), mode))
+    if base.gpus <= 1 or mode == "single":
+        plan.replicas.append(base)
+        return plan
+    port = free_port()
+    plan.share_devices = True
+    # split the CPU threads between the ranks (torchrun does the same): N ranks each spinning
+    # a full OpenMP pool on a CPU-side collective oversubscribe the host by N x
+    threads = max(1, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1) // base.gpus)
+    for r in range(base.gpus):
+        env = {"OMP_NUM_THREADS": str(threads)}
+        env.update(base.env)
+        env.update(rank_env(r, base.gpus, port))
+        plan.replicas.append(ReplicaPlan("primary" if r == 0 else "rank", r, list(base.argv), env, base.cwd, 1,
+                                         r == 0, entrypoint=base.entrypoint, function=base.function))
+    return plan
+
+
+def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Optional[Dict[str, str]] = None,
+              multi_gpu_launch: str = "ranks") -> LaunchPlan:
     kind = run_spec.get("kind", "")
     spec = run_spec.get("spec") or {}
     if kind == C.JOB_KIND_JOB:
@@ -134,8 +179,8 @@ def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Option
         c = _container(pod, primary_container)
         plan = LaunchPlan(kind=kind, deadline=float(spec.get("activeDeadlineSeconds") or 0),
                           backoff_limit=int(spec["backoffLimit"]) if "backoffLimit" in spec else 0)
-        plan.replicas.append(ReplicaPlan("primary", 0, _argv(c), _env(c), c.get("workingDir"), _gpus(c), True))
-        return plan
+        return _ranked(plan, ReplicaPlan("primary", 0, _argv(c), _env(c), c.get("workingDir"), _gpus(c), True),
+                       multi_gpu_launch)
     if kind == C.JOB_KIND_LOCAL:
         plan = LaunchPlan(kind=kind, deadline=float(spec.get("activeDeadlineSeconds") or 0),
                           backoff_limit=int(spec.get("backoffLimit") or 0))
@@ -143,14 +188,14 @@ def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Option
         args = [str(a) for a in spec.get("args") or []]
         gpus = int(spec.get("gpus") or 0)
         if spec.get("entrypoint"):
-            plan.replicas.append(ReplicaPlan("primary", 0, args, env, spec.get("workingDir"), gpus, True,
-                                             entrypoint=spec["entrypoint"]))
+            base = ReplicaPlan("primary", 0, args, env, spec.get("workingDir"), gpus, True,
+                               entrypoint=spec["entrypoint"])
         else:
             cmd = [str(a) for a in spec.get("command") or []] + args
             if not cmd:
                 raise JobSpecError("LocalProcess needs spec.command or spec.entrypoint")
-            plan.replicas.append(ReplicaPlan("primary", 0, cmd, env, spec.get("workingDir"), gpus, True))
-        return plan
+            base = ReplicaPlan("primary", 0, cmd, env, spec.get("workingDir"), gpus, True)
+        return _ranked(plan, base, multi_gpu_launch)
     if kind == "Function":
         plan = LaunchPlan(kind=kind, deadline=float(spec.get("activeDeadlineSeconds") or 0))
         env = {e["name"]: str(e["value"]) for e in spec.get("env") or [] if "value" in e}
@@ -166,7 +211,7 @@ def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Option
         if not rspecs:
             raise JobSpecError("%s has no %s" % (kind, key))
         plan = LaunchPlan(kind=kind, deadline=float((spec.get("runPolicy") or {}).get("activeDeadlineSeconds")
-                                                    or spec.get("activeDeadlineSeconds") or 0))
+                                                    or spec.get("activeDeadlineSeconds") or 0), share_devices=True)
         primary_role = _PRIMARY_ROLE[kind]
         if kind == "TFJob" and "Chief" not in rspecs and "Master" in rspecs:
             primary_role = "Master"
@@ -187,10 +232,14 @@ def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Option
             c = _container(pod, primary_container)
             n = int(rs.get("replicas", 1))
             for i in range(n):
-                env = _env(c)
+                env = {"OMP_NUM_THREADS": str(max(1, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+                                                  // max(1, world)))}
+                env.update(_env(c))
                 if kind in ("PyTorchJob", "XGBoostJob"):
-                    env.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
-                                "RANK": str(rank), "LOCAL_RANK": str(rank), "PET_NNODES": str(world)})
+                    # all replicas run on this node: LOCAL_RANK = RANK, and every replica sees the
+                    # trial's devices (share_devices), so rank r drives device r % device_count
+                    env.update(rank_env(rank, world, port))
+                    env["PET_NNODES"] = str(world)
                 elif kind == "TFJob":
                     env["TF_CONFIG"] = json.dumps({"cluster": cluster, "task": {"type": role.lower(), "index": i}})
                 elif kind == "MXJob":

@@ -83,6 +83,7 @@ class TrialRun:
     path_map: Dict[str, str] = field(default_factory=dict)
     deleted: bool = False
     scraper: Optional[object] = None  # PrometheusMetric collector (metricscollector/prometheus.py)
+    prom_final: str = ""  # KATIB_PROMETHEUS_FINAL snapshot path
 
 
 @dataclass
@@ -287,8 +288,16 @@ class Manager:
         if timeout_ms is None:
             timeout_ms = self.config.amd.poll_interval_ms
         events = self.runtime.poll(timeout_ms)
+        # PrometheusMetric scrapes are blocking HTTP reads: take the due list under the lock,
+        # scrape without it, record the results under it again
         with self._lock:
-            self._scrape_prometheus()
+            due = self._due_scrapes()
+        scraped = [(tkey, sc.scrape()) for tkey, sc in due]
+        with self._lock:
+            for tkey, logs in scraped:
+                run = self.runs.get(tkey)
+                if logs and run is not None and run.scraper is not None and not run.deleted:
+                    self.store.report(tkey[1], logs)
             for ev in events:
                 self._on_runtime_event(ev)
             for key in list(self.experiments):
@@ -743,7 +752,7 @@ class Manager:
             if run.plan is None:
                 try:
                     run.plan = make_plan(trial.spec.run_spec, trial.spec.primary_container_name or "",
-                                         trial.spec.primary_pod_labels)
+                                         trial.spec.primary_pod_labels, self.config.amd.multi_gpu_launch)
                 except JobSpecError as e:
                     self._finish_trial(tkey, "Failed", "JobSpecInvalid", str(e))
                     continue
@@ -830,19 +839,25 @@ class Manager:
             mpath = (hg.path if hg is not None and hg.path else C.DEFAULT_PROMETHEUS_PATH)
             port = free_port()  # one port per trial: concurrent trials cannot share the spec's
             run.scraper = Scraper(port, mpath, run.collector["metric_names"])
-            prom_env = {"KATIB_PROMETHEUS_PORT": str(port), "KATIB_PROMETHEUS_PATH": mpath}
+            run.prom_final = os.path.join(run.trial_dir, "prometheus_final.prom")
+            if os.path.exists(run.prom_final):
+                os.remove(run.prom_final)  # a retry must not read the previous attempt's snapshot
+            prom_env = {"KATIB_PROMETHEUS_PORT": str(port), "KATIB_PROMETHEUS_PATH": mpath,
+                        "KATIB_PROMETHEUS_FINAL": run.prom_final}
         log_path = os.path.join(run.trial_dir, "metrics.log")
         base_env = {"KATIB_TRIAL_NAME": name, "KATIB_EXPERIMENT_NAME": exp_name, "KATIB_TRIAL_DIR": run.trial_dir,
                     "KATIB_NAMESPACE": ns, "PYTHONUNBUFFERED": "1",
-                    "HIP_VISIBLE_DEVICES": ",".join(str(d) for d in run.devices) if run.devices else "",
+                    "HIP_VISIBLE_DEVICES": ",".join(str(d) for d in sorted(set(run.devices))),
                     "KATIB_AMD_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or "",
                     "KATIB_TRIAL_CHECKPOINT_DIR": extra_map and list(extra_map.values())[0] or "",
                     # trials may run the built-in workloads with `python -m katib_amd.workloads.X`
                     "PYTHONPATH": os.pathsep.join(p for p in (_PKG_ROOT, os.environ.get("PYTHONPATH", "")) if p)}
         base_env.update(prom_env)
-        # each replica gets its share of the trial's devices
+        # each replica gets its share of the trial's devices; rank plans and training-operator
+        # jobs see all of them (a rank picks LOCAL_RANK % device_count, parallel/comm.py)
         dev_iter = iter(run.devices)
         plan = run.plan
+        all_devs = sorted(set(run.devices))
         run.attempt += 1
         run.phase = "Launching"
         run.started = time.time()
@@ -855,7 +870,8 @@ class Manager:
             devs = [next(dev_iter) for _ in range(rep.gpus)] if run.devices else []
             env = dict(base_env)
             if run.devices:
-                env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devs) if devs else ""
+                vis = all_devs if plan.share_devices else sorted(set(devs))
+                env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in vis)
             env.update({k: map_paths([v], run.path_map)[0] for k, v in rep.env.items()})
             if "PYTHONPATH" in rep.env:
                 env["PYTHONPATH"] = os.pathsep.join((env["PYTHONPATH"], _PKG_ROOT))
@@ -867,7 +883,8 @@ class Manager:
             if not rep.primary:
                 run.aux.append(proc_name)
             self._proc_to_trial[proc_name] = tkey
-            if (rep.entrypoint or rep.function) and rep.gpus <= 1 and self.config.amd.warm_workers:
+            if (rep.entrypoint or rep.function) and rep.gpus <= 1 and len(plan.replicas) == 1 \
+                    and self.config.amd.warm_workers:
                 payload = {"trial": name, "env": env, "cwd": cwd}
                 if rep.function:
                     payload["function"] = rep.function
@@ -1002,6 +1019,10 @@ class Manager:
         code = ev["exit_code"]
         if run.collector.get("kind") == 2:
             self._collect_tfevent(trial, run)
+        if run.scraper is not None and run.prom_final:
+            logs = run.scraper.read_final(run.prom_final)  # the value published right before exit
+            if logs:
+                self.store.report(tkey[1], logs)
         outcome = SE.classify_exit(bool(ev["early_stopped"]), code, ev["worker"] >= 0, bool(run.early_stopped),
                                    bool(ev["deadline_exceeded"]), TC.is_killed(trial), run.attempt,
                                    run.plan.backoff_limit)
@@ -1018,16 +1039,17 @@ class Manager:
             msg = ev["message"] or ""
             self._finish_trial(tkey, "Failed", "Error", "exit code %d%s" % (code, (": " + msg) if msg else ""))
 
-    def _scrape_prometheus(self):
-        """PrometheusMetric collector: scrape every running trial whose interval is due."""
+    def _due_scrapes(self):
+        """PrometheusMetric collector: running trials whose scrape interval is due."""
         now = time.time()
+        out = []
         for tkey, run in self.runs.items():
             sc = run.scraper
             if sc is None or run.phase not in ("Launching", "Running") or not sc.due(now):
                 continue
-            logs = sc.scrape(now)
-            if logs:
-                self.store.report(tkey[1], logs)
+            sc.next_at = now + sc.interval  # not due again while this scrape is in flight
+            out.append((tkey, sc))
+        return out
 
     def _collect_tfevent(self, trial, run):
         from ..metricscollector.tfevent import collect

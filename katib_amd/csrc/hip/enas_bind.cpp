@@ -136,4 +136,8 @@ void register_enas(py::module& m) {
   m.def("enas_n_params", [](int64_t H, int64_t n_ops) { return E::offsets(H, n_ops).n; });
   m.def("enas_lds_bytes", [](int64_t H, int64_t n_ops, int64_t L) { return E::lds_bytes(H, n_ops, L); });
   m.attr("ENAS_LOG_FIELDS") = E::kLogFields;
+  m.attr("ENAS_MAX_H") = E::kMaxH;
+  m.attr("ENAS_MAX_OPS") = E::kMaxOps;
+  m.attr("ENAS_MAX_LAYERS") = E::kMaxLayers;
+  m.attr("ENAS_LDS_LIMIT") = 160 * 1024;
 }

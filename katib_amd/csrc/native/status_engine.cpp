@@ -41,8 +41,7 @@ std::string objective_value(const TrialFacts& t) {
 TrialsSummary summarize_trials(const std::vector<TrialFacts>& trials, ObjectiveType type, bool has_goal,
                                double goal) {
   TrialsSummary s;
-  double best_val = 0.0;
-  bool have_best_val = false;
+  double best_val = 0.0;  // bestTrialValue starts at 0 (status_util.go)
   for (int i = 0; i < static_cast<int>(trials.size()); ++i) {
     const TrialFacts& t = trials[i];
     s.buckets[static_cast<int>(classify(t.conditions))].push_back(i);
@@ -53,9 +52,11 @@ TrialsSummary summarize_trials(const std::vector<TrialFacts>& trials, ObjectiveT
       s.best = i;  // non-numeric metric: the latest trial wins (status_util.go:99-104)
       continue;
     }
-    if (s.best == -1 || !have_best_val) {
+    // Reference semantics, kept exactly: only the FIRST trial with any metric initialises
+    // the best value; when a non-numeric metric set best first, numeric trials compare
+    // against the zero-initialised value (status_util.go:99-110).
+    if (s.best == -1) {
       best_val = x;
-      have_best_val = true;
       s.best = i;
     }
     if (type == ObjectiveType::Minimize) {

@@ -135,6 +135,16 @@ static void test_slots_concurrent() {
   pool.record_fault(3, 2);
   pool.record_fault(3, 2);
   CHECK(pool.quarantined().size() == 1 && pool.capacity() == 14);
+  // multi-slot trials: distinct devices first, then stacked slots
+  SlotPool one(1, 2);
+  auto two = one.acquire(2);
+  CHECK(two.size() == 2 && two[0] == 0 && two[1] == 0 && one.free_slots() == 0);
+  CHECK(one.acquire(1).empty());
+  SlotPool four(4, 2);
+  auto a = four.acquire(3);
+  CHECK(a.size() == 3 && a[0] != a[1] && a[1] != a[2]);
+  auto b = four.acquire(5);
+  CHECK(b.size() == 5 && four.free_slots() == 0);
 }
 
 static void test_runtime() {

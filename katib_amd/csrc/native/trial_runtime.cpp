@@ -38,16 +38,34 @@ std::vector<int> SlotPool::acquire(int n) {
   std::vector<int> out;
   if (n <= 0) return out;
   // least-loaded devices first so parallel trials spread one per GPU
+  // A multi-GPU trial takes n slots on n distinct devices when it can; with more slots
+  // than devices per trial (slots_per_device > 1, e.g. a 2-rank trial on a 1-GPU box)
+  // the remaining slots are stacked on the least-loaded devices already chosen.
   std::vector<int> order;
+  int free_total = 0;
   for (int d = 0; d < n_; ++d)
-    if (!bad_.count(d) && used_[d] < per_) order.push_back(d);
+    if (!bad_.count(d) && used_[d] < per_) {
+      order.push_back(d);
+      free_total += per_ - used_[d];
+    }
+  if (free_total < n) return out;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return used_[a] < used_[b]; });
-  if (static_cast<int>(order.size()) < n) return out;
-  for (int i = 0; i < n; ++i) {
-    used_[order[i]]++;
-    out.push_back(order[i]);
+  std::vector<int> take(n_, 0);
+  int got = 0;
+  while (got < n) {  // round-robin over the candidates: distinct devices first
+    for (int d : order) {
+      if (got == n) break;
+      if (used_[d] + take[d] < per_) {
+        take[d]++;
+        got++;
+      }
+    }
   }
-  std::sort(out.begin(), out.end());
+  for (int d = 0; d < n_; ++d)
+    for (int k = 0; k < take[d]; ++k) {
+      used_[d]++;
+      out.push_back(d);
+    }
   return out;
 }
 

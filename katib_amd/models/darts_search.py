@@ -326,6 +326,15 @@ class DartsSearch:
     def set_lr(self, lr: float):
         self.lr.fill_(lr)
 
+    def sync_bn_stats(self):
+        """Average the BN running statistics over the ranks (each rank tracks its own shard's
+        batch statistics, like DDP without SyncBN) so that every rank validates with the same
+        model. The mean of per-rank running variances ignores the spread of the per-rank
+        means, a second-order term at equal shard sizes."""
+        if self.comm.distributed:
+            self.comm.allreduce_mean_(self.bn.mean)
+            self.comm.allreduce_mean_(self.bn.var)
+
     def step(self, tx, ty, vx, vy):
         if self.static is None:
             self.static = {"tx": tx.clone(), "ty": ty.clone(), "vx": vx.clone(), "vy": vy.clone()}

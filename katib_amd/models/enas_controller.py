@@ -197,8 +197,17 @@ class EnasControllerHip(EnasController):
         import importlib
 
         self._K = importlib.import_module("katib_amd._hipkern")  # raises if the extension is not built
-        if self.H > 64:
+        K = self._K
+        # every kernel limit is checked here, at construction, so make_controller("auto") can
+        # fall back to the torch controller instead of failing later in enas_sample/enas_train
+        if self.H > min(64, getattr(K, "ENAS_MAX_H", 64)):
             raise ValueError("the HIP ENAS controller supports controller_hidden_size <= 64")
+        if not 1 <= self.num_operations <= getattr(K, "ENAS_MAX_OPS", 1024):
+            raise ValueError("the HIP ENAS controller supports at most %d operations" % K.ENAS_MAX_OPS)
+        if not 1 <= self.num_layers <= getattr(K, "ENAS_MAX_LAYERS", 64):
+            raise ValueError("the HIP ENAS controller supports at most %d layers" % K.ENAS_MAX_LAYERS)
+        if K.enas_lds_bytes(self.H, self.num_operations, self.num_layers) > getattr(K, "ENAS_LDS_LIMIT", 160 * 1024):
+            raise ValueError("the ENAS controller does not fit the 160 KB LDS of one CU")
         self.device = torch.device(device or "cuda")
         params = dict(self.named_parameters())
         self.flat = torch.cat([params[n].detach().reshape(-1) for n in PARAM_ORDER]).to(self.device).contiguous()
@@ -295,7 +304,13 @@ class EnasControllerHip(EnasController):
 
 def make_controller(backend: Optional[str] = None, **kw) -> EnasController:
     """``backend``: "hip" (MI355X kernel), "torch" (host oracle) or "auto" (default, env
-    ``KATIB_AMD_ENAS_BACKEND``): the HIP kernel when a GPU and the extension are present."""
+    ``KATIB_AMD_ENAS_BACKEND``): the HIP kernel when a GPU and the extension are present and
+    the search space fits its limits (operations, layers, 160 KB LDS).
+
+    The controller runs on the scheduler's current GPU (cuda:0 unless the scheduler process
+    is pinned): GetSuggestions shares that GPU with whatever trial is placed on it, for the
+    ~16 ms of one ENAS suggestion call (50 REINFORCE steps in one workgroup). Set
+    ``KATIB_AMD_ENAS_BACKEND=torch`` to keep the scheduler off the GPU entirely."""
     backend = (backend or os.environ.get("KATIB_AMD_ENAS_BACKEND", "auto")).lower()
     if backend == "torch":
         return EnasController(**kw)
@@ -304,6 +319,6 @@ def make_controller(backend: Optional[str] = None, **kw) -> EnasController:
     if torch.cuda.is_available() and kw.get("hidden_size", 64) <= 64:
         try:
             return EnasControllerHip(**kw)
-        except (ImportError, OSError):
+        except (ImportError, OSError, ValueError):  # no extension, or a kernel limit is exceeded
             pass
     return EnasController(**kw)

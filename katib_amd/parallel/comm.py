@@ -26,21 +26,40 @@ class Comm:
         self.xgmi = None  # one-shot xGMI all-reduce (parallel/xgmi.py), see enable_xgmi()
 
     @staticmethod
-    def from_env(device_type: Optional[str] = None) -> "Comm":
-        """torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT)."""
+    def from_env(device_type: Optional[str] = None, backend: Optional[str] = None) -> "Comm":
+        """torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / LOCAL_WORLD_SIZE / MASTER_ADDR /
+        MASTER_PORT), as set by ``torch.distributed.run`` or by the scheduler's rank plans
+        (``controller/jobs.py``).
+
+        Rank r drives visible device ``LOCAL_RANK % device_count``: every rank of a trial sees
+        the trial's whole device list. When there are more local ranks than devices (a 2-rank
+        trial placed on a 1-GPU box with ``slots_per_device: 2``) the ranks share a GPU, which
+        RCCL refuses, so the process group is gloo and the gradient all-reduce runs as the
+        one-shot IPC kernel (``parallel/xgmi.py``; host copies through gloo if that is off).
+        ``backend`` (a trial's ``--backend`` flag) or ``KATIB_AMD_DIST_BACKEND`` overrides the
+        choice, except that ``nccl`` on ranks sharing a device becomes gloo."""
         ws = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         lrank = int(os.environ.get("LOCAL_RANK", str(rank)))
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
         if device_type is None:
             device_type = "cuda" if torch.cuda.is_available() else "cpu"
+        shared = False
         if device_type == "cuda":
-            torch.cuda.set_device(lrank)
-            device = torch.device("cuda", lrank)
+            ndev = max(1, torch.cuda.device_count())
+            idx = lrank % ndev
+            shared = lws > ndev
+            torch.cuda.set_device(idx)
+            device = torch.device("cuda", idx)
         else:
             device = torch.device("cpu")
+        want = backend
         backend = None
         if ws > 1:
-            backend = "nccl" if device_type == "cuda" else "gloo"
+            backend = want or os.environ.get("KATIB_AMD_DIST_BACKEND") or (
+                "nccl" if device_type == "cuda" and not shared else "gloo")
+            if backend == "nccl" and (shared or device_type != "cuda"):
+                backend = "gloo"
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 kw = {}
@@ -57,7 +76,7 @@ class Comm:
     def enable_xgmi(self) -> bool:
         """Collective: set up the one-shot xGMI all-reduce for small float32 messages
         (falls back to RCCL when unavailable, disabled or failing its self-test)."""
-        if self.xgmi is None and self.world_size > 1 and self.backend == "nccl":
+        if self.xgmi is None and self.world_size > 1 and self.device.type == "cuda":
             from . import xgmi
 
             self.xgmi = xgmi.create(self)
@@ -111,7 +130,7 @@ class Comm:
     def barrier(self):
         if self.world_size > 1:
             if self.backend == "nccl":
-                dist.barrier(device_ids=[self.local_rank])
+                dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
 

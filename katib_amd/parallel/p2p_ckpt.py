@@ -18,14 +18,16 @@ it, so the child reads them straight from that GPU:
 The files written by :func:`torch.save` stay the durable copy (FromVolume resume,
 crash of the producer): :func:`fetch` returns ``None`` whenever the producer is
 gone or the handle cannot be mapped, and the caller falls back to the files.
-The handle file is a pickle written by this module only.
+The handle file is JSON: plain integers and hex strings for the IPC handles, and names
+from a fixed whitelist for the tensor / storage classes and dtypes. The checkpoint
+directory is writable by the trial (user code), so nothing in it is ever unpickled.
 """
 
 from __future__ import annotations
 
 import collections
+import json
 import os
-import pickle
 import socket
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -44,10 +46,13 @@ def _flatten(obj, tensors: List[torch.Tensor]):
         tensors.append(obj)
         return {"__tensor__": len(tensors) - 1}
     if isinstance(obj, dict):
-        return {k: _flatten(v, tensors) for k, v in obj.items()}
+        if all(isinstance(k, str) for k in obj) and not ({"__tensor__", "__tuple__", "__items__"} & set(obj)):
+            return {k: _flatten(v, tensors) for k, v in obj.items()}
+        # non-string keys (an optimizer state_dict's parameter ids) survive JSON as pairs
+        return {"__items__": [[k, _flatten(v, tensors)] for k, v in obj.items()]}
     if isinstance(obj, (list, tuple)):
         out = [_flatten(v, tensors) for v in obj]
-        return out if isinstance(obj, list) else ("__tuple__", out)
+        return out if isinstance(obj, list) else {"__tuple__": out}
     return obj
 
 
@@ -55,12 +60,45 @@ def _unflatten(obj, tensors: List[torch.Tensor]):
     if isinstance(obj, dict):
         if set(obj) == {"__tensor__"}:
             return tensors[obj["__tensor__"]]
+        if set(obj) == {"__tuple__"}:
+            return tuple(_unflatten(v, tensors) for v in obj["__tuple__"])
+        if set(obj) == {"__items__"}:
+            return {(k if not isinstance(k, list) else tuple(k)): _unflatten(v, tensors) for k, v in obj["__items__"]}
         return {k: _unflatten(v, tensors) for k, v in obj.items()}
-    if isinstance(obj, tuple) and len(obj) == 2 and obj[0] == "__tuple__":
-        return tuple(_unflatten(v, tensors) for v in obj[1])
     if isinstance(obj, list):
         return [_unflatten(v, tensors) for v in obj]
     return obj
+
+
+_DTYPES = {str(d): d for d in (torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64, torch.int32,
+                                torch.int16, torch.int8, torch.uint8, torch.bool)}
+
+
+def _storage_classes():
+    return {c.__name__: c for c in (torch.UntypedStorage, torch.storage.TypedStorage)}
+
+
+def _encode_handle(args) -> List:
+    """The rebuild_cuda_tensor argument tuple of ``reduce_tensor`` as JSON values."""
+    (tensor_cls, size, stride, toff, storage_cls, dtype, device, handle, sbytes, soff, req, rc_handle, rc_off,
+     ev_handle, ev_sync) = args
+    if tensor_cls is not torch.Tensor or storage_cls.__name__ not in _storage_classes():
+        raise TypeError("unsupported tensor/storage class for a P2P checkpoint")
+    hx = lambda b: b.hex() if isinstance(b, (bytes, bytearray)) else None  # noqa: E731
+    return [list(size), list(stride), int(toff), storage_cls.__name__, str(dtype), int(device), hx(handle),
+            int(sbytes), int(soff), bool(req), hx(rc_handle), int(rc_off), hx(ev_handle), bool(ev_sync)]
+
+
+def _decode_handle(v: List):
+    """Inverse of :func:`_encode_handle`; only whitelisted classes and dtypes are accepted."""
+    (size, stride, toff, sname, dname, device, handle, sbytes, soff, req, rc_handle, rc_off, ev_handle,
+     ev_sync) = v
+    scls = _storage_classes()[str(sname)]
+    dtype = _DTYPES[str(dname)]
+    fb = lambda h: bytes.fromhex(h) if isinstance(h, str) else None  # noqa: E731
+    return (torch.Tensor, torch.Size([int(x) for x in size]), tuple(int(x) for x in stride), int(toff), scls, dtype,
+            int(device), fb(handle), int(sbytes), int(soff), bool(req), fb(rc_handle), int(rc_off), fb(ev_handle),
+            bool(ev_sync))
 
 
 def publish(state: Any, ckpt_dir: str, key: Optional[str] = None) -> bool:
@@ -89,7 +127,7 @@ def publish(state: Any, ckpt_dir: str, key: Optional[str] = None) -> bool:
                 layout[i] = (str(dt), off, tuple(tensors[i].shape), n)
                 off += n
             bufs.append(buf)
-            handles[str(dt)] = reduce_tensor(buf)[1]
+            handles[str(dt)] = _encode_handle(reduce_tensor(buf)[1])
     torch.cuda.current_stream(dev).synchronize()
     key = key or os.path.abspath(ckpt_dir)
     _CACHE[key] = bufs
@@ -98,9 +136,9 @@ def publish(state: Any, ckpt_dir: str, key: Optional[str] = None) -> bool:
         _CACHE.popitem(last=False)
     os.makedirs(ckpt_dir, exist_ok=True)
     tmp = os.path.join(ckpt_dir, HANDLE_FILE + ".tmp")
-    with open(tmp, "wb") as f:
-        pickle.dump({"pid": os.getpid(), "host": socket.gethostname(), "device": dev.index, "key": key,
-                     "skeleton": skeleton, "layout": layout, "handles": handles}, f)
+    with open(tmp, "w") as f:
+        json.dump({"pid": os.getpid(), "host": socket.gethostname(), "device": dev.index, "key": key,
+                   "skeleton": skeleton, "layout": layout, "handles": handles}, f)
     os.replace(tmp, os.path.join(ckpt_dir, HANDLE_FILE))
     return True
 
@@ -120,8 +158,11 @@ def fetch(ckpt_dir: str, device: Optional[torch.device] = None) -> Optional[Any]
     path = os.path.join(ckpt_dir, HANDLE_FILE)
     if not torch.cuda.is_available() or not os.path.exists(path):
         return None
-    with open(path, "rb") as f:
-        meta = pickle.load(f)  # written by publish() above
+    try:
+        with open(path) as f:
+            meta = json.load(f)  # data only: classes/dtypes are resolved through whitelists
+    except (OSError, ValueError):
+        return None
     if meta.get("host") != socket.gethostname() or not _alive(int(meta["pid"])):
         return None
     device = device or torch.device("cuda", torch.cuda.current_device())
@@ -132,8 +173,8 @@ def fetch(ckpt_dir: str, device: Optional[torch.device] = None) -> Optional[Any]
             local[str(b.dtype)] = b.to(device, copy=True)
     if not local:
         try:
-            for dt, args in meta["handles"].items():
-                src = rebuild_cuda_tensor(*args)
+            for dt, enc in meta["handles"].items():
+                src = rebuild_cuda_tensor(*_decode_handle(enc))
                 dst = torch.empty(src.numel(), dtype=src.dtype, device=device)
                 dst.copy_(src)  # device-to-device: xGMI peer copy across GPUs
                 torch.cuda.synchronize(device)

@@ -7,6 +7,14 @@ per-epoch validation and the final ``Best-Genotype=Genotype(...)`` line collecte
 with the ``([\\w-]+)=(Genotype.*)`` filter. MI355X additions: data-parallel search
 across the trial's GPUs (``WORLD_SIZE`` ranks, RCCL), HIP-graph capture of the
 search step, the HIP op backend, and synthetic device-resident CIFAR-10.
+
+Data parallelism keeps the reference's algorithm: ``batch_size`` is the *global* batch
+(the reference's single-GPU batch) and each of the W ranks takes ``batch_size / W`` rows of
+it, so a 1-GPU and an 8-GPU search take the same number of steps per epoch over the same
+data. BN batch statistics are per rank (DDP semantics, no SyncBN); the running statistics
+used by validation are averaged over the ranks before every validation pass, and the
+validation accuracy is the global one, ``sum(correct) / sum(n)`` over all ranks' shards
+(the reference averages over the whole valid split, ``run_trial.py:225-255``).
 """
 
 from __future__ import annotations
@@ -36,6 +44,27 @@ def _strip(s: str) -> str:
     if len(s) >= 2 and s[0] == s[-1] == '"':
         s = s[1:-1]
     return s
+
+
+def validate(search, comm, batches, max_batches: int = 0):
+    """Validation pass over this rank's shard -> global (mean loss, top-1) over all ranks.
+
+    BN running statistics are first averaged over the ranks (``sync_bn_stats``); the loss
+    and correct counts accumulate on the device (no host sync per batch) and one all-reduce
+    of [sum loss*n, sum correct, n] gives ``sum(correct) / sum(n)`` over the whole split."""
+    import torch
+
+    search.sync_bn_stats()
+    acc = torch.zeros(3, dtype=torch.float64, device=search.device)
+    for i, (vx, vy) in enumerate(batches):
+        if max_batches and i >= max_batches:
+            break
+        loss, top1, _ = search.evaluate(vx, vy)
+        acc[:2] += torch.stack([loss, top1]).double() * vy.numel()
+        acc[2] += vy.numel()
+    comm.allreduce_sum_(acc)
+    tot_loss, correct, n = acc.tolist()
+    return tot_loss / max(n, 1.0), correct / max(n, 1.0)
 
 
 def main(argv=None):
@@ -68,7 +97,11 @@ def main(argv=None):
     ds = cifar10(dev, n=args.num_train)
     split = args.num_train // 2
     train, valid = ds.subset(0, split), ds.subset(split, args.num_train)
-    bs = int(st["batch_size"])
+    gbs = int(st["batch_size"])  # global batch
+    bs = max(1, gbs // comm.world_size)  # per-rank share
+    if comm.rank == 0 and bs * comm.world_size != gbs:
+        print(">>> batch_size %d is not divisible by %d ranks: global batch %d" % (gbs, comm.world_size,
+                                                                                   bs * comm.world_size))
     epochs = int(st["num_epochs"])
     lr_max, lr_min = float(st["w_lr"]), float(st["w_lr_min"])
     print_step = int(st["print_step"])
@@ -91,18 +124,11 @@ def main(argv=None):
                 loss, top1, top5 = search.train_metrics(ty)
                 print("Train: [%2d/%d] Step %03d/%03d Loss %.3f Prec@(1,5) (%.1f%%, %.1f%%)"
                       % (epoch + 1, epochs, step, nsteps - 1, loss, 100 * top1, 100 * top5), flush=True)
-        # validation (no_grad forward over the valid split)
-        tot, c1, n = 0.0, 0.0, 0
-        for vx, vy in valid.batches(bs, seed=5000 + epoch, shard=comm.rank, num_shards=comm.world_size,
-                                    drop_last=True):
-            if args.max_steps and n >= args.max_steps * bs:
-                break
-            loss, top1, _ = search.evaluate(vx, vy)
-            tot += float(loss) * vy.numel()
-            c1 += float(top1) * vy.numel()
-            n += vy.numel()
-        top1 = c1 / max(n, 1)
-        top1 = comm.allreduce_max(top1) if comm.distributed else top1
+        # validation (no_grad forward over the valid split): loss / correct counts accumulate on
+        # the device (no host sync per batch), then one all-reduce gives the global accuracy
+        vbatches = valid.batches(bs, seed=5000 + epoch, shard=comm.rank, num_shards=comm.world_size,
+                                 drop_last=True)
+        _, top1 = validate(search, comm, vbatches, args.max_steps)
         geno = search.genotype()
         if comm.rank == 0:
             print("Valid: [%2d/%d] Final Prec@1 %.4f%%" % (epoch + 1, epochs, 100 * top1))

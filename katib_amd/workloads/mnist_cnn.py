@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .common import device
+from ..parallel.comm import Comm
 
 
 class Net(nn.Module):
@@ -72,24 +72,22 @@ def _data(n, seed, dev):
 
 def main(argv=None):
     args = parse_args(argv if argv is not None else [])
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    dev = torch.device("cpu") if args.no_cuda else device()
+    # DDP (mnist.py:130-133,164-166,189-192): one rank per GPU, rank r on device LOCAL_RANK %
+    # device_count; ranks sharing a GPU fall back to gloo + the one-shot IPC all-reduce (Comm)
+    comm = Comm.from_env("cpu" if args.no_cuda or not torch.cuda.is_available() else "cuda",
+                         backend=args.backend if args.backend != "mpi" else None)
+    ws, rank, dev = comm.world_size, comm.rank, comm.device
     torch.manual_seed(args.seed)
-    dist = None
-    if ws > 1:
-        import torch.distributed as dist
-
-        backend = args.backend if dev.type == "cuda" else "gloo"
-        kw = {"device_id": dev} if backend == "nccl" else {}
-        dist.init_process_group(backend, rank=rank, world_size=ws, **kw)
+    dist = comm if comm.distributed else None
+    if dist is not None and dev.type == "cuda":
+        comm.enable_xgmi()
     x, y = _data(args.num_train + args.num_test, 55, dev)
     tx, ty, vx, vy = x[:args.num_train], y[:args.num_train], x[args.num_train:], y[args.num_train:]
     model = Net().to(dev)
     params = list(model.parameters())
     if dist is not None:
         flat = torch.nn.utils.parameters_to_vector(params).detach()
-        dist.broadcast(flat, 0)
+        comm.broadcast_(flat, 0)
         torch.nn.utils.vector_to_parameters(flat, params)
     opt = torch.optim.SGD(params, lr=args.lr, momentum=args.momentum)
     writer = None
@@ -125,8 +123,7 @@ def main(argv=None):
             loss.backward()
             if dist is not None:
                 g = torch.cat([p.grad.reshape(-1) for p in params])
-                dist.all_reduce(g)
-                g.div_(ws)
+                comm.allreduce_mean_(g)
                 torch.nn.utils.vector_to_parameters(g, [p.grad for p in params])
             opt.step()
             step += 1
@@ -157,8 +154,8 @@ def main(argv=None):
     if log_file is not None:
         log_file.close()
     if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+        comm.barrier()
+        comm.destroy()
     return acc
 
 

@@ -489,6 +489,39 @@ def test_prometheus_collector(manager):
     assert values == ["0.25", "0.5", "0.75"]  # one entry per change, not per scrape
 
 
+def test_prometheus_final_value_published_right_before_exit(manager):
+    """A trial that publishes its objective and exits at once: the value between the last
+    scrape and the exit reaches the observation log through KATIB_PROMETHEUS_FINAL."""
+    code = textwrap.dedent("""
+        import sys
+        sys.path.insert(0, %r)
+        from katib_amd.metricscollector.prometheus import TrialExporter
+        ex = TrialExporter()
+        ex.set("acc", 0.125)
+        ex.set("acc", 0.875)
+        ex.close()
+    """ % ROOT)
+    e = quadratic_yaml(name="promfinal", command=[PY, "-c", code, "${trialParameters.a}"], parallel=1, max_trials=1,
+                       params=[{"name": "a", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                       extra_spec=yaml.safe_dump({
+                           "objective": {"type": "maximize", "objectiveMetricName": "acc"},
+                           "metricsCollectorSpec": {"collector": {"kind": "PrometheusMetric"}}}))
+    manager.create_experiment(e)
+    done = manager.run_until_complete("promfinal", timeout=60)
+    assert EC.is_succeeded(done), done.status.conditions
+    ms = {m.name: m for m in done.status.current_optimal_trial.observation.metrics}
+    assert ms["acc"].latest == "0.875"
+
+
+def test_prometheus_label_sets_do_not_interleave():
+    from katib_amd.metricscollector.prometheus import Scraper
+
+    sc = Scraper(1, "/metrics", ["loss"])
+    assert [v for _, _, v in sc.observe('loss{split="train"} 1\nloss{split="val"} 2\n', 0.0)] == ["1"]
+    assert sc.observe('loss{split="train"} 1\nloss{split="val"} 3\n', 1.0) == []  # val is ignored
+    assert [v for _, _, v in sc.observe('loss 5\nloss{split="train"} 1\n', 2.0)] == ["5"]  # unlabelled wins
+
+
 def test_prometheus_exposition_parser():
     from katib_amd.metricscollector.prometheus import Scraper, parse_exposition
 

@@ -25,12 +25,14 @@ def test_p2p_checkpoint_between_processes(tmp_path):
 
 
 def test_p2p_fetch_missing_producer(tmp_path):
-    import pickle
+    import json
 
     from katib_amd.parallel import p2p_ckpt
 
     d = tmp_path / "m"
     d.mkdir()
-    with open(d / p2p_ckpt.HANDLE_FILE, "wb") as f:
-        pickle.dump({"pid": 2 ** 22 + 12345, "host": "nohost", "handles": {}, "layout": [], "skeleton": {}}, f)
+    with open(d / p2p_ckpt.HANDLE_FILE, "w") as f:
+        json.dump({"pid": 2 ** 22 + 12345, "host": "nohost", "handles": {}, "layout": [], "skeleton": {}}, f)
+    assert p2p_ckpt.fetch(str(d)) is None
+    (d / p2p_ckpt.HANDLE_FILE).write_bytes(b"\x80\x04not json")  # e.g. a pickle planted by trial code
     assert p2p_ckpt.fetch(str(d)) is None

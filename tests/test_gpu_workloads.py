@@ -55,3 +55,52 @@ def test_tpe_mnist_mlp_on_gpu(tmp_path):
         assert float(best["Validation-accuracy"].max) > 0.5
     finally:
         m.shutdown()
+
+
+def test_darts_job_two_gpus_through_manager(tmp_path):
+    """examples/nas/darts-cifar10.yaml with amd.com/gpu: 2 through the Manager: two rank
+    processes (rank plan, controller/jobs.py) share the box's GPU (2 slots per device), so
+    the process group is gloo and the DP gradient all-reduce is the one-shot IPC kernel
+    inside the captured step; rank 0 reports one Best-Genotype."""
+    m = _mgr(tmp_path, 2)
+    try:
+        e = load_experiment(os.path.join(EX, "nas", "darts-cifar10.yaml"))
+        c = e.spec.trial_template.trial_spec["spec"]["template"]["spec"]["containers"][0]
+        c["resources"] = {"limits": {"amd.com/gpu": 2}}
+        c["command"] += ["--num-train=4096", "--max-steps=4"]
+        for s in e.spec.algorithm.algorithm_settings:
+            if s.name == "num_epochs":
+                s.value = "1"
+        m.create_experiment(e)
+        done = m.run_until_complete(e.metadata.name, timeout=600)
+        trials = m.list_trials(e.metadata.name)
+        assert EC.is_succeeded(done), [t.status.conditions[-1].message[-2000:] for t in trials]
+        t = m.get_trial(done.status.current_optimal_trial.best_trial_name)
+        geno = [x for x in t.status.observation.metrics if x.name == "Best-Genotype"]
+        assert geno and geno[0].latest.startswith("Genotype(normal=")
+        tdir = str(tmp_path / "state" / "trials" / "default" / t.metadata.name)
+        assert os.path.exists(os.path.join(tdir, "rank-1.log"))
+        assert open(os.path.join(tdir, "metrics.log")).read().count("Best-Genotype=") == 1
+    finally:
+        m.shutdown()
+
+
+def test_pytorchjob_gpu_replicas(tmp_path):
+    """The PyTorchJob example with its GPU resources kept: Master and Worker replicas on the
+    box's GPU (ranks share it: gloo group + one-shot IPC all-reduce)."""
+    m = _mgr(tmp_path, 2)
+    try:
+        e = load_experiment(os.path.join(EX, "distributed", "pytorchjob-mnist.yaml"))
+        for role in ("Master", "Worker"):
+            c = e.spec.trial_template.trial_spec["spec"]["pytorchReplicaSpecs"][role]["template"]["spec"][
+                "containers"][0]
+            c["command"] += ["--num-train=2048", "--num-test=512"]
+        e.spec.max_trial_count, e.spec.parallel_trial_count, e.spec.max_failed_trial_count = 2, 1, 1
+        m.create_experiment(e)
+        done = m.run_until_complete(e.metadata.name, timeout=600)
+        trials = m.list_trials(e.metadata.name)
+        assert EC.is_succeeded(done), [t.status.conditions[-1].message[-2000:] for t in trials]
+        mm = {x.name: x for x in done.status.current_optimal_trial.observation.metrics}
+        assert float(mm["loss"].latest) > 0
+    finally:
+        m.shutdown()

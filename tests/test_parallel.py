@@ -42,3 +42,39 @@ def test_comm_single_process_noop():
     assert c.allreduce_mean_(t) is t and float(t.sum()) == 3.0
     assert c.allreduce_max(2.5) == 2.5
     assert not c.distributed
+
+
+def test_darts_dp_global_validation():
+    """Validation accuracy of a 2-rank DARTS trial is sum(correct)/sum(n) over both shards,
+    equal to a single process validating the same split."""
+    port = _free_port()
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dp_valid_worker.py")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), worker],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert abs(res["top1"] - res["top1_single"]) < 1e-9, res
+    assert abs(res["loss"] - res["loss_single"]) < 1e-5 * max(1.0, abs(res["loss_single"])), res
+
+
+def test_p2p_handle_file_is_json_roundtrip():
+    """The P2P checkpoint handle file is data-only JSON (no pickle from a trial-writable
+    directory): the nested skeleton - int-keyed optimizer state, tuples - round-trips."""
+    import json as _json
+
+    from katib_amd.parallel import p2p_ckpt as P
+
+    st = {"model": {"w": torch.zeros(3)},
+          "optim": {"state": {0: {"step": torch.tensor(5.0)}},
+                    "param_groups": [{"lr": 0.1, "betas": (0.9, 0.99), "params": [0]}]}, "step": 42}
+    ts = []
+    sk = _json.loads(_json.dumps(P._flatten(st, ts)))
+    out = P._unflatten(sk, ts)
+    assert out["optim"]["state"][0]["step"] is ts[1]
+    assert out["optim"]["param_groups"][0]["betas"] == (0.9, 0.99) and out["step"] == 42
+    import pytest
+
+    with pytest.raises(KeyError):  # classes / dtypes only through the whitelists
+        P._decode_handle([[3], [1], 0, "os.system", "torch.float32", 0, "00", 12, 0, False, None, 0, None, False])

@@ -82,9 +82,16 @@ def test_non_numeric_metric_makes_latest_best():
     _, best, _ = N.summarize_trials(rows, 1, None)
     # "b" becomes best, then "c" is compared against the numeric best 0.1 and loses
     assert best == 1
+    # a non-numeric metric set best first: numeric trials are compared against the
+    # zero-initialised bestTrialValue, exactly as status_util.go:99-110 does
     rows = [row("a", SUCCEEDED, "x"), row("b", SUCCEEDED, "0.4")]
     _, best, _ = N.summarize_trials(rows, 1, None)
-    assert best == 1  # first numeric value seeds the best
+    assert best == 0  # minimize: 0.4 < 0 is false, "a" stays best
+    _, best, goal = N.summarize_trials(rows, 2, 0.3)
+    assert best == 1 and goal  # maximize: 0.4 > 0, and the goal is checked on that value
+    rows = [row("a", SUCCEEDED, "x"), row("b", SUCCEEDED, "-0.4")]
+    _, best, _ = N.summarize_trials(rows, 1, None)
+    assert best == 1
 
 
 def test_unavailable_metrics_are_skipped():
