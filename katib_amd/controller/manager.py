@@ -853,6 +853,10 @@ class Manager:
                     # trials may run the built-in workloads with `python -m katib_amd.workloads.X`
                     "PYTHONPATH": os.pathsep.join(p for p in (_PKG_ROOT, os.environ.get("PYTHONPATH", "")) if p)}
         base_env.update(prom_env)
+        if run.cpu_slot and "OMP_NUM_THREADS" not in os.environ:
+            # CPU trials share the host: cpu_slots concurrent trials each spinning a full
+            # OpenMP pool oversubscribe it cpu_slots times over
+            base_env["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // max(1, self.config.amd.cpu_slots)))
         # each replica gets its share of the trial's devices; rank plans and training-operator
         # jobs see all of them (a rank picks LOCAL_RANK % device_count, parallel/comm.py)
         dev_iter = iter(run.devices)

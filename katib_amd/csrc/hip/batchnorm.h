@@ -27,5 +27,10 @@ hipError_t bwd(const bf16* dy, const bf16* y, const bf16* x, const float* gamma,
                const float* invstd, bf16* dx, bf16* dres, float* dgamma, float* dbeta, float* coef, float* part, int P,
                int C, hipStream_t st);
 
+// Per-channel sum of a [P, C] bf16 activation into out[C] fp32 (bias gradients): the statistics
+// pass into part (R * 2 * C floats) + one finalize launch; deterministic, no atomics and no
+// zero-initialised workspace, so it replays correctly from a HIP graph.
+hipError_t channel_sum(const bf16* x, float* out, float* part, int P, int C, hipStream_t st);
+
 }  // namespace bn
 }  // namespace katib_hip

@@ -155,6 +155,15 @@ __global__ __launch_bounds__(256) void fwd_finalize_k(const float* __restrict__ 
   }
 }
 
+__global__ __launch_bounds__(256) void sum_finalize_k(const float* __restrict__ part, int R, int C,
+                                                      float* __restrict__ out) {
+  __shared__ float red[2][4][64];
+  float s, q;
+  sum_parts(part, R, C, s, q, red);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (threadIdx.x < 64 && c < C) out[c] = s;
+}
+
 __global__ void eval_coef_k(const float* __restrict__ rmean, const float* __restrict__ rvar,
                             const float* __restrict__ gamma, const float* __restrict__ beta, float eps, int C,
                             float* __restrict__ ss) {
@@ -261,6 +270,15 @@ hipError_t fwd_train(const bf16* x, const bf16* res, bf16* y, const float* gamma
   const int64_t n8 = (int64_t)P * C / 8;
   hipLaunchKernelGGL(apply_k, dim3(ew_grid(n8)), dim3(256), 0, st, xx, reinterpret_cast<const u16*>(res),
                      reinterpret_cast<u16*>(y), ss, n8, C, relu);
+  return hipGetLastError();
+}
+
+hipError_t channel_sum(const bf16* x, float* out, float* part, int P, int C, hipStream_t st) {
+  int R, rows, cvb;
+  plan(P, C, &R, &rows, &cvb);
+  hipLaunchKernelGGL(stats_k<0>, dim3((C / 8 + cvb - 1) / cvb, R), dim3(256), 0, st, reinterpret_cast<const u16*>(x),
+                     nullptr, nullptr, nullptr, nullptr, P, C, rows, cvb, part);
+  hipLaunchKernelGGL(sum_finalize_k, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, out);
   return hipGetLastError();
 }
 

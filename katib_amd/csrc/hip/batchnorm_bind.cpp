@@ -104,9 +104,21 @@ void bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, const Tensor& x, c
      "bn_bwd");
 }
 
+void channel_sum(const Tensor& x, const Tensor& out) {
+  int64_t P, C;
+  dims(x, P, C);
+  chk_act(x, P, C, "x");
+  chk_vec(out, C, "out");
+  int R, rows, cvb;
+  B_::plan((int)P, (int)C, &R, &rows, &cvb);
+  auto part = at::empty({(int64_t)R * 2 * C}, x.options().dtype(at::kFloat));
+  ok(B_::channel_sum(bp(x), out.data_ptr<float>(), part.data_ptr<float>(), (int)P, (int)C, stream()), "channel_sum");
+}
+
 }  // namespace
 
 void register_batchnorm(py::module& m) {
+  m.def("channel_sum", &channel_sum, "per-channel sum of a [P, C] bf16 activation (bias gradients), graph-safe");
   m.def("bn_fwd_train", &bn_fwd_train, "NHWC bf16 batch norm (+residual, +ReLU), training statistics");
   m.def("bn_fwd_eval", &bn_fwd_eval, "NHWC bf16 batch norm (+residual, +ReLU) with running statistics");
   m.def("bn_bwd", &bn_bwd, "NHWC bf16 batch norm backward (ReLU mask from the output, residual gradient)");

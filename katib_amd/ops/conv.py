@@ -96,6 +96,39 @@ class _ConvFn(torch.autograd.Function):
         return gx, gw, None, None, None, None
 
 
+def channel_sum_nhwc(g: torch.Tensor) -> torch.Tensor:
+    """Sum of an [N, C, H, W] gradient over (N, H, W) -> fp32 [C] on the HIP channel-sum kernel
+    (C % 8 == 0), never through PyTorch's cross-workgroup reduction: on this ROCm stack that
+    reduction (global staging buffer + semaphores) reads its staging memory before writing it
+    when replayed from a HIP graph, which turned the captured ENAS child step NaN
+    (profiles/enas_child_capture_rootcause_r03.log)."""
+    N, C, H, W = g.shape
+    rows = g.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous().view(-1, C)
+    out = torch.empty(C, device=g.device, dtype=torch.float32)
+    kernels().channel_sum(rows, out)
+    return out
+
+
+class _BiasAddFn(torch.autograd.Function):
+    """y + bias[c]; the bias gradient is the HIP channel sum (see :func:`channel_sum_nhwc`)."""
+
+    @staticmethod
+    def forward(ctx, y, bias):
+        ctx.bdtype = bias.dtype
+        return y + bias.to(y.dtype).view(1, -1, 1, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        gb = channel_sum_nhwc(gy).to(ctx.bdtype) if ctx.needs_input_grad[1] else None
+        return gy, gb
+
+
+def bias_add(y: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    if y.is_cuda and y.shape[1] % 8 == 0:
+        return _BiasAddFn.apply(y, bias)
+    return y + bias.to(y.dtype).view(1, -1, 1, 1)
+
+
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, padding=0, dilation=1,
            out_hw=None) -> torch.Tensor:
     """bf16 NHWC implicit-GEMM convolution (groups=1) with an fp32 weight master.
@@ -104,7 +137,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, padding=0, dil
         x = x.to(torch.bfloat16)  # like autocast; keeps the Function's input grad bf16
     y = _ConvFn.apply(x, w, _pair(stride), _pair(padding), _pair(dilation), out_hw)
     if bias is not None:
-        y = y + bias.to(y.dtype).view(1, -1, 1, 1)
+        y = bias_add(y, bias)
     return y
 
 

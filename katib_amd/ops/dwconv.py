@@ -69,8 +69,9 @@ class _DwFn(torch.autograd.Function):
             part = torch.empty((rows, C * dm, K * K), device=gy.device, dtype=torch.float32)
             k.dw_wgrad(xn, gyn, part, ctx.geom)
             gw = part.sum(0).view(ctx.wshape).to(ctx.wdtype)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = gyn.float().sum((0, 1, 2))
+        if ctx.has_b and ctx.needs_input_grad[2]:  # HIP channel sum: no PyTorch reduction under capture
+            gb = torch.empty(C * dm, device=gy.device, dtype=torch.float32)
+            k.channel_sum(gyn.view(-1, C * dm), gb)
         return gx, gw, gb, None
 
 

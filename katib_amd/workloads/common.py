@@ -4,8 +4,11 @@ default collector format (``name=value``).
 
 Synthetic data (no network in the target environment): every dataset is generated
 from a fixed seed by a *teacher* so that hyperparameters matter - a random linear
-teacher for MNIST-shaped vectors, class-conditional spatial patterns for
-CIFAR-shaped images, and a sparse first-order Markov chain for token streams.
+teacher with label noise for MNIST-shaped vectors, overlapping multi-modal
+class patterns with random translations and label noise for CIFAR-shaped images, and a
+sparse first-order Markov chain for token streams. None of them saturates: the earlier
+single-template image teacher was fitted to >0.999 after one epoch by every ResNet trial,
+so an HPO experiment could not tell its trials apart.
 """
 
 from __future__ import annotations
@@ -36,29 +39,57 @@ def _fmt(v):
 
 
 # ----------------------------------------------------------------------------- datasets
-def teacher_vectors(n: int, dim: int = 784, classes: int = 10, seed: int = 0, dev=None, noise: float = 0.5):
-    """x ~ N(0, 1); y = argmax(x @ T + noise) for a fixed random teacher T."""
+def teacher_vectors(n: int, dim: int = 784, classes: int = 10, seed: int = 0, dev=None, noise: float = 0.5,
+                    label_noise: float = 0.05):
+    """x ~ N(0, 1); y = argmax(x @ T + noise) for a fixed random linear teacher T, then a
+    fraction ``label_noise`` of the labels replaced by random ones (accuracy caps near
+    ``1 - 0.9 * label_noise``). Over the TPE example's ranges the MLP's accuracy after 3
+    epochs spans ~0.15 (lr 0.3 diverges) to ~0.85, so the search has something to rank."""
     g = torch.Generator().manual_seed(seed)
     T = torch.randn(dim, classes, generator=g) / dim ** 0.5
     x = torch.randn(n, dim, generator=g)
     y = (x @ T + noise * torch.randn(n, classes, generator=g) / dim ** 0.5).argmax(1)
+    flip = torch.rand(n, generator=g) < label_noise
+    y = torch.where(flip, torch.randint(0, classes, (n,), generator=g), y)
     return x.to(dev), y.to(dev)
 
 
-def pattern_images(n: int, shape=(3, 32, 32), classes: int = 10, seed: int = 0, dev=None, noise: float = 1.0,
-                   dtype=torch.float32):
-    """Per-class smooth spatial template + Gaussian noise (CIFAR-10 shaped)."""
+def pattern_images(n: int, shape=(3, 32, 32), classes: int = 10, seed: int = 0, dev=None, noise: float = 1.5,
+                   dtype=torch.float32, modes: int = 3, shift: int = 4, label_noise: float = 0.1):
+    """CIFAR-10-shaped images that do not saturate: every class is a mixture of ``modes``
+    prototypes, each prototype = a shared texture from a small common bank (so classes
+    overlap) + a weaker class-specific pattern; every sample is one prototype with random
+    amplitude, a random translation of up to ``shift`` pixels (so the model has to be
+    translation-tolerant, not memorise pixels) and Gaussian noise; a fraction
+    ``label_noise`` of the labels is random. The best attainable accuracy is below
+    ``1 - 0.9 * label_noise``, and how close a trial gets depends on its learning rate,
+    width and epochs - the signal HyperBand / median-stop / PBT need to rank trials."""
     g = torch.Generator().manual_seed(seed)
     C, H, W = shape
-    base = torch.randn(classes, C, H // 4, W // 4, generator=g)
-    tmpl = torch.nn.functional.interpolate(base, size=(H, W), mode="bilinear", align_corners=False)
+    up = lambda t: torch.nn.functional.interpolate(t, size=(H, W), mode="bilinear", align_corners=False)  # noqa: E731
+    bank = up(torch.randn(6, C, H // 4, W // 4, generator=g))
+    own = up(torch.randn(classes * modes, C, H // 8, W // 8, generator=g))
+    mix = torch.randint(0, bank.shape[0], (classes * modes,), generator=g)
+    protos = bank[mix] + 0.6 * own  # [classes * modes, C, H, W]
     y = torch.randint(0, classes, (n,), generator=g)
     out = torch.empty(n, C, H, W, dtype=dtype, device=dev)
     chunk = 4096
     for i in range(0, n, chunk):
         yi = y[i:i + chunk]
-        xi = tmpl[yi] + noise * torch.randn(len(yi), C, H, W, generator=g)
+        m = len(yi)
+        pid = yi * modes + torch.randint(0, modes, (m,), generator=g)
+        xi = protos[pid] * (0.5 + torch.rand(m, 1, 1, 1, generator=g))
+        if shift:
+            dy = torch.randint(-shift, shift + 1, (m,), generator=g)
+            dx = torch.randint(-shift, shift + 1, (m,), generator=g)
+            rows = (torch.arange(H).view(1, H) - dy.view(m, 1)) % H  # [m, H]
+            cols = (torch.arange(W).view(1, W) - dx.view(m, 1)) % W
+            xi = xi[torch.arange(m).view(m, 1, 1, 1), torch.arange(C).view(1, C, 1, 1),
+                    rows.view(m, 1, H, 1), cols.view(m, 1, 1, W)]
+        xi = xi + noise * torch.randn(m, C, H, W, generator=g)
         out[i:i + chunk] = xi.to(device=dev, dtype=dtype)
+    flip = torch.rand(n, generator=g) < label_noise
+    y = torch.where(flip, torch.randint(0, classes, (n,), generator=g), y)
     return out, y.to(dev)
 
 
@@ -75,6 +106,21 @@ def markov_tokens(n_tokens: int, vocab: int = 50257, seed: int = 0, dev=None, fa
         toks[:, i] = state
         state = succ[state, torch.randint(0, fanout, (chains,), generator=g)]
     return toks.reshape(-1)[:n_tokens].to(dev)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] -> [N, C] average as ONE pooling window (``avg_pool2d`` with the whole plane
+    as the kernel), not ``adaptive_avg_pool2d(x, 1)``: for output 1x1 PyTorch lowers that to
+    ``mean`` over (H, W), and on a channels-last bf16 activation the mean is a strided
+    reduction whose cross-workgroup path (a global staging buffer plus semaphores reset by a
+    memset before the kernel) reads its staging buffer before it is written when replayed
+    from a HIP graph on this ROCm stack: with the graph's memory pool poisoned with NaN
+    before a replay, that ``mean`` is the first op with a non-finite output
+    (scripts/enas_nan_locate.py, profiles/enas_child_capture_rootcause_r03.log). That was
+    the captured ENAS child step's NaN: stale staging data from earlier replays usually
+    averages to finite garbage, occasionally to NaN/Inf, and the eager validation between
+    epochs (or a host sync between replays) changed what the stale memory held."""
+    return torch.nn.functional.avg_pool2d(x, (x.shape[2], x.shape[3])).flatten(1)
 
 
 # ----------------------------------------------------------------------------- graphs

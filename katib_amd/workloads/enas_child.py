@@ -36,7 +36,7 @@ import torch.nn.functional as F
 from ..ops import batchnorm as hbn
 from ..ops import conv as hconv
 from ..ops import dwconv as hdw
-from .common import CapturedStep, Timer, device, pattern_images, report
+from .common import CapturedStep, Timer, device, global_avg_pool, pattern_images, report
 
 
 def _same_pad(size: int, k: int, s: int):
@@ -151,7 +151,7 @@ class ChildNet(nn.Module):
         layers = [x]
         for op, ins in zip(self.ops, self.inputs):
             layers.append(op(_concat([layers[i] for i in ins])))
-        return self.fc(self.drop(F.adaptive_avg_pool2d(layers[-1], 1).flatten(1)))
+        return self.fc(self.drop(global_avg_pool(layers[-1])))
 
 
 def _chw(sizes):
@@ -178,13 +178,87 @@ def parse_args(argv):
     p.add_argument("--batch-size", type=int, default=128)
     p.add_argument("--num-train", type=int, default=50000)
     p.add_argument("--num-valid", type=int, default=10000)
-    # eager by default: measured on MI355X the eager step is faster (28.4 s vs 31.7 s for 3
-    # epochs) and the HIP-graph-captured step turns NaN at a deterministic replay once eager
-    # work runs between replays (profiles/enas_child_capture_{bisect,probe,fix}_r02.log;
-    # open issue, scripts/enas_repro.py reproduces it)
-    p.add_argument("--capture", type=int, default=0)
+    # HIP-graph-captured train step (default); --capture 0 runs it eagerly
+    p.add_argument("--capture", type=int, default=1)
     p.add_argument("--seed", type=int, default=0)
     return p.parse_args(argv)
+
+
+class ChildTrainer:
+    """The trial's model, optimizer and (optionally HIP-graph-captured) train step; ``main``
+    drives it epoch by epoch, tests drive it step by step."""
+
+    def __init__(self, arch, nn_config, num_train=50000, num_valid=10000, batch_size=128, capture=True, seed=0,
+                 comm=None):
+        from ..parallel.comm import Comm
+
+        dev = device()
+        cuda = dev.type == "cuda"
+        torch.manual_seed(seed)
+        self.comm = comm or (Comm.from_env(dev.type) if cuda else Comm())
+        self.dev, self.cuda = dev, cuda
+        mf = torch.channels_last if cuda else torch.contiguous_format
+        c, h, w = _chw(nn_config["input_sizes"])
+        x, y = pattern_images(num_train + num_valid, (c, h, w), seed=777, dev=dev,
+                              dtype=torch.bfloat16 if cuda else torch.float32, noise=2.0)
+        x = x.contiguous(memory_format=mf)
+        self.tx, self.ty, self.vx, self.vy = x[:num_train], y[:num_train], x[num_train:], y[num_train:]
+        self.model = model = ChildNet(arch, nn_config).to(dev).to(memory_format=mf)
+        comm = self.comm
+        if comm.world_size > 1:  # every rank starts from rank 0's weights
+            flat0 = torch.nn.utils.parameters_to_vector(model.parameters()).detach()
+            comm.broadcast_(flat0)
+            torch.nn.utils.vector_to_parameters(flat0, model.parameters())
+        self.opt = opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=cuda, capturable=cuda)
+        self.params = list(model.parameters())
+        for p_ in self.params:
+            p_.grad = torch.zeros_like(p_)
+        self.bs = batch_size
+        self.shard = num_train // comm.world_size
+        self.steps = max(1, self.shard // batch_size)
+        self.idx = idx = torch.zeros(batch_size, dtype=torch.long, device=dev)
+        self.acc_buf = acc_buf = torch.zeros(2, device=dev)  # loss sum, correct
+        tx, ty = self.tx, self.ty
+
+        def train_step():
+            xb, yb = tx.index_select(0, idx), ty.index_select(0, idx)
+            with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda):
+                logits = model(xb)
+            loss = F.cross_entropy(logits.float(), yb)
+            opt.zero_grad(set_to_none=False)
+            loss.backward()
+            acc_buf[0].add_(loss.detach())
+            acc_buf[1].add_((logits.argmax(1) == yb).sum())
+            if comm.world_size == 1:
+                opt.step()
+            return acc_buf
+
+        # captured by default: the NaN seen in round 2 came from PyTorch reductions on
+        # channels-last bf16 tensors (GAP mean, bias sums), now HIP kernels / a pooling window
+        self.step_fn = CapturedStep(train_step, enabled=bool(capture) and comm.world_size == 1, no_miopen=True)
+
+    def step(self, batch_idx: torch.Tensor):
+        self.idx.copy_(batch_idx)
+        self.step_fn()
+        if self.comm.world_size > 1:
+            flat = torch.cat([p_.grad.reshape(-1) for p_ in self.params])
+            self.comm.allreduce_mean_(flat)
+            torch.nn.utils.vector_to_parameters(flat, [p_.grad for p_ in self.params])
+            self.opt.step()
+
+    @torch.no_grad()
+    def validate(self, num_valid=None, chunk=1000):
+        """Eager eval-mode pass over the validation split -> (mean loss, accuracy)."""
+        self.model.eval()
+        n = self.vx.shape[0] if num_valid is None else num_valid
+        vl, vc = 0.0, 0.0
+        with torch.autocast(device_type=self.dev.type, dtype=torch.bfloat16, enabled=self.cuda):
+            for i in range(0, n, chunk):
+                lg = self.model(self.vx[i:i + chunk]).float()
+                vl += float(F.cross_entropy(lg, self.vy[i:i + chunk], reduction="sum"))
+                vc += float((lg.argmax(1) == self.vy[i:i + chunk]).sum())
+        self.model.train()
+        return vl / max(n, 1), vc / max(n, 1)
 
 
 def main(argv=None):
@@ -192,76 +266,24 @@ def main(argv=None):
     arch = json.loads(_unquote(args.architecture).replace("'", '"'))
     nn_config = json.loads(_unquote(args.nn_config).replace("'", '"'))
     print(">>> arch received by trial\n%s" % arch, flush=True)
-    dev = device()
-    cuda = dev.type == "cuda"
-    torch.manual_seed(args.seed)
-    from ..parallel.comm import Comm
-
-    comm = Comm.from_env(dev.type) if cuda else Comm()
-    mf = torch.channels_last if cuda else torch.contiguous_format
-    c, h, w = _chw(nn_config["input_sizes"])
-    x, y = pattern_images(args.num_train + args.num_valid, (c, h, w), seed=777, dev=dev,
-                          dtype=torch.bfloat16 if cuda else torch.float32, noise=2.0)
-    x = x.contiguous(memory_format=mf)
-    tx, ty, vx, vy = x[:args.num_train], y[:args.num_train], x[args.num_train:], y[args.num_train:]
-    model = ChildNet(arch, nn_config).to(dev).to(memory_format=mf)
-    if comm.world_size > 1:  # every rank starts from rank 0's weights
-        flat0 = torch.nn.utils.parameters_to_vector(model.parameters()).detach()
-        comm.broadcast_(flat0)
-        torch.nn.utils.vector_to_parameters(flat0, model.parameters())
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=cuda, capturable=cuda)
-    params = list(model.parameters())
-    for p_ in params:
-        p_.grad = torch.zeros_like(p_)
-    bs = args.batch_size
-    shard = args.num_train // comm.world_size
-    steps = max(1, shard // bs)
-    idx = torch.zeros(bs, dtype=torch.long, device=dev)
-    acc_buf = torch.zeros(2, device=dev)  # loss sum, correct
-
-    def train_step():
-        xb, yb = tx.index_select(0, idx), ty.index_select(0, idx)
-        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda):
-            logits = model(xb)
-        loss = F.cross_entropy(logits.float(), yb)
-        opt.zero_grad(set_to_none=False)
-        loss.backward()
-        acc_buf[0].add_(loss.detach())
-        acc_buf[1].add_((logits.argmax(1) == yb).sum())
-        if comm.world_size == 1:
-            opt.step()
-        return acc_buf
-
-    step = CapturedStep(train_step, enabled=bool(args.capture) and comm.world_size == 1, no_miopen=True)
+    tr = ChildTrainer(arch, nn_config, args.num_train, args.num_valid, args.batch_size, bool(args.capture), args.seed)
+    comm, dev, bs, steps = tr.comm, tr.dev, tr.bs, tr.steps
     gen = torch.Generator(device=dev).manual_seed(args.seed + comm.rank)
     timer = Timer()
     va = 0.0
     for epoch in range(args.num_epochs):
-        model.train()
-        perm = torch.randperm(shard, device=dev, generator=gen)[:steps * bs].view(steps, bs) + comm.rank * shard
-        acc_buf.zero_()
+        tr.model.train()
+        perm = torch.randperm(tr.shard, device=dev, generator=gen)[:steps * bs].view(steps, bs) + comm.rank * tr.shard
+        tr.acc_buf.zero_()
         for s in range(steps):
-            idx.copy_(perm[s])
-            step()
-            if comm.world_size > 1:
-                flat = torch.cat([p_.grad.reshape(-1) for p_ in params])
-                comm.allreduce_mean_(flat)
-                torch.nn.utils.vector_to_parameters(flat, [p_.grad for p_ in params])
-                opt.step()
-        model.eval()
-        with torch.no_grad(), torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=cuda):
-            vl, vc = 0.0, 0.0
-            for i in range(0, args.num_valid, 1000):
-                lg = model(vx[i:i + 1000]).float()
-                vl += float(F.cross_entropy(lg, vy[i:i + 1000], reduction="sum"))
-                vc += float((lg.argmax(1) == vy[i:i + 1000]).sum())
-        va = vc / max(args.num_valid, 1)
+            tr.step(perm[s])
+        vl, va = tr.validate(args.num_valid)
         if comm.rank == 0:
             print("\nTotal Epoch {}/{}".format(epoch + 1, args.num_epochs))
-            print("Training-Accuracy={}".format(float(acc_buf[1]) / (steps * bs)))
-            print("Training-Loss={}".format(float(acc_buf[0]) / steps))
+            print("Training-Accuracy={}".format(float(tr.acc_buf[1]) / (steps * bs)))
+            print("Training-Loss={}".format(float(tr.acc_buf[0]) / steps))
             print("Validation-Accuracy={}".format(va))
-            print("Validation-Loss={}".format(vl / max(args.num_valid, 1)), flush=True)
+            print("Validation-Loss={}".format(vl), flush=True)
     if comm.rank == 0:
         report(train_seconds=timer.elapsed())
     return va

@@ -24,7 +24,7 @@ import torch.nn.functional as F
 
 from ..ops import batchnorm as hbn
 from ..ops import conv as hconv
-from .common import CapturedStep, Timer, device, pattern_images, report
+from .common import CapturedStep, Timer, device, global_avg_pool, pattern_images, report
 
 Conv = hconv.Conv2d  # HIP implicit GEMM on GPU, stock nn.Conv2d on CPU
 BN = hbn.BatchNorm2d  # HIP NHWC batch norm (+ residual + ReLU) on GPU, stock module on CPU
@@ -90,7 +90,7 @@ class ResNet18(nn.Module):
 
     def forward(self, x):
         x = self.layers(self.stem_bn(self.stem_conv(x), relu=True))
-        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+        return self.fc(global_avg_pool(x))
 
 
 def main(argv=None):

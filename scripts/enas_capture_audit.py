@@ -133,8 +133,26 @@ def audit():
     print("AUDIT suspicious args: %d" % len(bad), flush=True)
 
 
-def replay(mode, n=200):
-    step = build()
+def _variants(parts):
+    """Swap HIP op families for PyTorch ones (same switches as scripts/enas_repro.py)."""
+    from katib_amd.ops import dwconv as hdw
+
+    if "torchbn" in parts:
+        hbn.BatchNorm2d.forward = lambda self, x, residual=None, relu=False: torch.nn.BatchNorm2d.forward(self, x)
+    if "noconv" in parts:
+        hconv.supported = lambda *a, **k: False
+    if "nodw" in parts:
+        hdw.supported = lambda *a, **k: False
+    if "adamfe" in parts:
+        class _AdamForeach(torch.optim.Adam):
+            def __init__(self, params, **kw):
+                kw.pop("fused", None)
+                super().__init__(params, foreach=True, **kw)
+        enas_child.torch.optim.Adam = _AdamForeach
+
+
+def replay(mode, n=200, capture=True, tag=""):
+    step = build(capture)
     env = {n_: c.cell_contents for n_, c in zip(step.fn.__code__.co_freevars, step.fn.__closure__ or ())}
     if "inner" in env:
         env = {n_: c.cell_contents for n_, c in zip(env["inner"].__code__.co_freevars, env["inner"].__closure__ or ())}
@@ -157,13 +175,28 @@ def replay(mode, n=200):
             if not math.isfinite(v) and first is None:
                 first = r
                 break
-    print("REPLAY mode=%s replays=%d first_nonfinite=%s loss_sum=%s" % (mode, n, first, float(acc[0])), flush=True)
+    print("REPLAY mode=%s capture=%d %s replays=%d first_nonfinite=%s loss_sum=%s"
+          % (mode, int(capture), tag, n, first, float(acc[0])), flush=True)
 
 
 if __name__ == "__main__":
     what = sys.argv[1:] or ["audit", "replay"]
-    if "audit" in what:
+    if what[:1] == ["_one"]:
+        what = what
+    elif "audit" in what:
         audit()
     if "replay" in what:
         for mode in ("none", "sync", "alloc", "allocbig"):
             replay(mode)
+    for w in (what if what[:1] != ["_one"] else []):  # "<mode>:<capture 0|1>[:variants]": one child each
+        if w.count(":") >= 1:
+            import subprocess
+
+            r = subprocess.run([sys.executable, __file__, "_one", w], capture_output=True, text=True, timeout=300)
+            print("\n".join(ln for ln in (r.stdout + r.stderr).splitlines() if ln.startswith("REPLAY") or
+                            "Error" in ln)[-2000:] or "rc=%d" % r.returncode, flush=True)
+    if what[:1] == ["_one"]:
+        mode, cap, var = (what[1].split(":") + [""])[:3]
+        parts = set(var.split("+")) if var else set()
+        _variants(parts)
+        replay(mode, capture=cap == "1", tag=var)

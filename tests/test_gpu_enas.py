@@ -5,6 +5,7 @@ baseline, gradients of every parameter and Adam update; sampled arcs must follow
 controller's softmax / sigmoid probabilities.
 """
 import math
+import os
 
 import pytest
 import torch
@@ -172,3 +173,61 @@ def test_enas_service_uses_hip_controller():
     reply = svc.GetSuggestions(enas_request(trials=[("t0", 0.6), ("t1", 0.8)], n=3))
     assert len(reply.parameter_assignments) == 3
     assert svc.controller.train_step == 50 and svc.last_train_log
+
+
+def _fixture_arch():
+    import json
+
+    cfg = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                                      "enas_repro_arch.json")))
+    return json.loads(cfg["architecture"]), json.loads(cfg["nn_config"].replace("'", '"'))
+
+
+def test_enas_child_captured_steps_match_eager_with_validation():
+    """100 HIP-graph-captured ENAS child steps with eager validation passes interleaved stay
+    finite and track the eager run (the architecture that used to NaN)."""
+    import torch
+
+    from katib_amd.workloads.enas_child import ChildTrainer
+
+    arch, cfg = _fixture_arch()
+    runs = {}
+    for capture in (True, False):
+        tr = ChildTrainer(arch, cfg, num_train=8192, num_valid=1000, capture=capture, seed=3)
+        g = torch.Generator(device=tr.dev).manual_seed(11)
+        losses, vals = [], []
+        for s in range(100):
+            tr.step(torch.randint(0, 8192, (tr.bs,), device=tr.dev, generator=g))
+            if s % 25 == 24:
+                vals.append(tr.validate())
+                losses.append(float(tr.acc_buf[0]))
+        assert all(math.isfinite(p.float().sum().item()) for p in tr.model.parameters()), capture
+        runs[capture] = (losses, vals)
+    (lc, vc), (le, ve) = runs[True], runs[False]
+    assert all(math.isfinite(x) for x in lc + [v for pair in vc for v in pair]), (lc, vc)
+    for a, b in zip(lc, le):
+        assert abs(a - b) <= 0.05 * max(1.0, abs(b)), (lc, le)
+    assert abs(vc[-1][1] - ve[-1][1]) < 0.08, (vc, ve)
+
+
+def test_enas_child_graph_reads_nothing_stale():
+    """With the graph's private pool poisoned with NaN before every replay, the captured ENAS
+    child step still produces finite losses and parameters: no op inside the graph reads a
+    temporary it did not write first (katib_amd/utils/graphcheck.py)."""
+    import torch
+
+    from katib_amd.utils.graphcheck import poison_graph_pool
+    from katib_amd.workloads.enas_child import ChildTrainer
+
+    arch, cfg = _fixture_arch()
+    tr = ChildTrainer(arch, cfg, num_train=4096, num_valid=500, capture=True, seed=1)
+    g = torch.Generator(device=tr.dev).manual_seed(5)
+    for s in range(12):
+        if tr.step_fn.graph is not None:
+            assert poison_graph_pool(tr.step_fn.graph) > 0
+        tr.step(torch.randint(0, 4096, (tr.bs,), device=tr.dev, generator=g))
+        torch.cuda.synchronize()
+        assert math.isfinite(float(tr.acc_buf[0])), s
+        if s == 6:
+            tr.validate()  # eager work between replays
+    assert all(bool(torch.isfinite(p).all()) for p in tr.model.parameters())

@@ -104,3 +104,55 @@ def test_pytorchjob_gpu_replicas(tmp_path):
         assert float(mm["loss"].latest) > 0
     finally:
         m.shutdown()
+
+
+def test_resnet_hyperband_medianstop_gpu(tmp_path):
+    """BASELINE config 3 at a realistic size on one MI355X (8 warm workers): HyperBand's first
+    bracket (8 + 4 + 2 + 1 trials) then the second bracket's fresh random samples, which
+    carry the median-stop rule of the finished trials; the synthetic task does not saturate,
+    so trials differ by >= 0.1 accuracy and the rule stops at least one."""
+    m = _mgr(tmp_path, 8)
+    try:
+        e = load_experiment(os.path.join(EX, "early-stopping", "hyperband-medianstop-resnet18.yaml"))
+        spec = e.spec.trial_template.trial_spec["spec"]
+        spec["args"] = list(spec["args"]) + ["--num-train=10000", "--num-valid=2000"]
+        e.spec.max_trial_count, e.spec.parallel_trial_count, e.spec.max_failed_trial_count = 21, 8, 2
+        m.create_experiment(e)
+        done = m.run_until_complete(e.metadata.name, timeout=900)
+        trials = m.list_trials(e.metadata.name)
+        assert EC.is_succeeded(done), [t.status.conditions[-1].message[-1500:] for t in trials]
+        accs = []
+        for t in trials:
+            for x in (t.status.observation.metrics if t.status.observation else []):
+                if x.name == "Validation-accuracy" and x.max not in (None, "unavailable"):
+                    accs.append(float(x.max))
+        print("accuracies", sorted(accs), "early stopped", done.status.trials_early_stopped)
+        assert max(accs) - min(accs) >= 0.1 and max(accs) < 0.97, accs
+        assert (done.status.trials_early_stopped or 0) >= 1
+    finally:
+        m.shutdown()
+
+
+def test_resnet_captured_step_with_eval_and_poisoned_pool(monkeypatch, capsys):
+    """ResNet-18 trial: captured train step, eager eval pass between epochs, and the graph's
+    private pool poisoned with NaN before every replay - the loss and accuracy stay finite,
+    so no op inside the graph reads a temporary it did not write."""
+    import math
+    import re
+
+    from katib_amd.utils.graphcheck import poison_graph_pool
+    from katib_amd.workloads import common, resnet_cifar
+
+    orig = common.CapturedStep.__call__
+
+    def poisoned(self):
+        if self.graph is not None:
+            poison_graph_pool(self.graph)
+        return orig(self)
+    monkeypatch.setattr(common.CapturedStep, "__call__", poisoned)
+    acc = resnet_cifar.main(["--epochs", "3", "--num-train", "4096", "--num-valid", "1024", "--width", "16",
+                             "--batch-size", "256", "--lr", "0.1"])
+    out = capsys.readouterr().out
+    losses = [float(m) for m in re.findall(r"loss=([^\s]+)", out)]
+    assert len(losses) == 3 and all(math.isfinite(v) for v in losses), out
+    assert 0.15 < acc <= 1.0
