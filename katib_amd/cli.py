@@ -313,6 +313,13 @@ def cmd_metrics_collector(a, rest):
     return collect(parse_args(rest))
 
 
+def cmd_openapi(a):
+    from .api import openapi
+
+    print(openapi.dumps(include_k8s=a.with_k8s))
+    return 0
+
+
 def cmd_inject(a):
     """Print the pod with the metrics collector injected (the /mutate-pod webhook's
     rewrite) for running a trial's pod on a cluster."""
@@ -410,6 +417,10 @@ def build_parser():
     inj.add_argument("--early-stopping-algorithm", default="", help="algorithm serving -s-earlystop")
     inj.add_argument("--db-manager", default="", help="DBManager address (default from KATIB_DB_MANAGER_*)")
     inj.set_defaults(fn=cmd_inject)
+
+    oa = sub.add_parser("openapi", help="print the v1beta1 Swagger 2.0 document (reference swagger.json layout)")
+    oa.add_argument("--with-k8s", action="store_true", help="also define the v1.ObjectMeta / v1.Time types")
+    oa.set_defaults(fn=cmd_openapi)
     return p
 
 

@@ -92,6 +92,10 @@ class ApiServer:
             return 200, "text/plain", b"ok"
         if path == "/metrics":
             return 200, "text/plain; version=0.0.4", m.metrics.expose().encode()
+        if path in ("/openapi/v2", "/swagger.json"):  # generated from the model table (api/openapi.py)
+            from ..api import openapi
+
+            return 200, "application/json", openapi.dumps(include_k8s=True).encode()
         if path == "/katib/trace":  # Chrome/Perfetto timeline of trials and suggestion calls
             return _json(m.tracer.chrome_trace())
         if path == "/katib/trace/latencies":
