@@ -191,9 +191,27 @@ class ApiServer:
                     view.update(e.to_k8s().get("status") or {})
                     out.append(view)
             return _json(out)
+        if path == "/katib/fetch_algorithms":  # the UI's algorithm / early-stopping pickers
+            return _json({"algorithms": sorted(m.config.suggestions), "earlyStopping": sorted(m.config.early_stoppings)})
+        if path == "/katib/edit_experiment_budget" and method == "POST":  # SDK edit_experiment_budget
+            data = _load_body(body) or {}
+            exp = self._get(m.get_experiment, data.get("experimentName"), data.get("namespace"), "experiments")
+            for key, attr in (("maxTrialCount", "max_trial_count"), ("parallelTrialCount", "parallel_trial_count"),
+                              ("maxFailedTrialCount", "max_failed_trial_count")):
+                if data.get(key) is not None:
+                    setattr(exp.spec, attr, int(data[key]))
+            try:
+                return _json(m.update_experiment(exp).to_k8s())
+            except ValidationError as e:
+                raise _Err(400, "Invalid", str(e))
         if path == "/katib/create_experiment" and method == "POST":  # backend.go:86-136
             data = _load_body(body)
             doc = data.get("postData") if isinstance(data, dict) and "postData" in data else None
+            if isinstance(doc, str):  # the UI's editor sends YAML (or JSON) text
+                try:
+                    doc = yaml.safe_load(doc)
+                except yaml.YAMLError as e:
+                    raise _Err(400, "BadRequest", "postData is not valid YAML/JSON: %s" % e)
             if doc is None:
                 raise _Err(500, "InternalError", "Couldn't load the 'postData' field of the request's data")
             try:

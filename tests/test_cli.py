@@ -190,11 +190,23 @@ def test_ui_backend_routes(manager):
             raise AssertionError("%s: %s" % (path, ex.read().decode()))
 
     try:
-        assert b"Katib experiments" in call("/katib/")
+        page = call("/katib/")
+        for el in (b'id="exps"', b'id="v-create"', b"formExperiment", b"parallel(", b"genotypeSvg"):
+            assert el in page  # list, creation wizard, trials charts, NAS architecture view
+        algos = json.loads(call("/katib/fetch_algorithms"))
+        assert "random" in algos["algorithms"] and "medianstop" in algos["earlyStopping"]
         e = load_experiment(EXAMPLE)
         e.spec.max_trial_count, e.spec.parallel_trial_count, e.spec.max_failed_trial_count = 2, 1, 1
-        call("/katib/create_experiment/", {"postData": e.to_k8s()})
+        import yaml as _yaml
+
+        call("/katib/create_experiment/", {"postData": _yaml.safe_dump(e.to_k8s())})  # the editor sends YAML text
         manager.run_until_complete("random-quadratic", timeout=120)
+        try:  # a finished experiment with resumePolicy Never cannot be restarted (validator.go:98-124)
+            call("/katib/edit_experiment_budget", {"experimentName": "random-quadratic", "namespace": "default",
+                                                   "maxTrialCount": 4})
+            raise RuntimeError("budget edit of a finished Never-policy experiment was accepted")
+        except AssertionError as ex:
+            assert "can be restarted" in str(ex)
         exps = json.loads(call("/katib/fetch_experiments/?namespace=default"))
         assert [(x["name"], x["type"], x["status"]) for x in exps] == [("random-quadratic", "hp", "Succeeded")]
         assert exps[0]["trialsSucceeded"] == 2
