@@ -106,6 +106,48 @@ void check_batch(const std::vector<py::tuple>& calls) {
 
 #define SAME_SHAPE(b, fld) TORCH_CHECK(b.e[i].fld == b.e[0].fld, "edges in a batch must share " #fld)
 
+// one entry of a dw-pw stage: (x, dw, pw, inbn|None, d, z, stats|None); returns whether it has an input BN
+static bool fill_dwpw(const py::tuple& t, DwPwFwdArgs& a, int64_t K, int64_t dil, int64_t S, int64_t pad, int nentries,
+                      bool use_mfma) {
+  Tensor x = t[0].cast<Tensor>(), dw = t[1].cast<Tensor>(), pw = t[2].cast<Tensor>();
+  auto inbn = t[3].cast<c10::optional<py::tuple>>();
+  Tensor d = t[4].cast<Tensor>(), z = t[5].cast<Tensor>();
+  OptT stats = t[6].cast<OptT>();
+  check_f32(x, "x"); check_f32(dw, "dw"); check_f32(pw, "pw"); check_f32(d, "d"); check_f32(z, "z");
+  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+  TORCH_CHECK((K == 3 || K == 5) && (dil == 1 || dil == 2) && (S == 1 || S == 2), "K in {3,5}, dil, S in {1,2}");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Ho = z.size(2), Wo = z.size(3);
+  TORCH_CHECK(dw.numel() == C * K * K && pw.numel() == C * C, "weight shapes");
+  TORCH_CHECK(z.size(0) == N && z.size(1) == C && d.sizes() == z.sizes(), "output shapes");
+  TORCH_CHECK(64 % Wo == 0 && Ho % (64 / Wo) == 0, "tile constraint: 64 % Wo == 0 and Ho % (64/Wo) == 0");
+  TORCH_CHECK(C <= kMaxC, "C too large");
+  TORCH_CHECK(Ho == (H + 2 * pad - dil * (K - 1) - 1) / S + 1, "output height mismatch");
+  a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.pw = pw.data_ptr<float>();
+  a.d = d.data_ptr<float>(); a.z = z.data_ptr<float>(); a.stats = ptr_or_null<double>(stats);
+  if (a.stats) TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * C, "stats f64 [kRep][2C]");
+  a.N = N; a.C = C; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.pad = pad;
+  const int TR = 64 / Wo;
+  const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
+  a.chunk = pick_chunk(C, IR * IW, C * 64 + 4 * C);
+  if (C == 4 || C == 8 || C == 16) {
+    // dwpw_plane: `chunk` = row bands per image, ~2048 workgroups per launch and >= 4
+    // output rows per band, capped so the staged band fits 64 KB of LDS
+    int nb = std::max(1, std::min(Ho / 4, 2048 / std::max(N * nentries, 1)));
+    auto band_bytes = [&](int b) {
+      const int BR = (Ho + b - 1) / b;
+      return (size_t)C * ((BR - 1) * S + (K - 1) * dil + 1) * (W + 2 * pad) * sizeof(float);
+    };
+    while (band_bytes(nb) > 65536 && nb < Ho) ++nb;
+    a.chunk = nb;
+  }
+  a.use_mfma = (use_mfma && C % 16 == 0) ? 1 : 0;
+  const bool prebn = inbn.has_value();
+  if (prebn) a.inbn = make_bn(*inbn, C);
+  a.variant = (((K == 5) * 4 + (dil == 2) * 2 + (S == 2)) * 4) + (prebn ? 2 : 0);
+  return prebn;
+}
+
 // (x, dw, pw, inbn|None, d, z, stats|None)
 void dwpw_fwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, int64_t pad, bool use_mfma) {
   check_batch<DwPwFwdBatch>(calls);
@@ -113,46 +155,37 @@ void dwpw_fwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, i
   bt.n = calls.size();
   bool prebn = false;
   for (int i = 0; i < bt.n; ++i) {
-    const py::tuple& t = calls[i];
-    Tensor x = t[0].cast<Tensor>(), dw = t[1].cast<Tensor>(), pw = t[2].cast<Tensor>();
-    auto inbn = t[3].cast<c10::optional<py::tuple>>();
-    Tensor d = t[4].cast<Tensor>(), z = t[5].cast<Tensor>();
-    OptT stats = t[6].cast<OptT>();
-    check_f32(x, "x"); check_f32(dw, "dw"); check_f32(pw, "pw"); check_f32(d, "d"); check_f32(z, "z");
-    TORCH_CHECK(x.dim() == 4, "x must be NCHW");
-    const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-    const int Ho = z.size(2), Wo = z.size(3);
-    TORCH_CHECK(dw.numel() == C * K * K && pw.numel() == C * C, "weight shapes");
-    TORCH_CHECK(z.size(0) == N && z.size(1) == C && d.sizes() == z.sizes(), "output shapes");
-    TORCH_CHECK(64 % Wo == 0 && Ho % (64 / Wo) == 0, "tile constraint: 64 % Wo == 0 and Ho % (64/Wo) == 0");
-    TORCH_CHECK(C <= kMaxC, "C too large");
-    TORCH_CHECK(Ho == (H + 2 * pad - dil * (K - 1) - 1) / S + 1, "output height mismatch");
-    DwPwFwdArgs& a = bt.e[i];
-    a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.pw = pw.data_ptr<float>();
-    a.d = d.data_ptr<float>(); a.z = z.data_ptr<float>(); a.stats = ptr_or_null<double>(stats);
-    if (a.stats) TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * C, "stats f64 [kRep][2C]");
-    a.N = N; a.C = C; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.pad = pad;
-    const int TR = 64 / Wo;
-    const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (Wo - 1) * S + (K - 1) * dil + 1;
-    a.chunk = pick_chunk(C, IR * IW, C * 64 + 4 * C);
-    if (C == 4 || C == 8 || C == 16) {
-      // dwpw_plane: `chunk` = row bands per image, ~2048 workgroups per launch and >= 4
-      // output rows per band, capped so the staged band fits 64 KB of LDS
-      int nb = std::max(1, std::min(Ho / 4, 2048 / std::max(N * (int)calls.size(), 1)));
-      auto band_bytes = [&](int b) {
-        const int BR = (Ho + b - 1) / b;
-        return (size_t)C * ((BR - 1) * S + (K - 1) * dil + 1) * (W + 2 * pad) * sizeof(float);
-      };
-      while (band_bytes(nb) > 65536 && nb < Ho) ++nb;
-      a.chunk = nb;
-    }
-    a.use_mfma = (use_mfma && C % 16 == 0) ? 1 : 0;
-    if (i == 0) prebn = inbn.has_value();
-    TORCH_CHECK(inbn.has_value() == prebn, "edges in a batch must agree on the input BN");
-    if (prebn) a.inbn = make_bn(*inbn, C);
+    const bool pb = fill_dwpw(calls[i], bt.e[i], K, dil, S, pad, bt.n, use_mfma);
+    if (i == 0) prebn = pb;
+    TORCH_CHECK(pb == prebn, "edges in a batch must agree on the input BN");
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
   }
   launch_dwpw_fwd(bt, K, dil, S, prebn, cur_stream());
+}
+
+// Mixed (K, dil, S, input-BN) entries of one node stage in one launch:
+// (x, dw, pw, inbn|None, d, z, stats|None, K, dil, S, pad) per entry. Entries that do not fit the
+// plane kernels (channel counts, alignment) run as per-group launches instead.
+void dwpw_fwd_multi(std::vector<py::tuple> calls) {
+  TORCH_CHECK(!calls.empty() && (int)calls.size() <= DwPwMultiBatch::kCap, "1..", DwPwMultiBatch::kCap, " entries");
+  DwPwMultiBatch bt{};
+  bt.n = calls.size();
+  int64_t kk[DwPwMultiBatch::kCap], dd[DwPwMultiBatch::kCap], ss[DwPwMultiBatch::kCap], pp[DwPwMultiBatch::kCap];
+  bool pre[DwPwMultiBatch::kCap];
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    TORCH_CHECK(t.size() == 11, "dwpw_fwd_multi entry: (x, dw, pw, inbn, d, z, stats, K, dil, S, pad)");
+    kk[i] = t[7].cast<int64_t>(); dd[i] = t[8].cast<int64_t>(); ss[i] = t[9].cast<int64_t>(); pp[i] = t[10].cast<int64_t>();
+    pre[i] = fill_dwpw(t, bt.e[i], kk[i], dd[i], ss[i], pp[i], bt.n, true);
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, Ho); SAME_SHAPE(bt, Wo);
+  }
+  if (launch_dwpw_multi(bt, cur_stream())) return;
+  for (int i = 0; i < bt.n; ++i) {  // fallback: one launch per entry (the plane path's band count is per batch)
+    DwPwFwdBatch one{};
+    one.n = 1;
+    fill_dwpw(calls[i], one.e[0], kk[i], dd[i], ss[i], pp[i], 1, true);
+    launch_dwpw_fwd(one, kk[i], dd[i], ss[i], pre[i], cur_stream());
+  }
 }
 
 // (x, pw, z, stats|None, co_off, off)
@@ -183,13 +216,16 @@ void pw_fwd(std::vector<py::tuple> calls, int64_t S) {
   launch_pw_fwd(bt, cur_stream());
 }
 
-// (x, zavg, zmax, stats_avg|None, stats_max|None, amax|None)
-void pool_fwd(std::vector<py::tuple> calls, int64_t S) {
+// (x, zavg, zmax, stats_avg|None, stats_max|None, amax|None[, S]); S < 0: per-entry S (7th field)
+static void pool_fwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
   check_batch<PoolFwdBatch>(calls);
   PoolFwdBatch bt{};
   bt.n = calls.size();
   for (int i = 0; i < bt.n; ++i) {
     const py::tuple& t = calls[i];
+    const int64_t S = S_all > 0 ? S_all : t[6].cast<int64_t>();
+    TORCH_CHECK(S == 1 || S == 2, "pool stride must be 1 or 2");
+    bt.e[i].S = (int)S;
     Tensor x = t[0].cast<Tensor>(), zavg = t[1].cast<Tensor>(), zmax = t[2].cast<Tensor>();
     OptT sa = t[3].cast<OptT>(), sm = t[4].cast<OptT>(), amax = t[5].cast<OptT>();
     check_f32(x, "x"); check_f32(zavg, "zavg"); check_f32(zmax, "zmax");
@@ -204,10 +240,16 @@ void pool_fwd(std::vector<py::tuple> calls, int64_t S) {
     if (a.stats_max) TORCH_CHECK(sm->scalar_type() == at::kDouble && sm->numel() >= kRep * 2 * x.size(1), "stats");
     a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = zavg.size(2); a.Wo = zavg.size(3);
     TORCH_CHECK(a.Ho == (a.H - 1) / S + 1 && zmax.sizes() == zavg.sizes(), "pool shapes");
-    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C);
+    if (S_all > 0) { SAME_SHAPE(bt, H); SAME_SHAPE(bt, W); }
   }
-  launch_pool_fwd(bt, S, cur_stream());
+  if (S_all > 0) launch_pool_fwd(bt, S_all, cur_stream());
+  else launch_pool_fwd_multi(bt, cur_stream());
 }
+
+void pool_fwd(std::vector<py::tuple> calls, int64_t S) { pool_fwd_impl(calls, S); }
+// stride-1 and stride-2 pools of a node in one launch: (..., amax|None, S) per entry
+void pool_fwd_multi(std::vector<py::tuple> calls) { pool_fwd_impl(calls, -1); }
 
 // calls: per edge (zs, bns, widx, w|None, id_idx, xid|None, upd); all edges summed into `out`
 void combine_fwd(std::vector<py::tuple> calls, OptT gamma, OptT beta, Tensor out, double momentum,
@@ -394,13 +436,16 @@ void dw_bwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, int
   launch_dw_bwd(bt, K, dil, S, prebn, cur_stream());
 }
 
-// (ga|None, gm|None, x, dout_id|None, w|None, id_idx, gx, amax|None, overwrite)
-void pool_bwd(std::vector<py::tuple> calls, int64_t S) {
+// (ga|None, gm|None, x, dout_id|None, w|None, id_idx, gx, amax|None, overwrite[, S]); S < 0: per entry
+static void pool_bwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
   check_batch<PoolBwdBatch>(calls);
   PoolBwdBatch bt{};
   bt.n = calls.size();
   for (int i = 0; i < bt.n; ++i) {
     const py::tuple& t = calls[i];
+    const int64_t S = S_all > 0 ? S_all : t[9].cast<int64_t>();
+    TORCH_CHECK(S == 1 || S == 2, "pool stride must be 1 or 2");
+    bt.e[i].S = (int)S;
     auto ga = t[0].cast<c10::optional<py::tuple>>(), gm = t[1].cast<c10::optional<py::tuple>>();
     Tensor x = t[2].cast<Tensor>();
     OptT dout_id = t[3].cast<OptT>(), w = t[4].cast<OptT>();
@@ -423,10 +468,18 @@ void pool_bwd(std::vector<py::tuple> calls, int64_t S) {
     if (a.dout_id) TORCH_CHECK(dout_id->sizes() == x.sizes(), "identity gradient shape");
     a.id_idx = id_idx; a.gx = gx.data_ptr<float>();
     a.overwrite = t[8].cast<bool>();
-    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C);
+    if (S_all > 0) { SAME_SHAPE(bt, H); SAME_SHAPE(bt, W); }
   }
-  launch_pool_bwd(bt, S, cur_stream());
+  // entries of one launch must write distinct input gradients (no ordering between them)
+  for (int i = 0; i < bt.n; ++i)
+    for (int j = i + 1; j < bt.n; ++j) TORCH_CHECK(bt.e[i].gx != bt.e[j].gx, "pool_bwd entries share a gx buffer");
+  if (S_all > 0) launch_pool_bwd(bt, S_all, cur_stream());
+  else launch_pool_bwd_multi(bt, cur_stream());
 }
+
+void pool_bwd(std::vector<py::tuple> calls, int64_t S) { pool_bwd_impl(calls, S); }
+void pool_bwd_multi(std::vector<py::tuple> calls) { pool_bwd_impl(calls, -1); }
 
 void fold_rows(Tensor buf) {
   check_f32(buf, "buf");
@@ -479,6 +532,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pw_bwd", &pw_bwd);
   m.def("dw_bwd", &dw_bwd);
   m.def("pool_bwd", &pool_bwd);
+  m.def("dwpw_fwd_multi", &dwpw_fwd_multi, "mixed (K, dil, S) dw-pw entries of one node stage in one launch");
+  m.def("pool_fwd_multi", &pool_fwd_multi, "stride-1 and stride-2 pools in one launch");
+  m.def("pool_bwd_multi", &pool_bwd_multi, "stride-1 and stride-2 pool backward in one launch");
   m.def("set_max_blocks", &set_max_blocks);
   m.def("fold_rows", &fold_rows);
   m.def("fold_f64", &fold_f64);

@@ -45,6 +45,8 @@ struct DwPwFwdArgs {
   const float* x; BNRef inbn; const float* dw; const float* pw;
   float* d; float* z; double* stats;  // stats: kRep replicas of [2C]
   int N, C, H, W, Ho, Wo, pad, chunk, use_mfma;
+  int variant;  // dwpw_plane_multi_kernel: ((K == 5) * 4 + (dil == 2) * 2 + (S == 2)) * 4 + prebn * 2 + vec
+  int nblk;     // dwpw_plane_multi_kernel: workgroups of this entry (grid.x is the max over entries)
 };
 
 struct PwFwdArgs {
@@ -56,6 +58,7 @@ struct PwFwdArgs {
 struct PoolFwdArgs {
   const float* x; float* zavg; float* zmax; double* stats_avg; double* stats_max; unsigned char* amax;
   int N, C, H, W, Ho, Wo;  // stats: kRep replicas of [2C] each
+  int S, nblk;             // pool_fwd_multi_kernel: per-entry stride and workgroups
 };
 
 struct CombineFwdArgs {
@@ -100,6 +103,7 @@ struct PoolBwdArgs {
   const unsigned char* amax;
   int overwrite;  // gx = result instead of +=
   int N, C, H, W, Ho, Wo;
+  int S;          // pool_bwd_multi_kernel: per-entry stride
 };
 
 // Edge batches: one launch runs the same kernel for up to M edges of a DARTS node that share
@@ -118,6 +122,9 @@ using CombineBwdBatch = Batch<CombineBwdArgs, 4>;
 using PwBwdBatch = Batch<PwBwdArgs, 8>;
 using DwBwdBatch = Batch<DwBwdArgs, 8>;
 using PoolBwdBatch = Batch<PoolBwdArgs, 8>;
+using DwPwMultiBatch = Batch<DwPwFwdArgs, 16>;  // a node's stage-1 (or stage-2) dw-pw entries, mixed K/dil/S
+static_assert(sizeof(DwPwMultiBatch) <= 4096 && sizeof(PoolBwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096,
+              "kernel argument blocks must fit the 4 KB kernarg segment");
 static_assert(sizeof(DwPwFwdBatch) <= 4096 && sizeof(CombineFwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096 && sizeof(PoolFwdBatch) <= 4096 &&
                   sizeof(CombineBwdBatch) <= 4096 && sizeof(PwBwdBatch) <= 4096 && sizeof(DwBwdBatch) <= 4096 &&
                   sizeof(PoolBwdBatch) <= 4096,
@@ -128,6 +135,10 @@ void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipSt
 void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st);
 void launch_pool_fwd(const PoolFwdBatch& b, int S, hipStream_t st);
 void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st);
+// mixed-variant launches: one launch for entries with different kernel size / dilation / stride
+bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st);
+void launch_pool_fwd_multi(PoolFwdBatch b, hipStream_t st);
+void launch_pool_bwd_multi(const PoolBwdBatch& b, hipStream_t st);
 void launch_combine_fwd(const CombineFwdBatch& b, hipStream_t st);
 void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st);
 void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st);

@@ -296,14 +296,13 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
 // ------------------------------------------------------------------------------------------------
 // PW = false (layers wider than 16 channels): depthwise only, d of C-channel group blockIdx.x % (a.C / C);
 // the pointwise then runs as its own GEMM (pw_fwd_wave_kernel)
-template <int K, int DIL, int S, bool PREBN, int C, bool VEC, bool PW = true>
-__global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
-  const DwPwFwdArgs& a = bt.e[blockIdx.y];
+template <int K, int DIL, int S, bool PREBN, int C, bool VEC, bool PW>
+__device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int bx) {
   constexpr int KK = K * K;
   const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, pad = a.pad;
   // workgroup = (image n, band of BR output rows); the band's input rows + halo are staged
   const int nb = a.chunk, BR = (Ho + nb - 1) / nb;  // chunk carries the band count
-  const int G = PW ? 1 : a.C / C, c0 = PW ? 0 : (blockIdx.x % G) * C, nbx = PW ? blockIdx.x : blockIdx.x / G;
+  const int G = PW ? 1 : a.C / C, c0 = PW ? 0 : (bx % G) * C, nbx = PW ? bx : bx / G;
   const int n = nbx / nb, band = nbx - n * nb;
   const int oy0 = band * BR, oy1 = min(Ho, oy0 + BR);
   const int HP = (BR - 1) * S + (K - 1) * DIL + 1, WP = W + 2 * pad, PL = HP * WP;
@@ -410,8 +409,38 @@ __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
     if ((lane & (32 / C - 1)) == 0) atomicAdd(sStat + wave_scatter_index<2 * C>(lane), v);
   }
   __syncthreads();
-  if (tid < 2 * C) atomicAdd(a.stats + rep_slot() * 2 * C + tid, (double)sStat[tid]);
+  if (tid < 2 * C) atomicAdd(a.stats + (bx % kRep) * 2 * C + tid, (double)sStat[tid]);
 }
+template <int K, int DIL, int S, bool PREBN, int C, bool VEC, bool PW = true>
+__global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
+  dwpw_plane_body<K, DIL, S, PREBN, C, VEC, PW>(bt.e[blockIdx.y], blockIdx.x);
+}
+
+// One launch for a node's whole separable-stage / dilated-conv forward: every entry (edge x
+// primitive) carries its own kernel size, dilation, stride, input-BN flag and band count, and
+// each workgroup runs the fully unrolled body of its entry's (K, DIL, S, PREBN, VEC) variant.
+// The entries are independent, so their workgroups overlap instead of running as 4-9 serial
+// launches that each leave most of the chip waiting on their own tails.
+#define DWPW_CASE(KK, DD, SS)                                                                      \
+  case ((KK == 5) * 4 + (DD == 2) * 2 + (SS == 2)) * 4 + 0: dwpw_plane_body<KK, DD, SS, false, C, false, PW>(a, bx); break; \
+  case ((KK == 5) * 4 + (DD == 2) * 2 + (SS == 2)) * 4 + 1: dwpw_plane_body<KK, DD, SS, false, C, true, PW>(a, bx); break;  \
+  case ((KK == 5) * 4 + (DD == 2) * 2 + (SS == 2)) * 4 + 2: dwpw_plane_body<KK, DD, SS, true, C, false, PW>(a, bx); break;  \
+  case ((KK == 5) * 4 + (DD == 2) * 2 + (SS == 2)) * 4 + 3: dwpw_plane_body<KK, DD, SS, true, C, true, PW>(a, bx); break;
+template <int C, bool PW>
+__global__ void __launch_bounds__(256) dwpw_plane_multi_kernel(DwPwMultiBatch bt) {
+  // a COPY of the entry: a reference into the by-value batch made hipcc spill the whole 2.3 KB
+  // batch to scratch once 32 variant bodies use it (ScratchSize 2320 B/lane, 20x slower)
+  const DwPwFwdArgs a = bt.e[blockIdx.y];
+  const int bx = blockIdx.x;
+  if (bx >= a.nblk) return;  // entries differ in their band counts (uniform per workgroup)
+  switch (a.variant) {
+    DWPW_CASE(3, 1, 1) DWPW_CASE(3, 1, 2) DWPW_CASE(5, 1, 1) DWPW_CASE(5, 1, 2)
+    DWPW_CASE(3, 2, 1) DWPW_CASE(3, 2, 2) DWPW_CASE(5, 2, 1) DWPW_CASE(5, 2, 2)
+    default: break;
+  }
+}
+#undef DWPW_CASE
+
 
 // ------------------------------------------------------------------------------------------------
 // pw_fwd_wave: z[:, co_off + co] = pw . act(x) for Cin, Cout multiples of 16 (<= 64), plus the BN
@@ -582,10 +611,9 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdBatch bt) {
 // pool_fwd: avg (count_include_pad=False) and max 3x3/pad 1, stride S. One block per (n, c) plane.
 // ------------------------------------------------------------------------------------------------
 template <int S>
-__global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdBatch bt) {
-  const PoolFwdArgs& a = bt.e[blockIdx.y];
+__device__ __forceinline__ void pool_fwd_body(const PoolFwdArgs& a, const int bx, const int gx) {
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
-  const int c = blockIdx.x % C, g0 = blockIdx.x / C, G = gridDim.x / C;
+  const int c = bx % C, g0 = bx / C, G = gx / C;
   float sa = 0, sa2 = 0, sm = 0, sm2 = 0;
   for (int n = g0; n < a.N; n += G) {
     const int nc = n * C + c;
@@ -631,9 +659,22 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdBatch bt) {
   if (threadIdx.x < 4) {
     float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     double* dst = threadIdx.x < 2 ? a.stats_avg : a.stats_max;
-    if (dst) atomicAdd(dst + rep_slot() * 2 * C + (threadIdx.x & 1) * C + c, (double)t);
+    if (dst) atomicAdd(dst + (bx % kRep) * 2 * C + (threadIdx.x & 1) * C + c, (double)t);
   }
 }
+template <int S>
+__global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdBatch bt) {
+  pool_fwd_body<S>(bt.e[blockIdx.y], blockIdx.x, gridDim.x);
+}
+
+// stride-1 and stride-2 pooling of a node in one launch (entry a.S; a.nblk workgroups, a multiple of C)
+__global__ void __launch_bounds__(256) pool_fwd_multi_kernel(PoolFwdBatch bt) {
+  const PoolFwdArgs a = bt.e[blockIdx.y];  // copy: see dwpw_plane_multi_kernel
+  if ((int)blockIdx.x >= a.nblk) return;
+  if (a.S == 1) pool_fwd_body<1>(a, blockIdx.x, a.nblk);
+  else pool_fwd_body<2>(a, blockIdx.x, a.nblk);
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // combine_fwd: out = sum_k w[k] * BN_k(z_k) + wid * x  (elementwise), running stats in block 0
@@ -1490,10 +1531,9 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
 // pool_bwd: gx += avg^T(dz_avg) + max^T(dz_max) + wid * dout (identity skip), per (n,c) plane
 // ------------------------------------------------------------------------------------------------
 template <int S>
-__global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdBatch bt) {
-  const PoolBwdArgs& a = bt.e[blockIdx.y];
+__device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx) {
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, HWo = Ho * Wo;
-  const int nc = blockIdx.x, c = nc % C;
+  const int nc = bx, c = nc % C;
   const size_t ob = (size_t)nc * HWo;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sGa = smem;                                          // [HWo] dz_avg / window count
@@ -1550,6 +1590,19 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdBatch bt) {
     else a.gx[(size_t)nc * H * W + q] += g;
   }
 }
+template <int S>
+__global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdBatch bt) {
+  pool_bwd_body<S>(bt.e[blockIdx.y], blockIdx.x);
+}
+
+// stride-1 and stride-2 pool backward of a node in one launch (different edges: different gx)
+__global__ void __launch_bounds__(256) pool_bwd_multi_kernel(PoolBwdBatch bt) {
+  const PoolBwdArgs a = bt.e[blockIdx.y];  // copy: see dwpw_plane_multi_kernel
+  if ((int)blockIdx.x >= a.N * a.C) return;
+  if (a.S == 1) pool_bwd_body<1>(a, blockIdx.x);
+  else pool_bwd_body<2>(a, blockIdx.x);
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // dw_bwd_plane: dw_bwd for narrow layers (C <= 16), the backward twin of dwpw_plane. One
@@ -1860,6 +1913,96 @@ void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, h
   DISPATCH(3, 1, 1) DISPATCH(3, 1, 2) DISPATCH(5, 1, 1) DISPATCH(5, 1, 2)
   DISPATCH(3, 2, 1) DISPATCH(3, 2, 2) DISPATCH(5, 2, 1) DISPATCH(5, 2, 2)
 #undef DISPATCH
+}
+
+// ------------------------------------------------------------------------------------------------
+// Mixed-variant launches (one per node stage instead of one per (K, dil, S) group). The entries
+// must share the channel count; returns false (nothing launched) when they do not fit the plane
+// kernels, and the caller falls back to the per-group launches.
+// ------------------------------------------------------------------------------------------------
+static int channel_groups(int N, int C, int n);
+
+bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st) {
+  if (b.n < 1) return true;
+  const int C = b.e[0].C, N = b.e[0].N;
+  static const bool split16 = !getenv("KATIB_HIP_DWPW_SPLIT") || atoi(getenv("KATIB_HIP_DWPW_SPLIT")) > 0;
+  const bool fused = C == 4 || C == 8 || (C == 16 && !split16);
+  const bool split = !fused && C % 16 == 0 && C <= 64;
+  if (!fused && !split) return false;
+  const int CG = fused ? C : 8, G = C / CG;
+  int maxblk = 0;
+  size_t lds = 0;
+  for (int i = 0; i < b.n; ++i) {
+    DwPwFwdArgs& a = b.e[i];
+    if (a.C != C || a.N != N) return false;
+    const int code = a.variant >> 2;
+    const int K = (code & 4) ? 5 : 3, DIL = (code & 2) ? 2 : 1, S = (code & 1) ? 2 : 1;
+    const bool aligned = ((((uintptr_t)a.x) | (uintptr_t)a.d | (uintptr_t)a.z) & 15) == 0;
+    if (split && (!aligned || (a.Ho * a.Wo) % 64 != 0 || a.W % 4 != 0)) return false;
+    int nb = std::max(1, std::min(a.Ho / 4, 2048 / std::max(N * b.n * G, 1)));
+    auto band_bytes = [&](int v) {
+      const int BR = (a.Ho + v - 1) / v;
+      return (size_t)CG * ((BR - 1) * S + (K - 1) * DIL + 1) * (a.W + 2 * a.pad) * sizeof(float);
+    };
+    while (band_bytes(nb) > 65536 && nb < a.Ho) ++nb;
+    a.chunk = nb;
+    a.nblk = N * nb * G;
+    const bool vec = a.W % 4 == 0 && (((uintptr_t)a.x) & 15) == 0;
+    a.variant = (a.variant & ~1) | (vec ? 1 : 0);
+    maxblk = std::max(maxblk, a.nblk);
+    lds = std::max(lds, band_bytes(nb));
+  }
+  const dim3 grid(maxblk, b.n);
+  if (fused) {
+    if (C == 4) hipLaunchKernelGGL((dwpw_plane_multi_kernel<4, true>), grid, dim3(256), lds, st, b);
+    else if (C == 8) hipLaunchKernelGGL((dwpw_plane_multi_kernel<8, true>), grid, dim3(256), lds, st, b);
+    else hipLaunchKernelGGL((dwpw_plane_multi_kernel<16, true>), grid, dim3(256), lds, st, b);
+    return true;
+  }
+  hipLaunchKernelGGL((dwpw_plane_multi_kernel<8, false>), grid, dim3(256), lds, st, b);
+  // the pointwise halves + BN statistics of every entry: one MFMA wave launch
+  PwFwdBatch pb{};
+  pb.n = b.n;
+  for (int i = 0; i < b.n; ++i) {
+    const DwPwFwdArgs& e = b.e[i];
+    PwFwdArgs& p = pb.e[i];
+    p.x = e.d; p.pw = e.pw; p.z = e.z; p.stats = e.stats;
+    p.N = e.N; p.Cin = e.C; p.Cout = e.C; p.CoutTotal = e.C; p.co_off = 0;
+    p.H = e.Ho; p.W = e.Wo; p.Ho = e.Ho; p.Wo = e.Wo; p.S = 1; p.off = 0; p.relu = 0;
+  }
+  bool same_hw = true;
+  for (int i = 1; i < b.n; ++i) same_hw &= b.e[i].Ho == b.e[0].Ho && b.e[i].Wo == b.e[0].Wo;
+  if (same_hw && (try_pw_fwd_wave<16, 16>(pb, st) || try_pw_fwd_wave<32, 32>(pb, st) || try_pw_fwd_wave<64, 64>(pb, st)))
+    return true;
+  for (int i = 0; i < b.n; ++i) {  // mixed output sizes (stride-1 and stride-2 entries): per entry
+    PwFwdBatch one{};
+    one.n = 1;
+    one.e[0] = pb.e[i];
+    if (!(try_pw_fwd_wave<16, 16>(one, st) || try_pw_fwd_wave<32, 32>(one, st) || try_pw_fwd_wave<64, 64>(one, st)))
+      launch_pw_fwd(one, st);
+  }
+  return true;
+}
+
+void launch_pool_fwd_multi(PoolFwdBatch b, hipStream_t st) {
+  int maxblk = 0;
+  for (int i = 0; i < b.n; ++i) {
+    PoolFwdArgs& a = b.e[i];
+    a.nblk = a.C * channel_groups(a.N, a.C, b.n);
+    maxblk = std::max(maxblk, a.nblk);
+  }
+  hipLaunchKernelGGL(pool_fwd_multi_kernel, dim3(maxblk, b.n), dim3(256), 0, st, b);
+}
+
+void launch_pool_bwd_multi(const PoolBwdBatch& b, hipStream_t st) {
+  int maxblk = 0;
+  size_t lds = 0;
+  for (int i = 0; i < b.n; ++i) {
+    const PoolBwdArgs& a = b.e[i];
+    maxblk = std::max(maxblk, a.N * a.C);
+    lds = std::max(lds, sizeof(float) * 2 * a.Ho * a.Wo + a.Ho * a.Wo + 16);
+  }
+  hipLaunchKernelGGL(pool_bwd_multi_kernel, dim3(maxblk, b.n), dim3(256), lds, st, b);
 }
 
 // LDS floats of one dw_bwd_plane band (nb bands per image)

@@ -150,6 +150,40 @@ def _launch(name: str, calls: List, *args):
         fn(calls[i:i + cap], *args)
 
 
+MULTI = __import__("os").environ.get("KATIB_HIP_MULTI", "1") != "0"  # mixed-variant launches (A/B switch)
+
+
+def _dwpw_multi(entries):
+    """dw-pw entries (x, dw, pw, inbn, d, z, stats, K, dil, S, pad) of one stage, mixed kernel sizes,
+    dilations and strides: one launch per 16 entries (per (K, dil, S) group with MULTI off)."""
+    if not entries:
+        return
+    if MULTI:
+        for i in range(0, len(entries), 16):
+            _K.dwpw_fwd_multi(entries[i:i + 16])
+        return
+    groups = defaultdict(list)
+    for e in entries:
+        groups[e[7:]].append(e[:7])
+    for (K, dil, S, pad), calls in groups.items():
+        _launch("dwpw_fwd", calls, K, dil, S, pad, True)
+
+
+def _pool_multi(entries):
+    """pool_fwd entries (x, zavg, zmax, stats_avg, stats_max, amax, S) of both strides."""
+    if not entries:
+        return
+    if MULTI:
+        for i in range(0, len(entries), _CAP["pool_fwd"]):
+            _K.pool_fwd_multi(entries[i:i + _CAP["pool_fwd"]])
+        return
+    groups = defaultdict(list)
+    for e in entries:
+        groups[e[6]].append(e[:6])
+    for S, calls in groups.items():
+        _launch("pool_fwd", calls, S)
+
+
 class EdgeSpec:
     """Static description of one edge: primitives, stride, parameter names, BN slots.
 
@@ -300,12 +334,12 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
             else:
                 raise ValueError(prim)
             e.widx.append(k)
-    # (forking these independent groups over side streams - concurrent graph branches - was
-    # measured slower on MI355X: B5 step 15.4 ms vs 13.05 ms sequential)
-    for (K, dil, S, pad), calls in dw_groups.items():
-        _launch("dwpw_fwd", calls, K, dil, S, pad, True)
-    for S, calls in pool_groups.items():
-        _launch("pool_fwd", calls, S)
+    # all (K, dil, S) groups of the stage in ONE mixed-variant launch (and both pool strides in
+    # one): independent entries overlap on the chip instead of running as 4-9 serial launches
+    # (forking the groups over side streams - concurrent graph branches - measured slower on
+    # MI355X: B5 step 15.4 ms vs 13.05 ms sequential)
+    _dwpw_multi([(*c, K, dil, S, pad) for (K, dil, S, pad), calls in dw_groups.items() for c in calls])
+    _pool_multi([(*c, S) for S, calls in pool_groups.items() for c in calls])
     if fr_calls:
         _launch("pw_fwd", fr_calls, 2)
     if training and stage1:
@@ -324,8 +358,7 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
                 e.upd.append(e.refs[sl[0]])
                 e.zs[k], e.bns[k] = z2, e.refs[sl[1]]
                 e.saved[prim] = (d1, z1, d2, z2)
-    for K, calls in s2_groups.items():
-        _launch("dwpw_fwd", calls, K, 1, 1, K // 2, True)
+    _dwpw_multi([(*c, K, 1, 1, K // 2) for K, calls in s2_groups.items() for c in calls])
     if training and stage2:
         _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage2))])
     # ---- weighted sums into the node output
@@ -379,8 +412,20 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
 
     gxs = [gx_of(e.i) for e in edges]
 
+    # dilated convs' pointwise backward is independent of the separable chain: its entries join
+    # the separable second stages' pw_bwd batch (one launch instead of two)
+    dils = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("dilated_convolution")]
+    pwd, dd_of = [], {}
+    for e, k, prim in dils:
+        d, z = e.saved[prim]
+        dd = torch.empty_like(d)
+        dd_of[(e.i, prim)] = dd
+        g, gst = sink(e, prim + ".pw")
+        pwd.append((src(e, k, z), e.P[prim + ".pw"], d, e.x, dd, None, g, 0, 0, gst))
     # ---- separable convs: both second stages, one fold, both first stages
     seps = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("separable_convolution")]
+    if not seps and pwd:
+        _launch("pw_bwd", pwd, 1, 0, True)
     if seps:
         red1 = zeros64(len(seps) * REP * 2 * C, dev) if training else None
         pw2, dw2 = [], defaultdict(list)
@@ -395,7 +440,9 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
             g, gst = sink(e, prim + ".1.dw")
             dw2[K].append((z1, e.refs[e.spec.slots[prim][0]], e.P[prim + ".1.dw"], dd2, g1, g, r1, gst, False))
             e.saved[prim + "/g1"] = (g1, r1)
-        _launch("pw_bwd", pw2, 1, 0, True)
+        _launch("pw_bwd", pw2 + (pwd if MULTI else []), 1, 0, True)
+        if not MULTI and pwd:
+            _launch("pw_bwd", pwd, 1, 0, True)
         for K, calls in dw2.items():
             _launch("dw_bwd", calls, K, 1, 1, K // 2)
         if training:
@@ -415,19 +462,14 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
         _launch("pw_bwd", pw1, 1, 0, True)
         for (K, S), calls in dw1.items():
             _launch("dw_bwd", calls, K, 1, S, K // 2)
-    # ---- dilated convs
-    dils = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("dilated_convolution")]
+    # ---- dilated convs (depthwise backward; the pointwise part ran above)
     if dils:
-        pwd, dwd = [], defaultdict(list)
+        dwd = defaultdict(list)
         for e, k, prim in dils:
             K = int(prim[-1])
-            d, z = e.saved[prim]
-            dd = torch.empty_like(d)
-            g, gst = sink(e, prim + ".pw")
-            pwd.append((src(e, k, z), e.P[prim + ".pw"], d, e.x, dd, None, g, 0, 0, gst))
             g, gst = sink(e, prim + ".dw")
-            dwd[(K, e.S)].append((e.x, None, e.P[prim + ".dw"], dd, gxs[e.i], g, None, gst, take_first(e.i)))
-        _launch("pw_bwd", pwd, 1, 0, True)
+            dwd[(K, e.S)].append((e.x, None, e.P[prim + ".dw"], dd_of[(e.i, prim)], gxs[e.i], g, None, gst,
+                                  take_first(e.i)))
         for (K, S), calls in dwd.items():
             _launch("dw_bwd", calls, K, 2, S, (K // 2) * 2)
     # ---- pools (+ the identity skip of stride-1 edges)
@@ -445,8 +487,13 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
         pools[e.S].append((ga, gm, e.x, dout if e.id_idx >= 0 else None, e.w, e.id_idx, gxs[e.i], am,
                            take_first(e.i)))
         e.id_done = True
-    for S, calls in pools.items():
-        _launch("pool_bwd", calls, S)
+    if MULTI:  # both strides in one launch (entries are distinct edges: distinct gx buffers)
+        allp = [(*c, S) for S, calls in pools.items() for c in calls]
+        for i in range(0, len(allp), _CAP["pool_bwd"]):
+            _K.pool_bwd_multi(allp[i:i + _CAP["pool_bwd"]])
+    else:
+        for S, calls in pools.items():
+            _launch("pool_bwd", calls, S)
     for e in edges:
         if e.id_idx >= 0 and not e.id_done:
             if take_first(e.i):
