@@ -56,6 +56,10 @@ int64_t storage_doubles_after(const Tensor& t) {
   return (int64_t)(t.storage().nbytes() / sizeof(double)) - t.storage_offset();
 }
 
+int64_t gs_numel(const py::tuple& t) {
+  return t[1].cast<Tensor>().numel();  // z, the pre-BN output the gradient is evaluated on
+}
+
 GradSrc make_gs(const py::tuple& t, int C) {
   GradSrc g{};
   TORCH_CHECK(t.size() == 9, "grad-source tuple has 9 fields");
@@ -85,6 +89,68 @@ GradSrc make_gs(const py::tuple& t, int C) {
     }
   }
   return g;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Self-folding launches (darts_ops.h FoldTail): a per-device ring of zeroed arrival counters,
+// registered once from Python outside any graph capture (set_fold_counters); every launch that
+// produces replicated f64 sums takes the next counter. Off unless KATIB_HIP_SELFFOLD=1 (the
+// Python side then launches fold_f64 as before; selffold_ready() tells it which mode is live).
+// ------------------------------------------------------------------------------------------------
+struct CtrRing {
+  unsigned* base = nullptr;
+  int size = 0;
+  int cursor = 0;
+};
+CtrRing g_ring[64];
+bool g_selffold = getenv("KATIB_HIP_SELFFOLD") && atoi(getenv("KATIB_HIP_SELFFOLD")) != 0;  // measured slower
+
+void set_selffold(bool on) { g_selffold = on; }
+
+int cur_device() {
+  int d = 0;
+  TORCH_CHECK(hipGetDevice(&d) == hipSuccess, "hipGetDevice");
+  return d;
+}
+
+void set_fold_counters(Tensor t) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.is_contiguous() && t.numel() >= 4 * kFoldCtrSlot,
+              "fold counters: contiguous int32 GPU tensor of >= 4 launch slots");
+  const int d = t.get_device();
+  TORCH_CHECK(d >= 0 && d < 64, "device index");
+  g_ring[d] = CtrRing{reinterpret_cast<unsigned*>(t.data_ptr<int>()), (int)(t.numel() / kFoldCtrSlot), 0};
+}
+
+bool selffold_ready() { return g_selffold && g_ring[cur_device()].base != nullptr; }
+
+void tail_begin(FoldTail& t) {
+  t.nseg = 0;
+  t.ctr = nullptr;
+  if (!g_selffold) return;
+  CtrRing& r = g_ring[cur_device()];
+  if (!r.base) return;
+  t.ctr = r.base + (size_t)r.cursor * kFoldCtrSlot;  // size counts launch slots
+  r.cursor = (r.cursor + 1) % r.size;
+}
+
+void tail_add(FoldTail& t, double* p, int n, int rs) {
+  if (!t.ctr || !p) return;
+  for (int s = 0; s < t.nseg; ++s)
+    if (t.p[s] == p) {
+      t.n[s] = std::max(t.n[s], n);
+      return;
+    }
+  TORCH_CHECK(t.nseg < kTailSeg, "self-fold: too many reduction segments in one launch");
+  // (a launch with no segment keeps ctr == nullptr: see tail_close)
+  t.p[t.nseg] = p;
+  t.n[t.nseg] = n;
+  t.rs[t.nseg] = rs;
+  ++t.nseg;
+}
+
+// a launch that ended up with nothing to fold (eval mode: no statistics) skips the epilogue
+void tail_close(FoldTail& t) {
+  if (t.nseg == 0) t.ctr = nullptr;
 }
 
 int pick_chunk(int C, int per_channel_floats, int fixed_floats) {
@@ -160,6 +226,9 @@ void dwpw_fwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, i
     TORCH_CHECK(pb == prebn, "edges in a batch must agree on the input BN");
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
   }
+  tail_begin(bt.tail);
+  for (int i = 0; i < bt.n; ++i) tail_add(bt.tail, bt.e[i].stats, 2 * bt.e[i].C, 2 * bt.e[i].C);
+  tail_close(bt.tail);
   launch_dwpw_fwd(bt, K, dil, S, prebn, cur_stream());
 }
 
@@ -179,10 +248,14 @@ void dwpw_fwd_multi(std::vector<py::tuple> calls) {
     pre[i] = fill_dwpw(t, bt.e[i], kk[i], dd[i], ss[i], pp[i], bt.n, true);
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, Ho); SAME_SHAPE(bt, Wo);
   }
+  tail_begin(bt.tail);
+  for (int i = 0; i < bt.n; ++i) tail_add(bt.tail, bt.e[i].stats, 2 * bt.e[i].C, 2 * bt.e[i].C);
+  tail_close(bt.tail);
   if (launch_dwpw_multi(bt, cur_stream())) return;
   for (int i = 0; i < bt.n; ++i) {  // fallback: one launch per entry (the plane path's band count is per batch)
     DwPwFwdBatch one{};
     one.n = 1;
+    one.tail = bt.tail;  // sequential launches may share the counter (each re-arms it)
     fill_dwpw(calls[i], one.e[0], kk[i], dd[i], ss[i], pp[i], 1, true);
     launch_dwpw_fwd(one, kk[i], dd[i], ss[i], pre[i], cur_stream());
   }
@@ -213,6 +286,9 @@ void pw_fwd(std::vector<py::tuple> calls, int64_t S) {
     a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off; a.relu = 1;
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, Cin); SAME_SHAPE(bt, Cout); SAME_SHAPE(bt, Ho); SAME_SHAPE(bt, Wo);
   }
+  tail_begin(bt.tail);
+  for (int i = 0; i < bt.n; ++i) tail_add(bt.tail, bt.e[i].stats, 2 * bt.e[i].CoutTotal, 2 * bt.e[i].CoutTotal);
+  tail_close(bt.tail);
   launch_pw_fwd(bt, cur_stream());
 }
 
@@ -243,6 +319,12 @@ static void pool_fwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, C);
     if (S_all > 0) { SAME_SHAPE(bt, H); SAME_SHAPE(bt, W); }
   }
+  tail_begin(bt.tail);
+  for (int i = 0; i < bt.n; ++i) {
+    tail_add(bt.tail, bt.e[i].stats_avg, 2 * bt.e[i].C, 2 * bt.e[i].C);
+    tail_add(bt.tail, bt.e[i].stats_max, 2 * bt.e[i].C, 2 * bt.e[i].C);
+  }
+  tail_close(bt.tail);
   if (S_all > 0) launch_pool_fwd(bt, S_all, cur_stream());
   else launch_pool_fwd_multi(bt, cur_stream());
 }
@@ -337,6 +419,12 @@ void combine_bwd_reduce(std::vector<py::tuple> calls) {
     }
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, HW);
   }
+  tail_begin(bt.tail);
+  for (int i = 0; i < bt.n; ++i) {
+    tail_add(bt.tail, bt.e[i].red, bt.e[i].rstride, bt.e[i].rstride);
+    tail_add(bt.tail, bt.e[i].gw, bt.e[i].gwstride, bt.e[i].gwstride);
+  }
+  tail_close(bt.tail);
   launch_combine_bwd_reduce(bt, cur_stream());
 }
 
@@ -393,13 +481,58 @@ void pw_bwd(std::vector<py::tuple> calls, int64_t S, int64_t mode, bool need_dx)
 }
 
 // (x, inbn|None, dw, dd, gout, gW|None, red|None, gstride, overwrite)
+void dw_bwd_fill(std::vector<py::tuple>& calls, DwBwdBatch& bt, const int64_t* Ks, int64_t dil, int64_t S,
+                 bool& prebn);
+
 void dw_bwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, int64_t pad) {
   check_batch<DwBwdBatch>(calls);
   DwBwdBatch bt{};
+  int64_t Ks[DwBwdBatch::kCap];
+  for (int i = 0; i < DwBwdBatch::kCap; ++i) Ks[i] = K;
+  TORCH_CHECK(pad == (K - 1) / 2 * dil, "dw_bwd padding must be 'same'");
+  bool prebn = false;
+  dw_bwd_fill(calls, bt, Ks, dil, S, prebn);
+  tail_close(bt.tail);
+  launch_dw_bwd(bt, K, dil, S, prebn, cur_stream());
+}
+
+// separable second stages of one node, mixed 3x3 / 5x5 (stride 1, input BN, distinct outputs):
+// entries (x, inbn, dw, dd, gout, gW|None, red|None, gstride, overwrite, K); one launch when the
+// plane kernel fits, else one launch per kernel size
+void dw_bwd_multi(std::vector<py::tuple> calls) {
+  check_batch<DwBwdBatch>(calls);
+  DwBwdBatch bt{};
+  int64_t Ks[DwBwdBatch::kCap];
+  for (size_t i = 0; i < calls.size(); ++i) {
+    TORCH_CHECK(calls[i].size() == 10, "dw_bwd_multi entry: (x, inbn, dw, dd, gout, gW, red, gstride, overwrite, K)");
+    Ks[i] = calls[i][9].cast<int64_t>();
+    TORCH_CHECK(Ks[i] == 3 || Ks[i] == 5, "K in {3, 5}");
+  }
+  bool prebn = false;
+  dw_bwd_fill(calls, bt, Ks, 1, 1, prebn);
+  TORCH_CHECK(prebn, "dw_bwd_multi is the separable second stage (input BN)");
+  for (int i = 0; i < bt.n; ++i) {
+    bt.e[i].variant = (int)Ks[i];
+    bt.e[i].pad = (int)Ks[i] / 2;
+  }
+  tail_close(bt.tail);
+  if (launch_dw_bwd_stage2_multi(bt, cur_stream())) return;
+  for (int64_t K : {3, 5}) {  // fallback: per kernel size, sharing the counter (sequential launches)
+    DwBwdBatch one{};
+    one.tail = bt.tail;
+    for (int i = 0; i < bt.n; ++i)
+      if (Ks[i] == K) one.e[one.n++] = bt.e[i];
+    if (one.n) launch_dw_bwd(one, K, 1, 1, true, cur_stream());
+  }
+}
+
+void dw_bwd_fill(std::vector<py::tuple>& calls, DwBwdBatch& bt, const int64_t* Ks, int64_t dil, int64_t S,
+                 bool& prebn) {
   bt.n = calls.size();
-  bool prebn = false, has_gw = false;
+  bool has_gw = false;
   for (int i = 0; i < bt.n; ++i) {
     const py::tuple& t = calls[i];
+    const int64_t K = Ks[i], pad = (K - 1) / 2 * dil;
     Tensor x = t[0].cast<Tensor>();
     auto inbn = t[1].cast<c10::optional<py::tuple>>();
     Tensor dw = t[2].cast<Tensor>(), dd = t[3].cast<Tensor>(), gout = t[4].cast<Tensor>();
@@ -433,7 +566,9 @@ void dw_bwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, int
     if (prebn) a.inbn = make_bn(*inbn, a.C);
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
   }
-  launch_dw_bwd(bt, K, dil, S, prebn, cur_stream());
+  tail_begin(bt.tail);
+  if (prebn)
+    for (int i = 0; i < bt.n; ++i) tail_add(bt.tail, bt.e[i].red, 2 * bt.e[i].C, 2 * bt.e[i].C);
 }
 
 // (ga|None, gm|None, x, dout_id|None, w|None, id_idx, gx, amax|None, overwrite[, S]); S < 0: per entry
@@ -479,6 +614,70 @@ static void pool_bwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
 }
 
 void pool_bwd(std::vector<py::tuple> calls, int64_t S) { pool_bwd_impl(calls, S); }
+
+// Whole input gradient of up to 4 edges of one node (distinct gx buffers), one launch:
+// per edge (x, gx, overwrite, convs, ga|None, gm|None, amax|None, dout_id|None, w|None, id_idx, S);
+// convs = 4 slots (sep 3x3, sep 5x5, dil 3x3, dil 5x5), each None or (dw, dd, gW|None, gstride).
+// Returns false (nothing launched) when the shapes fall outside the fused kernel.
+bool edge_bwd(std::vector<py::tuple> calls) {
+  check_batch<EdgeBwdBatch>(calls);
+  EdgeBwdBatch bt{};
+  bt.n = calls.size();
+  const int Ks[4] = {3, 5, 3, 5};
+  for (int i = 0; i < bt.n; ++i) {
+    const py::tuple& t = calls[i];
+    TORCH_CHECK(t.size() == 11, "edge_bwd entry: (x, gx, overwrite, convs, ga, gm, amax, dout_id, w, id_idx, S)");
+    Tensor x = t[0].cast<Tensor>(), gx = t[1].cast<Tensor>();
+    check_f32(x, "x"); check_f32(gx, "gx");
+    TORCH_CHECK(x.dim() == 4 && gx.sizes() == x.sizes(), "gx shape");
+    EdgeBwdArgs& a = bt.e[i];
+    a.x = x.data_ptr<float>(); a.gx = gx.data_ptr<float>(); a.overwrite = t[2].cast<bool>();
+    a.S = t[10].cast<int>();
+    TORCH_CHECK(a.S == 1 || a.S == 2, "stride");
+    a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3);
+    a.Ho = (a.H - 1) / a.S + 1; a.Wo = (a.W - 1) / a.S + 1;
+    auto convs = t[3].cast<std::vector<py::object>>();
+    TORCH_CHECK(convs.size() == 4, "4 conv slots");
+    for (int v = 0; v < 4; ++v) {
+      if (convs[v].is_none()) continue;
+      py::tuple c = convs[v].cast<py::tuple>();
+      Tensor dw = c[0].cast<Tensor>(), dd = c[1].cast<Tensor>();
+      OptT gW = c[2].cast<OptT>();
+      const int64_t gstride = c[3].cast<int64_t>();
+      check_f32(dw, "dw"); check_f32(dd, "dd");
+      TORCH_CHECK(dw.numel() == a.C * Ks[v] * Ks[v], "dw shape");
+      TORCH_CHECK(dd.dim() == 4 && dd.size(0) == a.N && dd.size(1) == a.C && dd.size(2) == a.Ho && dd.size(3) == a.Wo,
+                  "dd shape");
+      check_grad_sink(gW, (int64_t)a.C * Ks[v] * Ks[v], gstride);
+      a.dw[v] = dw.data_ptr<float>(); a.dd[v] = dd.data_ptr<float>(); a.gW[v] = ptr_or_null<float>(gW);
+      a.gstride[v] = gstride;
+      a.conv_mask |= 1 << v;
+    }
+    auto ga = t[4].cast<c10::optional<py::tuple>>(), gm = t[5].cast<c10::optional<py::tuple>>();
+    OptT amax = t[6].cast<OptT>(), dout_id = t[7].cast<OptT>(), w = t[8].cast<OptT>();
+    if (ga.has_value()) {
+      a.ga = make_gs(*ga, a.C);
+      TORCH_CHECK(gs_numel(*ga) == (int64_t)a.N * a.C * a.Ho * a.Wo, "avg-pool gradient source shape");
+    }
+    if (gm.has_value()) {
+      a.gm = make_gs(*gm, a.C);
+      TORCH_CHECK(gs_numel(*gm) == (int64_t)a.N * a.C * a.Ho * a.Wo, "max-pool gradient source shape");
+      TORCH_CHECK(amax.has_value() && amax->defined() && amax->scalar_type() == at::kByte &&
+                      amax->numel() == (int64_t)a.N * a.C * a.Ho * a.Wo,
+                  "max-pool backward needs the uint8 argmax from pool_fwd");
+      a.amax = amax->data_ptr<uint8_t>();
+    }
+    a.dout_id = ptr_or_null<float>(dout_id); a.w = ptr_or_null<float>(w); a.id_idx = t[9].cast<int>();
+    if (a.dout_id) {
+      check_f32(*dout_id, "dout_id");
+      TORCH_CHECK(dout_id->sizes() == x.sizes() && a.S == 1, "identity gradient shape");
+    }
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C);
+  }
+  for (int i = 0; i < bt.n; ++i)
+    for (int j = i + 1; j < bt.n; ++j) TORCH_CHECK(bt.e[i].gx != bt.e[j].gx, "edge_bwd entries share a gx buffer");
+  return launch_edge_bwd(bt, cur_stream());
+}
 void pool_bwd_multi(std::vector<py::tuple> calls) { pool_bwd_impl(calls, -1); }
 
 void fold_rows(Tensor buf) {
@@ -531,13 +730,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("combine_bwd_reduce", &combine_bwd_reduce);
   m.def("pw_bwd", &pw_bwd);
   m.def("dw_bwd", &dw_bwd);
+  m.def("dw_bwd_multi", &dw_bwd_multi, "separable second-stage depthwise backward of mixed kernel size in one launch");
   m.def("pool_bwd", &pool_bwd);
   m.def("dwpw_fwd_multi", &dwpw_fwd_multi, "mixed (K, dil, S) dw-pw entries of one node stage in one launch");
   m.def("pool_fwd_multi", &pool_fwd_multi, "stride-1 and stride-2 pools in one launch");
   m.def("pool_bwd_multi", &pool_bwd_multi, "stride-1 and stride-2 pool backward in one launch");
+  m.def("edge_bwd", &edge_bwd, "whole input gradient of a node's edges (convs, pools, identity) in one launch");
   m.def("set_max_blocks", &set_max_blocks);
   m.def("fold_rows", &fold_rows);
   m.def("fold_f64", &fold_f64);
+  m.def("set_fold_counters", &set_fold_counters, "register the current device's self-fold counter ring (int32, zeroed)");
+  m.def("selffold_ready", &selffold_ready, "launches on the current device fold their own f64 replicas");
+  m.def("set_selffold", &set_selffold, "turn self-folding launches on / off (default: KATIB_HIP_SELFFOLD)");
   m.attr("REP") = kRep;
   m.def("max_blocks", &max_blocks);
   register_xgmi(m);

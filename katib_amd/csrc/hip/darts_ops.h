@@ -87,6 +87,7 @@ struct DwBwdArgs {
   int gstride;  // floats between gW replicas (0: single accumulator); red: kRep replicas of [2C]
   int N, C, H, W, Ho, Wo, pad, chunk;
   int overwrite;  // non-PREBN: gout = masked grad (first writer of this input gradient) instead of +=
+  int variant, nbands, nblk;  // dw_bwd_stage2_multi_kernel: kernel size, row bands, workgroups of this entry
 };
 
 struct FoldArgs {  // buf[0][i] = sum_r buf[r][i]; rows 1.. zeroed
@@ -106,12 +107,32 @@ struct PoolBwdArgs {
   int S;          // pool_bwd_multi_kernel: per-entry stride
 };
 
+// Self-folding launches: a producer of replicated f64 reductions (BN statistics, BN-backward
+// sums, d alpha) folds them itself instead of leaving it to a fold_f64 launch. Every workgroup,
+// once its replica atomics have completed (s_waitcnt vmcnt(0): device-scope atomics are
+// performed memory-side, so no L2 write-back fence is involved), adds 1 to an arrival counter;
+// the workgroup that arrives last sums replicas 1.. into replica 0 with returning exchanges
+// (replica r <- 0) and one atomic add, then re-arms the counter. Consumers in later launches read
+// replica 0 only. Folding a segment twice is harmless (the second pass adds zeros).
+constexpr int kTailSeg = 16;
+constexpr int kFoldShards = 32;     // arrival counter shards per launch
+constexpr int kFoldCtrStride = 32;  // uints between counters (one 128-byte line each)
+constexpr int kFoldCtrSlot = (1 + kFoldShards) * kFoldCtrStride;  // uints per launch: top + shards
+struct FoldTail {
+  unsigned* ctr;   // kFoldCtrSlot uints: top counter, then the shard counters; zero between launches; nullptr: off
+  int nseg;
+  double* p[kTailSeg];
+  int n[kTailSeg];
+  int rs[kTailSeg];  // doubles between replicas
+};
+
 // Edge batches: one launch runs the same kernel for up to M edges of a DARTS node that share
 // shapes (blockIdx.y = edge). Passed by value in the kernarg segment (kept <= 4 KB).
 template <typename A, int M>
 struct Batch {
   A e[M];
   int n;
+  FoldTail tail;
   static constexpr int kCap = M;
 };
 using DwPwFwdBatch = Batch<DwPwFwdArgs, 8>;
@@ -123,6 +144,21 @@ using PwBwdBatch = Batch<PwBwdArgs, 8>;
 using DwBwdBatch = Batch<DwBwdArgs, 8>;
 using PoolBwdBatch = Batch<PoolBwdArgs, 8>;
 using DwPwMultiBatch = Batch<DwPwFwdArgs, 16>;  // a node's stage-1 (or stage-2) dw-pw entries, mixed K/dil/S
+
+// Whole input gradient of one DARTS edge (except the stride-2 skip's FactorizedReduce, which
+// accumulates afterwards): the transposed depthwise convolutions of the separable stage-1 and the
+// dilated convolutions (masked by relu'(x)), max / avg pool backward and the identity skip, formed
+// in LDS and written once (edge_bwd_kernel).
+struct EdgeBwdArgs {
+  const float* x; float* gx; int overwrite;
+  // conv slots: 0 sep 3x3, 1 sep 5x5 (dilation 1), 2 dil 3x3, 3 dil 5x5 (dilation 2)
+  const float* dw[4]; const float* dd[4]; float* gW[4]; int gstride[4]; int conv_mask;
+  GradSrc ga; GradSrc gm; const unsigned char* amax;  // ga.z / gm.z null: that pool is absent
+  const float* dout_id; const float* w; int id_idx;   // identity skip (stride 1)
+  int N, C, H, W, Ho, Wo, S, nb, nblk;
+};
+using EdgeBwdBatch = Batch<EdgeBwdArgs, 4>;
+static_assert(sizeof(EdgeBwdBatch) <= 4096, "edge_bwd batch must fit the 4 KB kernarg segment");
 static_assert(sizeof(DwPwMultiBatch) <= 4096 && sizeof(PoolBwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096,
               "kernel argument blocks must fit the 4 KB kernarg segment");
 static_assert(sizeof(DwPwFwdBatch) <= 4096 && sizeof(CombineFwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096 && sizeof(PoolFwdBatch) <= 4096 &&
@@ -132,6 +168,8 @@ static_assert(sizeof(DwPwFwdBatch) <= 4096 && sizeof(CombineFwdBatch) <= 4096 &&
 
 void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st);
 void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st);
+// separable second stages of mixed kernel size (stride 1, input BN); false: not launched
+bool launch_dw_bwd_stage2_multi(DwBwdBatch b, hipStream_t st);
 void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st);
 void launch_pool_fwd(const PoolFwdBatch& b, int S, hipStream_t st);
 void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st);
@@ -140,6 +178,8 @@ bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st);
 void launch_pool_fwd_multi(PoolFwdBatch b, hipStream_t st);
 void launch_pool_bwd_multi(const PoolBwdBatch& b, hipStream_t st);
 void launch_combine_fwd(const CombineFwdBatch& b, hipStream_t st);
+// false (nothing launched): shapes / alignment outside the fused kernel's plane layout
+bool launch_edge_bwd(EdgeBwdBatch b, hipStream_t st);
 void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st);
 void launch_pw_bwd(const PwBwdBatch& b, hipStream_t st);
 int max_blocks();

@@ -161,6 +161,53 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// Self-fold epilogue (darts_ops.h FoldTail). Called by EVERY thread of EVERY workgroup of the
+// launch, after the workgroup's last replica atomic. The arrival add is relaxed: the payload is
+// device-scope atomics (performed memory-side), drained by each wave's vmcnt(0) before the
+// workgroup barrier, and the folding workgroup reads it back with returning atomics only, so no
+// release / acquire fence (an XCD L2 write-back per workgroup) is needed.
+__device__ __forceinline__ void fold_tail(const FoldTail& t) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // two-level arrival: same-address atomics serialise memory-side (~12 ns each), so ~2000
+    // workgroups on one counter cost ~25 us; kFoldShards shard counters (own 128-B lines) cut
+    // the chain to total / kFoldShards, and each shard's last arriver adds to the top counter
+    const unsigned total = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const unsigned sh = L % kFoldShards;
+    const unsigned cnt = total / kFoldShards + (sh < total % kFoldShards ? 1u : 0u);
+    unsigned* cs = t.ctr + (1 + sh) * kFoldCtrStride;
+    int last = 0;
+    if (__hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == cnt - 1) {
+      __hip_atomic_store(cs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm the shard
+      const unsigned nsh = total < (unsigned)kFoldShards ? total : (unsigned)kFoldShards;
+      last = __hip_atomic_fetch_add(t.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  int tot = 0;
+  for (int s = 0; s < t.nseg; ++s) tot += t.n[s];
+  for (int g = threadIdx.x; g < tot; g += blockDim.x) {
+    int s = 0, i = g;
+    while (i >= t.n[s]) i -= t.n[s++];
+    double* p = t.p[s] + i;
+    const size_t rs = t.rs[s];
+    double v[kRep - 1];
+#pragma unroll
+    for (int r = 1; r < kRep; ++r)  // all exchanges in flight together
+      v[r - 1] = __hip_atomic_exchange(p + r * rs, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < kRep - 1; ++r) acc += v[r];
+    __hip_atomic_fetch_add(p, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(t.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------------------------------------
 // dwpw_fwd: z = pw . dw(act(in)), d = dw(act(in)); act = relu(x) or relu(BN(x))
 // grid: N * (Ho / TR) blocks, 256 threads. P = TR * Wo == 64 (host-enforced)
@@ -283,6 +330,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
   }
   if (a.stats)  // one contiguous f64 atomic vector per block
     for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.stats + rep_slot() * 2 * C + i, (double)sStat[i]);
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -414,6 +462,7 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
 template <int K, int DIL, int S, bool PREBN, int C, bool VEC, bool PW = true>
 __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {
   dwpw_plane_body<K, DIL, S, PREBN, C, VEC, PW>(bt.e[blockIdx.y], blockIdx.x);
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
 // One launch for a node's whole separable-stage / dilated-conv forward: every entry (edge x
@@ -432,12 +481,14 @@ __global__ void __launch_bounds__(256) dwpw_plane_multi_kernel(DwPwMultiBatch bt
   // batch to scratch once 32 variant bodies use it (ScratchSize 2320 B/lane, 20x slower)
   const DwPwFwdArgs a = bt.e[blockIdx.y];
   const int bx = blockIdx.x;
-  if (bx >= a.nblk) return;  // entries differ in their band counts (uniform per workgroup)
-  switch (a.variant) {
-    DWPW_CASE(3, 1, 1) DWPW_CASE(3, 1, 2) DWPW_CASE(5, 1, 1) DWPW_CASE(5, 1, 2)
-    DWPW_CASE(3, 2, 1) DWPW_CASE(3, 2, 2) DWPW_CASE(5, 2, 1) DWPW_CASE(5, 2, 2)
-    default: break;
+  if (bx < a.nblk) {  // entries differ in their band counts (uniform per workgroup)
+    switch (a.variant) {
+      DWPW_CASE(3, 1, 1) DWPW_CASE(3, 1, 2) DWPW_CASE(5, 1, 1) DWPW_CASE(5, 1, 2)
+      DWPW_CASE(3, 2, 1) DWPW_CASE(3, 2, 2) DWPW_CASE(5, 2, 1) DWPW_CASE(5, 2, 2)
+      default: break;
+    }
   }
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 #undef DWPW_CASE
 
@@ -534,7 +585,7 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
         s2[bo][r] += (z.x * z.x + z.y * z.y) + (z.z * z.z + z.w * z.w);
       }
   }
-  if (!a.stats) return;
+  if (a.stats) {
 #pragma unroll
   for (int bo = 0; bo < BO; ++bo)
 #pragma unroll
@@ -555,6 +606,8 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
     const int hi = i >= CO;
     atomicAdd(a.stats + rep_slot() * 2 * a.CoutTotal + hi * a.CoutTotal + a.co_off + (i - hi * CO), (double)sStat[i]);
   }
+  }
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -605,6 +658,7 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdBatch bt) {
       atomicAdd(a.stats + rep_slot() * 2 * a.CoutTotal + hi * a.CoutTotal + a.co_off + (i - hi * Cout),
                 (double)sStat[i]);
     }
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -665,14 +719,17 @@ __device__ __forceinline__ void pool_fwd_body(const PoolFwdArgs& a, const int bx
 template <int S>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(PoolFwdBatch bt) {
   pool_fwd_body<S>(bt.e[blockIdx.y], blockIdx.x, gridDim.x);
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
 // stride-1 and stride-2 pooling of a node in one launch (entry a.S; a.nblk workgroups, a multiple of C)
 __global__ void __launch_bounds__(256) pool_fwd_multi_kernel(PoolFwdBatch bt) {
   const PoolFwdArgs a = bt.e[blockIdx.y];  // copy: see dwpw_plane_multi_kernel
-  if ((int)blockIdx.x >= a.nblk) return;
-  if (a.S == 1) pool_fwd_body<1>(a, blockIdx.x, a.nblk);
-  else pool_fwd_body<2>(a, blockIdx.x, a.nblk);
+  if ((int)blockIdx.x < a.nblk) {
+    if (a.S == 1) pool_fwd_body<1>(a, blockIdx.x, a.nblk);
+    else pool_fwd_body<2>(a, blockIdx.x, a.nblk);
+  }
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
 
@@ -865,6 +922,7 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdBatch
       if (gw) atomicAdd(gw + a.widx[j - 2], (double)t);
     }
   }
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
 // on-the-fly BN backward: dz = wk * invstd * (g - S1/cnt - zhat * S2/cnt)
@@ -1525,6 +1583,7 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
     for (int i = tid; i < 2 * C; i += 256) atomicAdd(a.red + rep_slot() * 2 * C + i, (double)sRed[i]);
   if (a.gW)
     for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + (size_t)rep_slot() * a.gstride + i, sGW[i]);
+  if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1618,13 +1677,12 @@ __global__ void __launch_bounds__(256) pool_bwd_multi_kernel(PoolBwdBatch bt) {
 // Replaces the 64-pixel tiles whose halo rows were re-staged per tile behind two barriers.
 // ------------------------------------------------------------------------------------------------
 template <int K, int DIL, int S, bool PREBN, int C>
-__global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb, int dbg) {
-  const DwBwdArgs& a = bt.e[blockIdx.y];
+__device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int bx, const int nb, const int dbg) {
   constexpr int KK = K * K, PAD = (K - 1) / 2 * DIL, PO = (PAD + S - 1) / S, SH = S == 2 ? 1 : 0;
   const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   // channel groups: depthwise backward never mixes channels, so wider layers run as a.C / C
   // independent C-channel groups (blockIdx.x = (image * nb + band) * G + group)
-  const int G = a.C / C, grp = blockIdx.x % G, nbx = blockIdx.x / G, c0 = grp * C;
+  const int G = a.C / C, grp = bx % G, nbx = bx / G, c0 = grp * C;
   const int n = nbx / nb, band = nbx - n * nb;
   const int BRi = H / nb, iy0 = band * BRi, nrow = BRi;
   const int oyA = (iy0 - PAD) >> SH;                 // floor division (S in {1, 2})
@@ -1807,6 +1865,314 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
     for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + (size_t)rep_slot() * a.gstride + c0 * KK + i, sGW[i]);
 }
 
+template <int K, int DIL, int S, bool PREBN, int C>
+__global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb, int dbg) {
+  dw_bwd_plane_body<K, DIL, S, PREBN, C>(bt.e[blockIdx.y], blockIdx.x, nb, dbg);
+  if (bt.tail.ctr) fold_tail(bt.tail);
+}
+
+// a node's separable second stages (3x3 and 5x5, stride 1, input BN) in one launch: each entry
+// carries its kernel size and band count (a.variant = K, a.nbands, a.nblk); distinct outputs
+template <int C>
+__global__ void __launch_bounds__(256) dw_bwd_stage2_multi_kernel(DwBwdBatch bt) {
+  const DwBwdArgs a = bt.e[blockIdx.y];  // copy: see dwpw_plane_multi_kernel
+  if ((int)blockIdx.x < a.nblk) {
+    if (a.variant == 3) dw_bwd_plane_body<3, 1, 1, true, C>(a, blockIdx.x, a.nbands, 0);
+    else dw_bwd_plane_body<5, 1, 1, true, C>(a, blockIdx.x, a.nbands, 0);
+  }
+  if (bt.tail.ctr) fold_tail(bt.tail);
+}
+
+// ------------------------------------------------------------------------------------------------
+// edge_bwd: the whole input gradient of one edge in one pass (cf. dw_bwd_plane_kernel, whose band
+// layout it shares). Workgroup = (image, band of input rows, C-channel group); act = relu(x) of
+// the band is staged once and the gradient is accumulated in LDS:
+//   conv slots (sep 3x3 / 5x5 stage 1, dil 3x3 / 5x5): dd of the slot staged with its halo, the
+//     transposed depthwise gather added to sGX, the slot's depthwise weight gradient reduced in
+//     LDS and flushed with one atomic per weight (replica rep_slot());
+//   pools: dz_avg / window count and dz_max (BN backward on the fly from the combine reductions)
+//     of the output rows the band reaches, plus the argmax taps, staged and gathered;
+//   identity: w_id * dout.
+// gx = relu'(x) * conv + pool + identity, written (or added) once per element. Replaces the
+// per-(K, S) dw_bwd launches, the pool backward and the identity add of a node: 4-10 launches
+// that each re-read and re-wrote gx.
+// ------------------------------------------------------------------------------------------------
+template <int K, int DIL, int S, int C>
+__device__ __forceinline__ void edge_conv_part(const EdgeBwdArgs& a, const int v, const int n, const int c0,
+                                               const int iy0, const int nrow, float* sDD, const float* sAct,
+                                               float* sGX, float* sGW) {
+  constexpr int KK = K * K, PAD = (K - 1) / 2 * DIL, PO = (PAD + S - 1) / S, SH = S == 2 ? 1 : 0;
+  const int W = a.W, Ho = a.Ho, Wo = a.Wo, NP = nrow * W;
+  const int oyA = (iy0 - PAD) >> SH, oyB = (iy0 + nrow - 1 + PAD) >> SH;
+  const int ODR = oyB - oyA + 1, ODW = Wo + 2 * PO;
+  const int tid = threadIdx.x;
+  const float* ddn = a.dd[v] + ((size_t)n * a.C + c0) * Ho * Wo;
+  const int va = max(oyA, 0), vb = min(oyB, Ho - 1), vrows = vb - va + 1;
+  {
+    const int q4 = vrows * Wo / 4;
+#pragma unroll 4
+    for (int i = tid; i < C * q4; i += 256) {
+      const int c = i / q4, o = (i - c * q4) * 4, r = o / Wo, ox = o - r * Wo;
+      const float4 f = *reinterpret_cast<const float4*>(ddn + ((size_t)c * Ho + va) * Wo + o);
+      float* d = sDD + (c * ODR + va - oyA + r) * ODW + PO + ox;
+      d[0] = f.x;
+      d[1] = f.y;
+      d[2] = f.z;
+      d[3] = f.w;
+    }
+    for (int i = tid; i < C * ODR; i += 256) {
+      const int c = i / ODR, oy = oyA + i - c * ODR;
+      float* d = sDD + i * ODW;
+      if (oy < 0 || oy >= Ho) {
+        for (int q = 0; q < ODW; ++q) d[q] = 0.f;
+      } else {
+        for (int q = 0; q < PO; ++q) d[q] = d[PO + Wo + q] = 0.f;
+      }
+    }
+    for (int i = tid; i < C * KK; i += 256) sGW[i] = 0.f;
+  }
+  __syncthreads();
+  for (int p = tid; p < NP; p += 256) {
+    const int r = p / W, ix = p - r * W, iy = iy0 + r;
+    int srow[K], scol[K];
+    float mrow[K], mcol[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int t = iy + PAD - k * DIL, u = ix + PAD - k * DIL;
+      srow[k] = ((t >> SH) - oyA) * ODW;
+      scol[k] = (u >> SH) + PO;
+      mrow[k] = (S == 1 || (t & 1) == 0) ? 1.f : 0.f;
+      mcol[k] = (S == 1 || (u & 1) == 0) ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float* wk = a.dw[v] + (c0 + c) * KK;  // uniform -> scalar loads
+      const float* dd = sDD + c * ODR * ODW;
+      float ga = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky) {
+        float rowacc = 0.f;
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const float t = wk[ky * K + kx] * dd[srow[ky] + scol[kx]];
+          rowacc += S == 1 ? t : mcol[kx] * t;
+        }
+        ga += S == 1 ? rowacc : mrow[ky] * rowacc;
+      }
+      sGX[c * NP + p] += ga;  // own pixel: no other thread touches it
+    }
+  }
+  if (a.gW[v]) {
+    if (S == 1) {
+      // job = (channel, ky, own row): 4-pixel input quads against the dd row segment they meet
+      const int JB = C * K * nrow;
+      for (int j = tid; j < JB; j += 256) {
+        const int c = j / (K * nrow), rem = j - c * K * nrow, ky = rem / nrow, r = rem - ky * nrow;
+        const float* ddr = sDD + (c * ODR + iy0 + r + PAD - ky * DIL - oyA) * ODW + PO;
+        const float* inr = sAct + c * NP + r * W;
+        float acc[K];
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) acc[kx] = 0.f;
+        for (int ix = 0; ix < W; ix += 4) {
+          const float4 f = *reinterpret_cast<const float4*>(inr + ix);
+          float dseg[4 + 2 * PAD];
+#pragma unroll
+          for (int m = 0; m < 4 + 2 * PAD; ++m) dseg[m] = ddr[ix - PAD + m];
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx) {
+            const int o = 2 * PAD - kx * DIL;
+            acc[kx] += f.x * dseg[o] + f.y * dseg[o + 1] + f.z * dseg[o + 2] + f.w * dseg[o + 3];
+          }
+        }
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) atomicAdd(sGW + c * KK + ky * K + kx, acc[kx]);
+      }
+    } else {
+      constexpr int JOBS = C * KK, T = JOBS >= 256 ? 1 : 256 / JOBS;
+      for (int j = tid; j < JOBS * T; j += 256) {
+        const int job = j / T, part = j - job * T;
+        const int c = job / KK, tap = job - c * KK, ky = tap / K, kx = tap - ky * K;
+        const float* dd = sDD + c * ODR * ODW;
+        const float* in = sAct + c * NP;
+        float acc = 0.f;
+        for (int r = 0; r < nrow; ++r) {
+          const int t = iy0 + r + PAD - ky * DIL;
+          if (t & 1) continue;
+          const float* ddr = dd + ((t >> SH) - oyA) * ODW + PO;
+          const float* inr = in + r * W;
+          for (int ix = part * S + ((PAD - kx * DIL) & 1); ix < W; ix += T * S)
+            acc += inr[ix] * ddr[(ix + PAD - kx * DIL) >> SH];
+        }
+        atomicAdd(sGW + job, acc);
+      }
+    }
+  }
+  __syncthreads();
+  if (a.gW[v])
+    for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW[v] + (size_t)rep_slot() * a.gstride[v] + c0 * KK + i, sGW[i]);
+  __syncthreads();  // sDD / sGW are restaged by the next slot
+}
+
+template <int S, int C>
+__device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& a, const int bx) {
+  const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int G = a.C / C, grp = bx % G, nbx = bx / G, c0 = grp * C;
+  const int n = nbx / a.nb, band = nbx - n * a.nb;
+  const int nrow = H / a.nb, iy0 = band * nrow, NP = nrow * W;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sAct = smem;           // [C][NP] relu(x)
+  float* sGX = sAct + C * NP;   // [C][NP] conv gradient (pre-mask)
+  float* sDD = sGX + C * NP;    // staging: one conv slot's dd band, or the pool gradients
+  __shared__ float sGW[C * 25];
+  __shared__ float sCo[C][10];
+  const int tid = threadIdx.x;
+  const float* xn = a.x + ((size_t)n * a.C + c0) * H * W;
+  {
+    const int q4 = NP / 4;
+#pragma unroll 4
+    for (int i = tid; i < C * q4; i += 256) {
+      const int c = i / q4, o = (i - c * q4) * 4;
+      float4 f = *reinterpret_cast<const float4*>(xn + ((size_t)c * H + iy0) * W + o);
+      f.x = fmaxf(f.x, 0.f);
+      f.y = fmaxf(f.y, 0.f);
+      f.z = fmaxf(f.z, 0.f);
+      f.w = fmaxf(f.w, 0.f);
+      *reinterpret_cast<float4*>(sAct + c * NP + o) = f;
+      *reinterpret_cast<float4*>(sGX + c * NP + o) = float4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  const bool pa = a.ga.z != nullptr, pm = a.gm.z != nullptr;
+  if (tid < C) {  // pool BN coefficients and softmax weights per channel
+    float* co = sCo[tid];
+    co[0] = 0.f; co[1] = 1.f; co[2] = 0.f; co[3] = 0.f; co[4] = 0.f; co[5] = 1.f; co[6] = 0.f; co[7] = 0.f;
+    if (pa) {
+      bn_coeffs(a.ga.bn, c0 + tid, co[0], co[1]);
+      gs_means(a.ga, c0 + tid, co[2], co[3]);
+    }
+    if (pm) {
+      bn_coeffs(a.gm.bn, c0 + tid, co[4], co[5]);
+      gs_means(a.gm, c0 + tid, co[6], co[7]);
+    }
+    co[8] = pa && a.ga.w ? a.ga.w[a.ga.widx] : 1.f;
+    co[9] = pm && a.gm.w ? a.gm.w[a.gm.widx] : 1.f;
+  }
+  __syncthreads();
+  if (a.conv_mask & 1) edge_conv_part<3, 1, S, C>(a, 0, n, c0, iy0, nrow, sDD, sAct, sGX, sGW);
+  if (a.conv_mask & 2) edge_conv_part<5, 1, S, C>(a, 1, n, c0, iy0, nrow, sDD, sAct, sGX, sGW);
+  if (a.conv_mask & 4) edge_conv_part<3, 2, S, C>(a, 2, n, c0, iy0, nrow, sDD, sAct, sGX, sGW);
+  if (a.conv_mask & 8) edge_conv_part<5, 2, S, C>(a, 3, n, c0, iy0, nrow, sDD, sAct, sGX, sGW);
+  // pools: output rows whose 3x3 window (pad 1) touches the band's input rows
+  const int poA = max(0, (iy0 - 1 + S - 1) / S), poB = min(Ho - 1, (iy0 + nrow) / S);
+  const int PR = poB - poA + 1, PP = PR * Wo;
+  float* sGa = sDD;
+  float* sGm = sDD + C * PP;
+  unsigned char* sArg = reinterpret_cast<unsigned char*>(sDD + 2 * C * PP);
+  if (pa || pm) {
+    for (int i = tid; i < C * PP; i += 256) {
+      const int c = i / PP, o = poA * Wo + (i - c * PP), oy = o / Wo, ox = o - oy * Wo;
+      const size_t idx = ((size_t)n * a.C + c0 + c) * Ho * Wo + o;
+      const float* co = sCo[c];
+      float gav = 0.f, gmv = 0.f;
+      unsigned char arg = 255;
+      if (pa) {
+        const int y0 = max(oy * S - 1, 0), y1 = min(oy * S + 1, H - 1);
+        const int x0 = max(ox * S - 1, 0), x1 = min(ox * S + 1, W - 1);
+        gav = bn_bwd_val(a.ga, idx, co[0], co[1], co[8], co[2], co[3]) / (float)((y1 - y0 + 1) * (x1 - x0 + 1));
+      }
+      if (pm) {
+        gmv = bn_bwd_val(a.gm, idx, co[4], co[5], co[9], co[6], co[7]);
+        arg = a.amax[idx];
+      }
+      sGa[i] = gav;
+      sGm[i] = gmv;
+      sArg[i] = arg;
+    }
+    __syncthreads();
+  }
+  const float wid = (a.dout_id && a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+  for (int p = tid; p < NP; p += 256) {
+    const int r = p / W, ix = p - r * W, iy = iy0 + r;
+    const int oy_lo = iy - 1 < 0 ? 0 : (iy - 1 + S - 1) / S, oy_hi = min((iy + 1) / S, Ho - 1);
+    const int ox_lo = ix - 1 < 0 ? 0 : (ix - 1 + S - 1) / S, ox_hi = min((ix + 1) / S, Wo - 1);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float g = sAct[c * NP + p] > 0.f ? sGX[c * NP + p] : 0.f;
+      if (pa || pm) {
+        for (int oy = oy_lo; oy <= oy_hi; ++oy)
+          for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+            const int o = c * PP + (oy - poA) * Wo + ox;
+            g += sGa[o];
+            if (sArg[o] == (iy - oy * S + 1) * 3 + (ix - ox * S + 1)) g += sGm[o];
+          }
+      }
+      const size_t gi = ((size_t)n * a.C + c0 + c) * H * W + (size_t)iy * W + ix;
+      if (a.dout_id) g += wid * a.dout_id[gi];
+      a.gx[gi] = a.overwrite ? g : a.gx[gi] + g;
+    }
+  }
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) edge_bwd_kernel(EdgeBwdBatch bt) {
+  const EdgeBwdArgs a = bt.e[blockIdx.y];  // copy: see dwpw_plane_multi_kernel
+  if ((int)blockIdx.x >= a.nblk) return;
+  if (a.S == 1) edge_bwd_body<1, C>(a, blockIdx.x);
+  else edge_bwd_body<2, C>(a, blockIdx.x);
+}
+
+// LDS floats of one edge_bwd band: act + gradient planes, then the larger of the widest conv
+// slot's staged dd band and the pool staging
+static size_t edge_bwd_floats(const EdgeBwdArgs& a, int nb, int CG) {
+  const int nrow = a.H / nb, S = a.S, sh = S == 2 ? 1 : 0;
+  auto fdiv = [sh](int v) { return v >= 0 ? v >> sh : -((-v + (1 << sh) - 1) >> sh); };
+  size_t stage = 0;
+  const int pads[4] = {1, 2, 2, 4};
+  for (int v = 0; v < 4; ++v) {
+    if (!(a.conv_mask & (1 << v))) continue;
+    const int PAD = pads[v], PO = (PAD + S - 1) / S;
+    const int ODR = fdiv(nrow - 1 + PAD) - fdiv(-PAD) + 2;
+    stage = std::max(stage, (size_t)CG * ODR * (a.Wo + 2 * PO));
+  }
+  if (a.ga.z || a.gm.z) {
+    const size_t PP = (size_t)(nrow / S + 3) * a.Wo;
+    stage = std::max(stage, 2 * CG * PP + (CG * PP + 3) / 4);
+  }
+  return 2 * (size_t)CG * nrow * a.W + stage;
+}
+
+bool launch_edge_bwd(EdgeBwdBatch b, hipStream_t st) {
+  if (b.n < 1) return true;
+  const int C = b.e[0].C, N = b.e[0].N;
+  if (!(C == 4 || (C % 8 == 0 && C <= kMaxC))) return false;
+  const int CG = C == 4 ? 4 : 8, G = C / CG;
+  int maxblk = 0;
+  size_t lds = 0;
+  for (int i = 0; i < b.n; ++i) {
+    EdgeBwdArgs& a = b.e[i];
+    if (a.C != C || a.N != N || a.H != a.Ho * a.S || a.W != a.Wo * a.S || a.W % 4 || a.Wo % 4) return false;
+    uintptr_t bits = (uintptr_t)a.x;
+    for (int v = 0; v < 4; ++v)
+      if (a.conv_mask & (1 << v)) bits |= (uintptr_t)a.dd[v];
+    if (bits & 15) return false;
+    // bands: LDS per workgroup <= KATIB_HIP_EDGE_LDS_KB and >= KATIB_HIP_EDGE_WG workgroups per launch
+    static const int lds_kb = getenv("KATIB_HIP_EDGE_LDS_KB") ? atoi(getenv("KATIB_HIP_EDGE_LDS_KB")) : 48;
+    static const int min_wg = getenv("KATIB_HIP_EDGE_WG") ? atoi(getenv("KATIB_HIP_EDGE_WG")) : 1024;
+    int nb = 1;
+    while (nb < 32 && a.H % (2 * nb) == 0 &&
+           (edge_bwd_floats(a, nb, CG) * 4 > (size_t)lds_kb * 1024 || N * nb * G * b.n < min_wg))
+      nb *= 2;
+    if (edge_bwd_floats(a, nb, CG) * 4 > 64 * 1024) return false;
+    a.nb = nb;
+    a.nblk = N * nb * G;
+    maxblk = std::max(maxblk, a.nblk);
+    lds = std::max(lds, edge_bwd_floats(a, nb, CG) * sizeof(float));
+  }
+  const dim3 grid(maxblk, b.n);
+  if (CG == 4) hipLaunchKernelGGL(edge_bwd_kernel<4>, grid, dim3(256), lds, st, b);
+  else hipLaunchKernelGGL(edge_bwd_kernel<8>, grid, dim3(256), lds, st, b);
+  return true;
+}
+
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
@@ -1869,6 +2235,7 @@ static bool try_dwpw_split_g(const DwPwFwdBatch& b, bool prebn, hipStream_t st, 
   };
   while (band_bytes(nb) > 65536 && nb < a.Ho) ++nb;
   DwPwFwdBatch db = b;
+  db.tail.ctr = nullptr;  // the statistics come from the pointwise launch below, which folds them
   for (int i = 0; i < b.n; ++i) db.e[i].chunk = nb;
   dim3 grid(a.N * nb * G, b.n);
   const size_t lds = band_bytes(nb);
@@ -1876,6 +2243,7 @@ static bool try_dwpw_split_g(const DwPwFwdBatch& b, bool prebn, hipStream_t st, 
   else hipLaunchKernelGGL((dwpw_plane_kernel<K, DIL, S, false, CG, true, false>), grid, dim3(256), lds, st, db);
   PwFwdBatch pb{};
   pb.n = b.n;
+  pb.tail = b.tail;
   for (int i = 0; i < b.n; ++i) {
     const DwPwFwdArgs& e = b.e[i];
     PwFwdArgs& p = pb.e[i];
@@ -1959,10 +2327,15 @@ bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st) {
     else hipLaunchKernelGGL((dwpw_plane_multi_kernel<16, true>), grid, dim3(256), lds, st, b);
     return true;
   }
-  hipLaunchKernelGGL((dwpw_plane_multi_kernel<8, false>), grid, dim3(256), lds, st, b);
+  {
+    DwPwMultiBatch db = b;
+    db.tail.ctr = nullptr;  // statistics (and their fold) come from the pointwise launch
+    hipLaunchKernelGGL((dwpw_plane_multi_kernel<8, false>), grid, dim3(256), lds, st, db);
+  }
   // the pointwise halves + BN statistics of every entry: one MFMA wave launch
   PwFwdBatch pb{};
   pb.n = b.n;
+  pb.tail = b.tail;  // per-entry launches below share the counter: they run one after another
   for (int i = 0; i < b.n; ++i) {
     const DwPwFwdArgs& e = b.e[i];
     PwFwdArgs& p = pb.e[i];
@@ -1977,6 +2350,7 @@ bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st) {
   for (int i = 0; i < b.n; ++i) {  // mixed output sizes (stride-1 and stride-2 entries): per entry
     PwFwdBatch one{};
     one.n = 1;
+    one.tail = pb.tail;
     one.e[0] = pb.e[i];
     if (!(try_pw_fwd_wave<16, 16>(one, st) || try_pw_fwd_wave<32, 32>(one, st) || try_pw_fwd_wave<64, 64>(one, st)))
       launch_pw_fwd(one, st);
@@ -2065,6 +2439,34 @@ static void launch_dw_bwd_t(const DwBwdBatch& b, bool prebn, hipStream_t st) {
   dim3 grid(per_edge_blocks(a.N * (a.Ho / TR), b.n), b.n);
   if (prebn) hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, true>), grid, dim3(256), lds, st, b);
   else hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, b);
+}
+
+bool launch_dw_bwd_stage2_multi(DwBwdBatch b, hipStream_t st) {
+  if (b.n < 1) return true;
+  const DwBwdArgs& a0 = b.e[0];
+  if (!(a0.C == 4 || a0.C == 8 || (a0.C % 16 == 0 && a0.C <= kMaxC)) || !aligned16(b)) return false;
+  static const int grp = getenv("KATIB_HIP_DWB_GROUP") ? atoi(getenv("KATIB_HIP_DWB_GROUP")) : 8;
+  const int C = (a0.C == 4 || grp == 4) ? 4 : 8;  // wide layers: 8-channel groups (launch_dw_bwd_t)
+  if (a0.C % C) return false;
+  int maxblk = 0;
+  size_t lds = 0;
+  for (int i = 0; i < b.n; ++i) {
+    DwBwdArgs& a = b.e[i];
+    const int K = a.variant;
+    if ((K != 3 && K != 5) || a.C != a0.C || a.H != a.Ho || a.W != a.Wo || a.pad != K / 2 || a.Wo % 4) return false;
+    int nb = 1;
+    const int G = a.C / C;
+    while (nb < 8 && a.H % (2 * nb) == 0 &&
+           (dw_plane_floats(a, K, 1, 1, nb, false, C) * 4 > 40 * 1024 || a.N * nb * G * b.n < 1024))
+      nb *= 2;
+    a.nbands = nb;
+    a.nblk = a.N * nb * G;
+    maxblk = std::max(maxblk, a.nblk);
+    lds = std::max(lds, sizeof(float) * dw_plane_floats(a, K, 1, 1, nb, false, C));
+  }
+  if (C == 4) hipLaunchKernelGGL(dw_bwd_stage2_multi_kernel<4>, dim3(maxblk, b.n), dim3(256), lds, st, b);
+  else hipLaunchKernelGGL(dw_bwd_stage2_multi_kernel<8>, dim3(maxblk, b.n), dim3(256), lds, st, b);
+  return true;
 }
 
 void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st) {

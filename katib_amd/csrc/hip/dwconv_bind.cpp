@@ -5,6 +5,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include "dwconv.h"
+#include "pool_nhwc.h"
 
 namespace py = pybind11;
 using at::Tensor;
@@ -81,9 +82,55 @@ void dw_wgrad(const Tensor& x, const Tensor& gy, const Tensor& part, const std::
               "dw_wgrad launch failed");
 }
 
+// ---- NHWC bf16 pooling (pool_nhwc.hip): geometry (N, H, W, C, P, S)
+katib_hip::poolnhwc::Geom pool_geom(const std::vector<int64_t>& v) {
+  TORCH_CHECK(v.size() == 6, "pool geometry: N,H,W,C,P,S");
+  for (int64_t e : v) TORCH_CHECK(e > 0 && e < (1 << 30), "pool geometry value out of range");
+  katib_hip::poolnhwc::Geom g{(int)v[0], (int)v[1], (int)v[2], (int)v[3], (int)v[4], (int)v[5], 0, 0};
+  TORCH_CHECK(g.C % 8 == 0, "pool: C must be a multiple of 8");
+  TORCH_CHECK(g.P <= 16 && g.P <= g.H && g.P <= g.W, "pool window must fit the input (and be <= 16)");
+  g.OH = (g.H - g.P) / g.S + 1;
+  g.OW = (g.W - g.P) / g.S + 1;
+  TORCH_CHECK((int64_t)g.N * g.H * g.W * g.C < (1ll << 40), "tensor too large");
+  return g;
+}
+
+// x [N,H,W,C] bf16 -> y [N,OH,OW,C] bf16 (+ arg uint8, max pooling)
+void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& arg, bool is_max,
+              const std::vector<int64_t>& geom) {
+  const auto g = pool_geom(geom);
+  check(x, at::kBFloat16, (int64_t)g.N * g.H * g.W * g.C, "x");
+  check(y, at::kBFloat16, (int64_t)g.N * g.OH * g.OW * g.C, "y");
+  void* a = nullptr;
+  if (is_max) {
+    TORCH_CHECK(arg.has_value() && arg->defined(), "max pooling needs the argmax buffer");
+    check(*arg, at::kByte, (int64_t)g.N * g.OH * g.OW * g.C, "arg");
+    a = arg->data_ptr();
+  }
+  TORCH_CHECK(katib_hip::poolnhwc::launch_fwd(g, is_max, x.data_ptr(), y.data_ptr(), a, stream()) == hipSuccess,
+              "pool_fwd launch failed");
+}
+
+void pool_bwd(const Tensor& gy, const c10::optional<Tensor>& arg, const Tensor& gx, bool is_max,
+              const std::vector<int64_t>& geom) {
+  const auto g = pool_geom(geom);
+  check(gy, at::kBFloat16, (int64_t)g.N * g.OH * g.OW * g.C, "gy");
+  check(gx, at::kBFloat16, (int64_t)g.N * g.H * g.W * g.C, "gx");
+  const void* a = nullptr;
+  if (is_max) {
+    TORCH_CHECK(arg.has_value() && arg->defined(), "max pooling backward needs the argmax buffer");
+    check(*arg, at::kByte, (int64_t)g.N * g.OH * g.OW * g.C, "arg");
+    a = arg->data_ptr();
+  }
+  TORCH_CHECK(katib_hip::poolnhwc::launch_bwd(g, is_max, gy.data_ptr(), a, gx.data_ptr(), stream()) == hipSuccess,
+              "pool_bwd launch failed");
+}
+
 }  // namespace
 
 void register_dwconv(py::module& m) {
+  m.def("pool_nhwc_fwd", &pool_fwd, "max / avg pooling forward (NHWC bf16, valid padding)");
+  m.def("pool_nhwc_bwd", &pool_bwd, "max / avg pooling backward (NHWC bf16, gather, no atomics)");
   m.def("dw_fwd", &dw_fwd, "depthwise conv forward (NHWC bf16)", py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("y"), py::arg("geom"));
   m.def("dw_dgrad", &dw_dgrad, "depthwise conv input gradient (NHWC bf16)");

@@ -56,11 +56,45 @@ REP = int(_K.REP)
 # than ~180 small fold launches.
 FOLD = __import__("os").environ.get("KATIB_HIP_FOLD", "1") != "0"
 _R = 1 if FOLD else REP
+# Self-folding producers (darts_ops.h FoldTail): with a counter ring registered for the device,
+# every launch that adds into f64 replicas folds them in its last workgroup, and the fold_f64
+# launches between producers and consumers disappear. Needs FOLD (consumers read replica 0).
+# Off by default (KATIB_HIP_SELFFOLD=1 turns it on): measured on MI355X, one arrival counter
+# made every producer ~15-25 us slower (2000 same-address atomics serialise memory-side: B5
+# step 12.1 ms), 32 sharded counters still lose to the fold launches (8.22 vs 8.05 ms),
+# profiles/darts_selffold_edge_ab_r03.log.
+SELFFOLD = __import__("os").environ.get("KATIB_HIP_SELFFOLD", "0") != "0"
+_CTR: Dict[int, torch.Tensor] = {}
 
 
-def _fold64(segs):
-    if FOLD:
-        _K.fold_f64(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
+def set_selffold(on: bool):
+    """A/B switch for tests and experiments (call between steps, never inside a capture)."""
+    global SELFFOLD
+    SELFFOLD = bool(on)
+    _K.set_selffold(SELFFOLD)
+_CTR_SIZE = 64 * 33 * 32  # 64 launch slots of (top + 32 shard) counters, 128 B apart
+
+
+def _selffold(dev) -> bool:
+    """Register the device's counter ring on first use (never inside a graph capture, whose
+    private pool must not own it) and report whether producers on the current device fold
+    their own replicas (the C++ side attaches tails under exactly this condition)."""
+    if not FOLD or not SELFFOLD:
+        return False
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _CTR:
+        if torch.cuda.is_current_stream_capturing():
+            return bool(_K.selffold_ready())
+        t = torch.zeros(_CTR_SIZE, dtype=torch.int32, device=torch.device("cuda", idx))
+        _K.set_fold_counters(t)
+        _CTR[idx] = t
+    return bool(_K.selffold_ready())
+
+
+def _fold64(segs, dev=None):
+    """fold_f64 launch between producers and consumers, unless the producers folded themselves."""
+    if FOLD and (dev is None or not _selffold(dev)):
+        _K.fold_f64(segs)
 _CAP = {"combine_fwd": 3, "dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 8,
         "dw_bwd": 8, "pool_bwd": 8}
 _REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
@@ -151,6 +185,11 @@ def _launch(name: str, calls: List, *args):
 
 
 MULTI = __import__("os").environ.get("KATIB_HIP_MULTI", "1") != "0"  # mixed-variant launches (A/B switch)
+# fused per-edge input gradient (edge_bwd_kernel) instead of per-family dw_bwd / pool_bwd launches.
+# Off by default: measured SLOWER on MI355X (B5 step 9.22 vs 8.05 ms; its 4 conv slots run
+# serially inside each workgroup, and fewer / larger bands only narrow the gap: 8.74 ms at 64 KB
+# bands), profiles/darts_selffold_edge_ab_r03.log. KATIB_HIP_EDGE_BWD=1 turns it on.
+EDGE_BWD = __import__("os").environ.get("KATIB_HIP_EDGE_BWD", "0") != "0"
 
 
 def _dwpw_multi(entries):
@@ -258,6 +297,7 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
     (out, edges) - ``edges`` is the state :func:`_node_backward` needs."""
     E = len(specs)
     xs = [t.contiguous() for t in xs]
+    _selffold(xs[0].device)  # before any producer launch: registers the counter ring on first use
     N, C = xs[0].shape[:2]
     S0 = specs[0].stride
     Ho = (xs[0].shape[2] - 1) // S0 + 1
@@ -343,7 +383,7 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
     if fr_calls:
         _launch("pw_fwd", fr_calls, 2)
     if training and stage1:
-        _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage1))])
+        _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage1))], dev)
     # ---- separable stage 2 (stride 1, input BN-apply prologue)
     s2_groups = defaultdict(list)
     for e in edges:
@@ -360,7 +400,7 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
                 e.saved[prim] = (d1, z1, d2, z2)
     _dwpw_multi([(*c, K, 1, 1, K // 2) for K, calls in s2_groups.items() for c in calls])
     if training and stage2:
-        _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage2))])
+        _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage2))], dev)
     # ---- weighted sums into the node output
     if out is None:
         out = torch.empty(N, C, Ho, Wo, device=dev)
@@ -404,7 +444,8 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
         calls.append((dout, e.zl, e.bl, e.x if e.id_idx >= 0 else None, e.red, e.widx, e.id_idx, e.gw))
         segs += [(e.red, e.nred, e.nred), (e.gw, e.w.numel(), e.w.numel())]
     _launch("combine_bwd_reduce", calls)
-    _K.fold_f64(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
+    if not _selffold(dev):
+        _K.fold_f64(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
 
     def src(e, k, z):  # GradSrc of a weighted, BN'd op output
         j = e.widx.index(k)
@@ -443,40 +484,37 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
         _launch("pw_bwd", pw2 + (pwd if MULTI else []), 1, 0, True)
         if not MULTI and pwd:
             _launch("pw_bwd", pwd, 1, 0, True)
-        for K, calls in dw2.items():
-            _launch("dw_bwd", calls, K, 1, 1, K // 2)
+        if MULTI:  # both kernel sizes in one launch (distinct g1 / red1 per entry)
+            allc = [(*c, K) for K, calls in dw2.items() for c in calls]
+            for i in range(0, len(allc), _CAP["dw_bwd"]):
+                _K.dw_bwd_multi(allc[i:i + _CAP["dw_bwd"]])
+        else:
+            for K, calls in dw2.items():
+                _launch("dw_bwd", calls, K, 1, 1, K // 2)
         if training:
-            _fold64([(red1[n * REP * 2 * C:(n + 1) * REP * 2 * C], 2 * C, 2 * C) for n in range(len(seps))])
-        pw1, dw1 = [], defaultdict(list)
+            _fold64([(red1[n * REP * 2 * C:(n + 1) * REP * 2 * C], 2 * C, 2 * C) for n in range(len(seps))], dev)
+        pw1 = []
         for e, k, prim in seps:
-            K = int(prim[-1])
             d1, z1, d2, z2 = e.saved[prim]
             g1, r1 = e.saved[prim + "/g1"]
             b1 = e.refs[e.spec.slots[prim][0]]
             gs1 = (g1, z1, r1[:C] if training else None, r1[C:2 * C] if training else None, b1, None, 0, _R, 2 * C)
             dd1 = torch.empty_like(d1)
+            e.saved[prim + "/dd1"] = dd1
             g, gst = sink(e, prim + ".0.pw")
             pw1.append((gs1, e.P[prim + ".0.pw"], d1, e.x, dd1, None, g, 0, 0, gst))
-            g, gst = sink(e, prim + ".0.dw")
-            dw1[(K, e.S)].append((e.x, None, e.P[prim + ".0.dw"], dd1, gxs[e.i], g, None, gst, take_first(e.i)))
         _launch("pw_bwd", pw1, 1, 0, True)
-        for (K, S), calls in dw1.items():
-            _launch("dw_bwd", calls, K, 1, S, K // 2)
-    # ---- dilated convs (depthwise backward; the pointwise part ran above)
-    if dils:
-        dwd = defaultdict(list)
-        for e, k, prim in dils:
-            K = int(prim[-1])
-            g, gst = sink(e, prim + ".dw")
-            dwd[(K, e.S)].append((e.x, None, e.P[prim + ".dw"], dd_of[(e.i, prim)], gxs[e.i], g, None, gst,
-                                  take_first(e.i)))
-        for (K, S), calls in dwd.items():
-            _launch("dw_bwd", calls, K, 2, S, (K // 2) * 2)
-    # ---- pools (+ the identity skip of stride-1 edges)
-    pools = defaultdict(list)
-    for e in edges:
-        if "pool" not in e.saved:
-            continue
+
+    # ---- every edge's input gradient: stage-1 separable and dilated depthwise backward, pools and
+    # the identity skip in ONE fused launch (edge_bwd_kernel), else the per-family launches below
+    first = {e.i: take_first(e.i) for e in edges}
+
+    def tf(i):  # the first writer of gx_of(i) overwrites it
+        f = first.get(i, False)
+        first[i] = False
+        return f
+
+    def pool_srcs(e):
         za, zm, am = e.saved["pool"]
         ga = gm = None
         for k, p in enumerate(e.spec.prims):
@@ -484,27 +522,76 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
                 ga = src(e, k, za)
             elif p == "max_pooling_3x3":
                 gm = src(e, k, zm)
-        pools[e.S].append((ga, gm, e.x, dout if e.id_idx >= 0 else None, e.w, e.id_idx, gxs[e.i], am,
-                           take_first(e.i)))
-        e.id_done = True
-    if MULTI:  # both strides in one launch (entries are distinct edges: distinct gx buffers)
-        allp = [(*c, S) for S, calls in pools.items() for c in calls]
-        for i in range(0, len(allp), _CAP["pool_bwd"]):
-            _K.pool_bwd_multi(allp[i:i + _CAP["pool_bwd"]])
-    else:
-        for S, calls in pools.items():
-            _launch("pool_bwd", calls, S)
-    for e in edges:
-        if e.id_idx >= 0 and not e.id_done:
-            if take_first(e.i):
-                torch.mul(dout, e.w[e.id_idx], out=gxs[e.i])
-            else:
-                gxs[e.i].add_(dout * e.w[e.id_idx])
+        return ga, gm, am
+
+    if EDGE_BWD:
+        entries = []
+        for e in edges:
+            convs = [None] * 4
+            for k, prim in enumerate(e.spec.prims):
+                if prim.startswith("separable_convolution"):
+                    g, gst = sink(e, prim + ".0.dw")
+                    convs[0 if prim[-1] == "3" else 1] = (e.P[prim + ".0.dw"], e.saved[prim + "/dd1"], g, gst)
+                elif prim.startswith("dilated_convolution"):
+                    g, gst = sink(e, prim + ".dw")
+                    convs[2 if prim[-1] == "3" else 3] = (e.P[prim + ".dw"], dd_of[(e.i, prim)], g, gst)
+            ga, gm, am = pool_srcs(e) if "pool" in e.saved else (None, None, None)
+            entries.append((e.x, gxs[e.i], first[e.i], convs, ga, gm, am, dout if e.id_idx >= 0 else None, e.w,
+                            e.id_idx, e.S))
+        ok = True
+        for i in range(0, len(entries), 4):
+            ok = ok and bool(_K.edge_bwd(entries[i:i + 4]))
+        if ok:
+            for e in edges:
+                first[e.i] = False
+        elif len(entries) > 4:  # a partial launch cannot be undone: fail loudly
+            raise RuntimeError("edge_bwd accepted part of a node's edges")
+    if not EDGE_BWD or not ok:
+        if seps:
+            dw1 = defaultdict(list)
+            for e, k, prim in seps:
+                K = int(prim[-1])
+                g, gst = sink(e, prim + ".0.dw")
+                dw1[(K, e.S)].append((e.x, None, e.P[prim + ".0.dw"], e.saved[prim + "/dd1"], gxs[e.i], g, None, gst,
+                                      tf(e.i)))
+            for (K, S), calls in dw1.items():
+                _launch("dw_bwd", calls, K, 1, S, K // 2)
+        # ---- dilated convs (depthwise backward; the pointwise part ran above)
+        if dils:
+            dwd = defaultdict(list)
+            for e, k, prim in dils:
+                K = int(prim[-1])
+                g, gst = sink(e, prim + ".dw")
+                dwd[(K, e.S)].append((e.x, None, e.P[prim + ".dw"], dd_of[(e.i, prim)], gxs[e.i], g, None, gst,
+                                      tf(e.i)))
+            for (K, S), calls in dwd.items():
+                _launch("dw_bwd", calls, K, 2, S, (K // 2) * 2)
+        # ---- pools (+ the identity skip of stride-1 edges)
+        pools = defaultdict(list)
+        for e in edges:
+            if "pool" not in e.saved:
+                continue
+            ga, gm, am = pool_srcs(e)
+            pools[e.S].append((ga, gm, e.x, dout if e.id_idx >= 0 else None, e.w, e.id_idx, gxs[e.i], am, tf(e.i)))
+            e.id_done = True
+        if MULTI:  # both strides in one launch (entries are distinct edges: distinct gx buffers)
+            allp = [(*c, S) for S, calls in pools.items() for c in calls]
+            for i in range(0, len(allp), _CAP["pool_bwd"]):
+                _K.pool_bwd_multi(allp[i:i + _CAP["pool_bwd"]])
+        else:
+            for S, calls in pools.items():
+                _launch("pool_bwd", calls, S)
+        for e in edges:
+            if e.id_idx >= 0 and not e.id_done:
+                if tf(e.i):
+                    torch.mul(dout, e.w[e.id_idx], out=gxs[e.i])
+                else:
+                    gxs[e.i].add_(dout * e.w[e.id_idx])
     # ---- stride-2 skip (FactorizedReduce): scattered adds, so its gx must exist already
     frc = []
     for e in edges:
         if "skip_connection" in e.saved:
-            if take_first(e.i):
+            if tf(e.i):
                 gxs[e.i].zero_()
             k = e.spec.prims.index("skip_connection")
             (z,) = e.saved["skip_connection"]
@@ -582,6 +669,7 @@ def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2):
     """ReLU -> 1x1 conv (ReLUConvBN, operations.py) or FactorizedReduce (two stride-2 1x1
     convs on offset grids, channel-concatenated) -> BN(affine=False). Returns (out, state)."""
     x = x.contiguous()
+    _selffold(x.device)
     N, Cin, H, W = x.shape
     fr = w2 is not None
     Cout = w1.shape[0] * (2 if fr else 1)
@@ -594,7 +682,7 @@ def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2):
     else:
         _K.pw_fwd([(x, w1, z, stats, 0, 0)], 1)
     if training:
-        _fold64([(stats, 2 * Cout, 2 * Cout)])
+        _fold64([(stats, 2 * Cout, 2 * Cout)], x.device)
     bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
     out = torch.empty_like(z)
     _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], None, None, out, momentum, training, False)
@@ -609,7 +697,7 @@ def _stdconv_backward(state, dout, need_x, sinks, keys):
     red = zeros64(REP * nred, x.device)
     if training:
         _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
-        _fold64([(red, nred, nred)])
+        _fold64([(red, nred, nred)], x.device)
     gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0, _R, nred)
     g1, s1 = sinks.get(w1, keys[0])
     if fr:  # the two stride-2 grids leave 3 of 4 input pixels untouched: start from zeros
@@ -842,7 +930,8 @@ class _StemConvBN(torch.autograd.Function):
         nred = 2 * C + 1
         red = zeros64(REP * nred, x.device)
         _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
-        _K.fold_f64([(red, nred, nred)])
+        if not _selffold(x.device):
+            _K.fold_f64([(red, nred, nred)])
         need = ctx.needs_input_grad
         grads = [None] * 8
         sinks = _Sinks()

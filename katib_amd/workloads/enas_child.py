@@ -17,7 +17,8 @@ MFMA kernels (``ops/conv.py``; TF 'same' padding handled inside the kernel's gat
 depthwise convolutions on the NHWC depthwise kernels (``ops/dwconv.py``; the 3-channel
 image input is zero-padded to 8 channels there, so no op falls back to MIOpen), batch norm
 on the NHWC bf16 HIP kernels (``ops/batchnorm.py``, channel counts that are multiples of
-8), synthetic CIFAR-10-shaped data in HBM, and data parallelism
+8), max / average pooling of the ``reduction`` op on the NHWC bf16 pool kernels
+(``ops/pool.py``), synthetic CIFAR-10-shaped data in HBM, and data parallelism
 over the trial's GPUs (``WORLD_SIZE`` ranks, RCCL all-reduce of the flat gradient)
 in place of ``tf.distribute.MirroredStrategy``.
 """
@@ -35,6 +36,7 @@ import torch.nn.functional as F
 
 from ..ops import batchnorm as hbn
 from ..ops import conv as hconv
+from ..ops import pool as hpool
 from ..ops import dwconv as hdw
 from .common import CapturedStep, Timer, device, global_avg_pool, pattern_images, report
 
@@ -97,15 +99,20 @@ class Op(nn.Module):
             else:
                 p = geti("pool_size", 2)
                 st = geti("stride", p)
-                self.pool = (nn.MaxPool2d(p, st) if cfg.get("reduction_type", "max_pooling") == "max_pooling"
-                             else nn.AvgPool2d(p, st))
+                self.is_max = cfg.get("reduction_type", "max_pooling") == "max_pooling"
+                self.p, self.st = p, st
+                self.pool = nn.MaxPool2d(p, st) if self.is_max else nn.AvgPool2d(p, st)
                 self.cout, self.hw = cin, (hw - p) // st + 1
         else:
             raise ValueError("unknown opt_type %r" % self.kind)
 
     def forward(self, x):
         if self.kind == "reduction":
-            return x if self.identity else self.pool(x)
+            if self.identity:
+                return x
+            if hpool.supported(x, self.p, self.st):  # HIP NHWC bf16 pooling (no MIOpen in the graph)
+                return hpool.pool2d(x, self.p, self.st, self.is_max)
+            return self.pool(x)
         return self.body(F.relu(x))
 
 
