@@ -313,6 +313,15 @@ def cmd_metrics_collector(a, rest):
     return collect(parse_args(rest))
 
 
+def cmd_install(a):
+    from .deploy import render
+
+    files = render(a.profile, a.prefix, python=a.python, user=a.user, state_dir=a.state_dir, gpus=a.gpus,
+                   slots_per_gpu=a.slots_per_gpu)
+    print(json.dumps({"profile": a.profile, "prefix": os.path.abspath(a.prefix), "files": sorted(files)}))
+    return 0
+
+
 def cmd_openapi(a):
     from .api import openapi
 
@@ -417,6 +426,16 @@ def build_parser():
     inj.add_argument("--early-stopping-algorithm", default="", help="algorithm serving -s-earlystop")
     inj.add_argument("--db-manager", default="", help="DBManager address (default from KATIB_DB_MANAGER_*)")
     inj.set_defaults(fn=cmd_inject)
+
+    ins = sub.add_parser("install", help="render a node install (katib-config.yaml, env file, systemd units)")
+    ins.add_argument("--profile", default="standalone", help="standalone | mysql | postgres | services")
+    ins.add_argument("--prefix", required=True, help="output directory")
+    ins.add_argument("--python", default="", help="interpreter for the units (default: this one)")
+    ins.add_argument("--user", default="katib")
+    ins.add_argument("--state-dir", default="/var/lib/katib-amd")
+    ins.add_argument("--gpus", type=int, default=None)
+    ins.add_argument("--slots-per-gpu", type=int, default=1)
+    ins.set_defaults(fn=cmd_install)
 
     oa = sub.add_parser("openapi", help="print the v1beta1 Swagger 2.0 document (reference swagger.json layout)")
     oa.add_argument("--with-k8s", action="store_true", help="also define the v1.ObjectMeta / v1.Time types")
