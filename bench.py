@@ -25,6 +25,11 @@ The same JSON line also carries
 
 Lower is better; vs_baseline = value / 282 s (B5, 1x NVIDIA GPU, end to end).
 Data: synthetic CIFAR-10-shaped tensors resident in HBM, random-init weights.
+
+``--dtype bf16`` (secondary config, BASELINE.json config 4's precision): the DARTS edge kernels
+of the ``_hipkern_zbf16`` build store the per-op intermediates (depthwise outputs, pre-BN op
+outputs) as bf16; node states, gradients, BN statistics, weights and all arithmetic stay fp32.
+The headline (default) is fp32 like the reference.
 """
 
 from __future__ import annotations
@@ -59,10 +64,20 @@ def main():
     ap.add_argument("--capture", type=int, default=1)
     ap.add_argument("--ops", default=os.environ.get("KATIB_AMD_DARTS_OPS", "hip"))
     ap.add_argument("--valid-batches", type=int, default=10)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16: per-op intermediates stored as bf16 (the _hipkern_zbf16 build)")
     ap.add_argument("--full-search", type=int, default=-1,
                     help="also run the whole search (epochs x (steps/epoch train steps + validation)) and report "
                          "its measured wall clock next to the projection (-1: on for the b5 config)")
     args = ap.parse_args()
+
+    if args.dtype == "bf16" and not os.environ.get("KATIB_AMD_HIPKERN"):
+        # the variant extension replaces the fp32 one module-wide: rerun in a child that loads it
+        # (before this process touches the GPU; the child inherits the torchrun env)
+        from katib_amd import _build
+
+        env = dict(os.environ, KATIB_AMD_HIPKERN=_build.zbf16_target())
+        return subprocess.call([sys.executable] + sys.argv, env=env)
 
     # trials/hour (BASELINE config 2) first, from rank 0, before this process touches the GPU:
     # the scheduler's warm workers then own every GPU while the experiment runs
@@ -84,6 +99,8 @@ def main():
         try:
             dops.set_backend("hip")
             from katib_amd.ops import hip_darts  # noqa: F401  (fails loudly if the extension is missing)
+            if args.dtype == "bf16" and hip_darts.ZDT != torch.bfloat16:
+                raise RuntimeError("--dtype bf16 needs the _hipkern_zbf16 build (KATIB_AMD_HIPKERN)")
         except Exception as e:
             if comm.rank == 0:
                 print("hip ops unavailable (%s); using torch ops" % e, file=sys.stderr)
@@ -167,7 +184,7 @@ def main():
 
     # same-node comparator: the PyTorch op backend, eager (no graph), same config and batch
     torch_ms = None
-    if args.comparator_steps > 0 and dev.type == "cuda":
+    if args.comparator_steps > 0 and dev.type == "cuda" and args.dtype == "fp32":
         dops.set_backend("torch")
         ref = DartsSearch(layout, dev, comm, capture=False)
         for i in range(2):
@@ -197,7 +214,9 @@ def main():
             "higher_is_better": False,
             "scaling": args.scaling,
             "vs_baseline": round(wall / B5_SECONDS, 5) if args.config == "b5" else None,
-            "dtype": "fp32",
+            "dtype": args.dtype,
+            "precision": ("fp32" if args.dtype == "fp32" else
+                          "bf16 per-op intermediates (d, z); fp32 node states, gradients, BN statistics, weights, math"),
             "data": "synthetic (CIFAR-10-shaped, device-resident); random-init weights",
             "config": {"model": "darts-cnn-cifar10 supernet (%s: C=%d, L=%d, N=%d, stem x%d, 6 primitives + none)"
                                 % (args.config, cfg["init_channels"], cfg["num_layers"], cfg["num_nodes"],
@@ -249,4 +268,4 @@ def trials_per_hour(gpus: int, per_gpu: int):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

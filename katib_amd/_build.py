@@ -140,6 +140,18 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", 
     return out
 
 
+def zbf16_target() -> str:
+    return os.path.join(PKG_DIR, "_hipkern_zbf16" + EXT_SUFFIX)
+
+
+def build_hip_zbf16(force: bool = False, verbose: bool = False) -> str:
+    """The bf16-intermediates variant of the HIP extension (``-DKATIB_DARTS_ZBF16``: the DARTS
+    edge kernels store depthwise outputs and pre-BN op outputs as bf16), loaded with
+    ``KATIB_AMD_HIPKERN=<this path>`` by ``bench.py --dtype bf16`` and its GPU tests."""
+    return build_hip(force=force, verbose=verbose, defines=["KATIB_DARTS_ZBF16"], out=zbf16_target(),
+                     build_dir=os.path.join(PKG_DIR, "csrc", "hip", "build_zbf16"))
+
+
 if __name__ == "__main__":
     print(build_native(verbose=True))
     print(build_hip(verbose=True))

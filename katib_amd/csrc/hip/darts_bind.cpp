@@ -21,6 +21,18 @@ void check_f32(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+// per-op intermediates (d, z): fp32, or bf16 in the KATIB_DARTS_ZBF16 build (darts_ops.h zt)
+constexpr at::ScalarType kZType = kZbf16 ? at::kBFloat16 : at::kFloat;
+
+void check_z(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == kZType, name, " must be ", kZbf16 ? "bfloat16" : "float32",
+              " (the per-op intermediates' storage type of this build)");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+zt* zptr(const Tensor& t) { return reinterpret_cast<zt*>(t.data_ptr()); }
+
 template <typename T>
 T* ptr_or_null(const OptT& t) {
   return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
@@ -65,9 +77,9 @@ GradSrc make_gs(const py::tuple& t, int C) {
   TORCH_CHECK(t.size() == 9, "grad-source tuple has 9 fields");
   Tensor gt = t[0].cast<Tensor>(), zt = t[1].cast<Tensor>();
   check_f32(gt, "g");
-  check_f32(zt, "z");
+  check_z(zt, "z");
   g.g = gt.data_ptr<float>();
-  g.z = zt.data_ptr<float>();
+  g.z = zptr(zt);
   OptT s1 = t[2].cast<OptT>(), s2 = t[3].cast<OptT>();
   g.S1 = ptr_or_null<double>(s1);
   g.S2 = ptr_or_null<double>(s2);
@@ -179,7 +191,10 @@ static bool fill_dwpw(const py::tuple& t, DwPwFwdArgs& a, int64_t K, int64_t dil
   auto inbn = t[3].cast<c10::optional<py::tuple>>();
   Tensor d = t[4].cast<Tensor>(), z = t[5].cast<Tensor>();
   OptT stats = t[6].cast<OptT>();
-  check_f32(x, "x"); check_f32(dw, "dw"); check_f32(pw, "pw"); check_f32(d, "d"); check_f32(z, "z");
+  const bool has_inbn = t[3].cast<c10::optional<py::tuple>>().has_value();
+  if (has_inbn) check_z(x, "x (previous stage z)");
+  else check_f32(x, "x");
+  check_f32(dw, "dw"); check_f32(pw, "pw"); check_z(d, "d"); check_z(z, "z");
   TORCH_CHECK(x.dim() == 4, "x must be NCHW");
   TORCH_CHECK((K == 3 || K == 5) && (dil == 1 || dil == 2) && (S == 1 || S == 2), "K in {3,5}, dil, S in {1,2}");
   const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -189,8 +204,8 @@ static bool fill_dwpw(const py::tuple& t, DwPwFwdArgs& a, int64_t K, int64_t dil
   TORCH_CHECK(64 % Wo == 0 && Ho % (64 / Wo) == 0, "tile constraint: 64 % Wo == 0 and Ho % (64/Wo) == 0");
   TORCH_CHECK(C <= kMaxC, "C too large");
   TORCH_CHECK(Ho == (H + 2 * pad - dil * (K - 1) - 1) / S + 1, "output height mismatch");
-  a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.pw = pw.data_ptr<float>();
-  a.d = d.data_ptr<float>(); a.z = z.data_ptr<float>(); a.stats = ptr_or_null<double>(stats);
+  a.x = x.data_ptr(); a.dw = dw.data_ptr<float>(); a.pw = pw.data_ptr<float>();
+  a.d = zptr(d); a.z = zptr(z); a.stats = ptr_or_null<double>(stats);
   if (a.stats) TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * C, "stats f64 [kRep][2C]");
   a.N = N; a.C = C; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.pad = pad;
   const int TR = 64 / Wo;
@@ -271,14 +286,14 @@ void pw_fwd(std::vector<py::tuple> calls, int64_t S) {
     Tensor x = t[0].cast<Tensor>(), pw = t[1].cast<Tensor>(), z = t[2].cast<Tensor>();
     OptT stats = t[3].cast<OptT>();
     const int co_off = t[4].cast<int>(), off = t[5].cast<int>();
-    check_f32(x, "x"); check_f32(pw, "pw"); check_f32(z, "z");
+    check_f32(x, "x"); check_f32(pw, "pw"); check_z(z, "z");
     const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
     const int Cout = pw.size(0), Ho = z.size(2), Wo = z.size(3);
     TORCH_CHECK(pw.size(1) == Cin && co_off + Cout <= z.size(1) && z.size(0) == N, "pw shapes");
     TORCH_CHECK((Ho * Wo) % 64 == 0, "Ho*Wo must be a multiple of 64");
     TORCH_CHECK(Cin <= kMaxC && Cout <= kMaxC, "channels");
     PwFwdArgs& a = bt.e[i];
-    a.x = x.data_ptr<float>(); a.pw = pw.data_ptr<float>(); a.z = z.data_ptr<float>();
+    a.x = x.data_ptr<float>(); a.pw = pw.data_ptr<float>(); a.z = zptr(z);
     a.stats = ptr_or_null<double>(stats);
     if (a.stats)
       TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * z.size(1), "stats [kRep][2Ctot]");
@@ -304,13 +319,13 @@ static void pool_fwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
     bt.e[i].S = (int)S;
     Tensor x = t[0].cast<Tensor>(), zavg = t[1].cast<Tensor>(), zmax = t[2].cast<Tensor>();
     OptT sa = t[3].cast<OptT>(), sm = t[4].cast<OptT>(), amax = t[5].cast<OptT>();
-    check_f32(x, "x"); check_f32(zavg, "zavg"); check_f32(zmax, "zmax");
+    check_f32(x, "x"); check_z(zavg, "zavg"); check_z(zmax, "zmax");
     PoolFwdArgs& a = bt.e[i];
     if (amax.has_value() && amax->defined()) {
       TORCH_CHECK(amax->scalar_type() == at::kByte && amax->numel() == zmax.numel(), "amax must be uint8 like zmax");
       a.amax = amax->data_ptr<uint8_t>();
     }
-    a.x = x.data_ptr<float>(); a.zavg = zavg.data_ptr<float>(); a.zmax = zmax.data_ptr<float>();
+    a.x = x.data_ptr<float>(); a.zavg = zptr(zavg); a.zmax = zptr(zmax);
     a.stats_avg = ptr_or_null<double>(sa); a.stats_max = ptr_or_null<double>(sm);
     if (a.stats_avg) TORCH_CHECK(sa->scalar_type() == at::kDouble && sa->numel() >= kRep * 2 * x.size(1), "stats");
     if (a.stats_max) TORCH_CHECK(sm->scalar_type() == at::kDouble && sm->numel() >= kRep * 2 * x.size(1), "stats");
@@ -357,9 +372,9 @@ void combine_fwd(std::vector<py::tuple> calls, OptT gamma, OptT beta, Tensor out
     a.N = out.size(0); a.C = C; a.HW = out.size(2) * out.size(3);
     a.nops = zs.size();
     for (size_t k = 0; k < zs.size(); ++k) {
-      check_f32(zs[k], "z");
+      check_z(zs[k], "z");
       TORCH_CHECK(zs[k].sizes() == out.sizes(), "combine input shape");
-      a.z[k] = zs[k].data_ptr<float>();
+      a.z[k] = zptr(zs[k]);
       a.bn[k] = make_bn(bns[k], C);
       a.widx[k] = widx[k];
     }
@@ -402,7 +417,8 @@ void combine_bwd_reduce(std::vector<py::tuple> calls) {
     TORCH_CHECK(a.nops <= kMaxOps && red.numel() >= (int64_t)kRep * a.rstride, "red size [kRep][(nops+1)C+1]");
     for (int k = 0; k < a.nops; ++k) {
       TORCH_CHECK(zs[k].sizes() == dout.sizes(), "z shape");
-      a.z[k] = zs[k].data_ptr<float>();
+      check_z(zs[k], "z");
+      a.z[k] = zptr(zs[k]);
       a.bn[k] = make_bn(bns[k], a.C);
     }
     a.dout = dout.data_ptr<float>(); a.xid = ptr_or_null<float>(xid); a.red = red.data_ptr<double>();
@@ -452,7 +468,8 @@ void pw_bwd(std::vector<py::tuple> calls, int64_t S, int64_t mode, bool need_dx)
     const int co_off = t[7].cast<int>(), off = t[8].cast<int>();
     const int64_t gstride = t[9].cast<int64_t>();
     const bool overwrite = t.size() > 10 && t[10].cast<bool>();
-    check_f32(pw, "pw"); check_f32(x, "x");
+    check_f32(pw, "pw");
+    if (mode != 0) check_f32(x, "x");  // mode 0 reads only the shape of x (the stage input, maybe a zt z)
     PwBwdArgs& a = bt.e[i];
     a.overwrite = overwrite;
     TORCH_CHECK(!overwrite || (mode == 1 && S == 1 && off == 0), "gx overwrite needs the stride-1 full-coverage form");
@@ -465,8 +482,10 @@ void pw_bwd(std::vector<py::tuple> calls, int64_t S, int64_t mode, bool need_dx)
     a.H = x.size(2); a.W = x.size(3);
     TORCH_CHECK(Cin * Cout <= 8192, "pw_bwd supports Cin*Cout <= 8192");
     TORCH_CHECK((a.Ho * a.Wo) % 64 == 0, "Ho*Wo % 64");
-    a.pw = pw.data_ptr<float>(); a.x = x.data_ptr<float>();
-    a.ain = ptr_or_null<float>(ain); a.dd = ptr_or_null<float>(dd); a.gx = ptr_or_null<float>(gx);
+    a.pw = pw.data_ptr<float>(); a.x = mode != 0 ? x.data_ptr<float>() : nullptr;
+    if (ain.has_value() && ain->defined()) check_z(*ain, "ain (depthwise output d)");
+    a.ain = ain.has_value() && ain->defined() ? zptr(*ain) : nullptr;
+    a.dd = ptr_or_null<float>(dd); a.gx = ptr_or_null<float>(gx);
     a.gW = ptr_or_null<float>(gW);
     if (mode == 0) {
       TORCH_CHECK(a.ain && (!need_dx || a.dd), "mode 0 needs ain (and dd)");
@@ -539,14 +558,16 @@ void dw_bwd_fill(std::vector<py::tuple>& calls, DwBwdBatch& bt, const int64_t* K
     OptT gW = t[5].cast<OptT>(), red = t[6].cast<OptT>();
     const int64_t gstride = t[7].cast<int64_t>();
     const bool overwrite = t[8].cast<bool>();
-    check_f32(x, "x"); check_f32(dw, "dw"); check_f32(dd, "dd"); check_f32(gout, "gout");
+    if (inbn.has_value()) check_z(x, "x (stage-1 z)");
+    else check_f32(x, "x");
+    check_f32(dw, "dw"); check_f32(dd, "dd"); check_f32(gout, "gout");
     DwBwdArgs& a = bt.e[i];
     a.N = x.size(0); a.C = x.size(1); a.H = x.size(2); a.W = x.size(3); a.Ho = dd.size(2); a.Wo = dd.size(3);
     TORCH_CHECK(64 % a.Wo == 0 && a.Ho % (64 / a.Wo) == 0, "tile constraint");
     TORCH_CHECK(a.H == a.Ho * S && a.W == a.Wo * S, "dw_bwd needs H == Ho*S");
     TORCH_CHECK(gout.sizes() == x.sizes(), "gout shape");
     TORCH_CHECK(dw.numel() == a.C * K * K && dd.size(1) == a.C, "dw_bwd weight / grad shapes");
-    a.x = x.data_ptr<float>(); a.dw = dw.data_ptr<float>(); a.dd = dd.data_ptr<float>();
+    a.x = x.data_ptr(); a.dw = dw.data_ptr<float>(); a.dd = dd.data_ptr<float>();
     a.gout = gout.data_ptr<float>(); a.gW = ptr_or_null<float>(gW); a.red = ptr_or_null<double>(red);
     check_grad_sink(gW, (int64_t)a.C * K * K, gstride);
     a.gstride = gstride;
@@ -743,6 +764,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("selffold_ready", &selffold_ready, "launches on the current device fold their own f64 replicas");
   m.def("set_selffold", &set_selffold, "turn self-folding launches on / off (default: KATIB_HIP_SELFFOLD)");
   m.attr("REP") = kRep;
+  m.attr("ZBF16") = kZbf16;  // per-op intermediates stored as bf16 (the _hipkern_zbf16 variant)
   m.def("max_blocks", &max_blocks);
   register_xgmi(m);
   register_conv(m);

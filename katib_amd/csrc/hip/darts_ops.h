@@ -1,8 +1,39 @@
 // Argument blocks for the DARTS edge kernels (darts_ops.hip). Passed by value.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
 
 namespace katib_hip {
+
+// Storage type of the per-op intermediates of a DARTS edge (depthwise outputs d, pre-BN op
+// outputs z: ~90 % of a supernet step's activation bytes). fp32 by default; the bf16 build
+// variant (-DKATIB_DARTS_ZBF16, _hipkern_zbf16.so) stores them as bf16 and keeps everything
+// else fp32: node states, every gradient, BN statistics and reductions, weights, the math.
+#ifdef KATIB_DARTS_ZBF16
+typedef __hip_bfloat16 zt;
+constexpr bool kZbf16 = true;
+#else
+typedef float zt;
+constexpr bool kZbf16 = false;
+#endif
+typedef float zf4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float z2f(float v) { return v; }
+__device__ __forceinline__ float z2f(__hip_bfloat16 v) { return __bfloat162float(v); }
+__device__ __forceinline__ void zput(float* p, float v) { *p = v; }
+__device__ __forceinline__ void zput(__hip_bfloat16* p, float v) { *p = __float2bfloat16(v); }
+// 4 consecutive elements (16-byte fp32 / 8-byte bf16 access; callers keep 16-byte alignment)
+__device__ __forceinline__ zf4 zld4(const float* p) { return *reinterpret_cast<const zf4*>(p); }
+__device__ __forceinline__ zf4 zld4(const __hip_bfloat16* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return zf4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+             __uint_as_float(u.y & 0xffff0000u)};
+}
+__device__ __forceinline__ void zst4(float* p, zf4 v) { *reinterpret_cast<zf4*>(p) = v; }
+__device__ __forceinline__ void zst4(__hip_bfloat16* p, zf4 v) {
+  __hip_bfloat16 b[4] = {__float2bfloat16(v.x), __float2bfloat16(v.y), __float2bfloat16(v.z), __float2bfloat16(v.w)};
+  *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(b);
+}
 
 constexpr int kMaxOps = 8;
 constexpr int kMaxC = 256;
@@ -30,7 +61,7 @@ struct BNRef {              // where a BN layer's normalisation statistics come 
 
 struct GradSrc {            // d(loss)/d(z) evaluated on the fly: BN backward of a weighted op
   const float* g;           // upstream gradient (dout of the edge, or a stored stage gradient)
-  const float* z;           // pre-BN tensor
+  const zt* z;              // pre-BN tensor
   const double* S1;         // [C] sum g            (replica r at + r*rstride)
   const double* S2;         // [C] sum g * zhat
   BNRef bn;
@@ -42,48 +73,51 @@ struct GradSrc {            // d(loss)/d(z) evaluated on the fly: BN backward of
 };
 
 struct DwPwFwdArgs {
-  const float* x; BNRef inbn; const float* dw; const float* pw;
-  float* d; float* z; double* stats;  // stats: kRep replicas of [2C]
+  const void* x;  // node state (fp32), or the previous stage's z (zt) when it carries an input BN
+  BNRef inbn; const float* dw; const float* pw;
+  zt* d; zt* z; double* stats;  // stats: kRep replicas of [2C]
   int N, C, H, W, Ho, Wo, pad, chunk, use_mfma;
   int variant;  // dwpw_plane_multi_kernel: ((K == 5) * 4 + (dil == 2) * 2 + (S == 2)) * 4 + prebn * 2 + vec
   int nblk;     // dwpw_plane_multi_kernel: workgroups of this entry (grid.x is the max over entries)
 };
 
 struct PwFwdArgs {
-  const float* x; const float* pw; float* z; double* stats;  // stats: kRep replicas of [2*CoutTotal]
+  const void* x;  // relu: node state (fp32); identity: a wide dw-pw stage's depthwise output d (zt)
+  const float* pw; zt* z; double* stats;  // stats: kRep replicas of [2*CoutTotal]
   int N, Cin, Cout, CoutTotal, co_off, H, W, Ho, Wo, S, off;
   int relu;  // 1: input = relu(x) (StdConv / FactorizedReduce); 0: identity (pointwise half of a dw-pw stage)
 };
 
 struct PoolFwdArgs {
-  const float* x; float* zavg; float* zmax; double* stats_avg; double* stats_max; unsigned char* amax;
+  const float* x; zt* zavg; zt* zmax; double* stats_avg; double* stats_max; unsigned char* amax;
   int N, C, H, W, Ho, Wo;  // stats: kRep replicas of [2C] each
   int S, nblk;             // pool_fwd_multi_kernel: per-entry stride and workgroups
 };
 
 struct CombineFwdArgs {
-  const float* z[kMaxOps]; BNRef bn[kMaxOps]; int widx[kMaxOps]; int nops;
+  const zt* z[kMaxOps]; BNRef bn[kMaxOps]; int widx[kMaxOps]; int nops;
   BNRef upd[kMaxOps]; int nupd;  // extra BN layers whose running stats are updated here (not summed)
   const float* w; int id_idx; const float* xid; const float* gamma; const float* beta;
   float* out; int N, C, HW; float momentum; int update_running; int accumulate;
 };
 
 struct CombineBwdArgs {
-  const float* dout; const float* z[kMaxOps]; BNRef bn[kMaxOps]; int nops;
+  const float* dout; const zt* z[kMaxOps]; BNRef bn[kMaxOps]; int nops;
   const float* xid; double* red; int N, C, HW;  // red: kRep replicas of [(nops+1)*C + 1]
   double* gw; int widx[kMaxOps]; int id_idx;  // optional: d(loss)/d(softmax weight), kRep replicas of [nw]
   int rstride, gwstride;
 };
 
 struct PwBwdArgs {
-  GradSrc gs; const float* pw; const float* ain; const float* x; float* dd; float* gx; float* gW;
+  GradSrc gs; const float* pw; const zt* ain; const float* x; float* dd; float* gx; float* gW;
   int gstride;  // floats between gW replicas (0: single accumulator)
   int N, Cin, Cout, CoutTotal, co_off, H, W, Ho, Wo, S, off, mode, need_dx;
   int overwrite;  // mode 1, stride 1: gx = masked grad instead of += (the kernel covers every pixel)
 };
 
 struct DwBwdArgs {
-  const float* x; BNRef inbn; const float* dw; const float* dd; float* gout; float* gW; double* red;
+  const void* x;  // node state (fp32), or the stage-1 z (zt) when it carries an input BN
+  BNRef inbn; const float* dw; const float* dd; float* gout; float* gW; double* red;
   int gstride;  // floats between gW replicas (0: single accumulator); red: kRep replicas of [2C]
   int N, C, H, W, Ho, Wo, pad, chunk;
   int overwrite;  // non-PREBN: gout = masked grad (first writer of this input gradient) instead of +=

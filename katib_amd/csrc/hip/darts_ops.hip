@@ -161,6 +161,23 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// An edge-kernel input that is either a node state (fp32) or the previous stage's z (zt, Z = true):
+// one element / four consecutive elements (i a multiple of 4, 16-byte-aligned base) as fp32
+template <bool Z>
+__device__ __forceinline__ float xval(const void* p, size_t i) {
+  if constexpr (Z) return z2f(static_cast<const zt*>(p)[i]);
+  else return static_cast<const float*>(p)[i];
+}
+template <bool Z>
+__device__ __forceinline__ float4 xval4(const void* p, size_t i) {
+  if constexpr (Z) {
+    const zf4 t = zld4(static_cast<const zt*>(p) + i);
+    return make_float4(t.x, t.y, t.z, t.w);
+  } else {
+    return *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+  }
+}
+
 // Self-fold epilogue (darts_ops.h FoldTail). Called by EVERY thread of EVERY workgroup of the
 // launch, after the workgroup's last replica atomic. The arrival add is relaxed: the payload is
 // device-scope atomics (performed memory-side), drained by each wave's vmcnt(0) before the
@@ -240,7 +257,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int n = t / tiles, oy0 = (t % tiles) * TR;
     const int iy0 = oy0 * S - pad, ix0 = -pad;
-    const float* xin = a.x + (size_t)n * C * H * W;
+    const size_t xin = (size_t)n * C * H * W;
     for (int c0 = 0; c0 < C; c0 += a.chunk) {
       const int cn = min(a.chunk, C - c0);
       const int tot = cn * IR * IW;
@@ -250,7 +267,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
         int iy = iy0 + r, ix = ix0 + q, c = c0 + cc;
         float v = 0.f;
         if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-          v = xin[((size_t)c * H + iy) * W + ix];
+          v = xval<PREBN>(a.x, xin + ((size_t)c * H + iy) * W + ix);
           if (PREBN) v = (v - sMean[c]) * sInv[c];
           v = fmaxf(v, 0.f);
         }
@@ -270,7 +287,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
 #pragma unroll
           for (int kx = 0; kx < K; ++kx) acc += wk[ky * K + kx] * src[ky * DIL * IW + kx * DIL];
         sD[c * P + p] = acc;
-        a.d[(((size_t)n * C + c) * Ho + oy0 + ty) * Wo + tx] = acc;
+        zput(a.d + (((size_t)n * C + c) * Ho + oy0 + ty) * Wo + tx, acc);
       }
       __syncthreads();
     }
@@ -297,7 +314,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
           for (int pb = 0; pb < 4; ++pb) {
             int p = pb * 16 + (lane & 15);
             float v = acc[pb][r];
-            a.z[(((size_t)n * C + co) * Ho + oy0 + p / Wo) * Wo + p % Wo] = v;
+            zput(a.z + (((size_t)n * C + co) * Ho + oy0 + p / Wo) * Wo + p % Wo, v);
             s += v;
             s2 += v * v;
           }
@@ -318,7 +335,7 @@ __global__ void __launch_bounds__(256) dwpw_fwd_kernel(DwPwFwdBatch bt) {
         const float* wrow = a.pw + cou * C;
         float v = 0.f;
         for (int ci = 0; ci < C; ++ci) v += wrow[ci] * sD[ci * P + lane];
-        a.z[(((size_t)n * C + cou) * Ho + oy0 + lane / Wo) * Wo + lane % Wo] = v;
+        zput(a.z + (((size_t)n * C + cou) * Ho + oy0 + lane / Wo) * Wo + lane % Wo, v);
         float s = wave_sum(v), s2 = wave_sum(v * v);
         if (lane == 0) {
           sStat[cou] += s;
@@ -365,7 +382,7 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
     sStat[C + tid] = 0.f;
   }
   __syncthreads();
-  const float* xin = a.x + ((size_t)n * a.C + c0) * H * W;
+  const size_t xin = ((size_t)n * a.C + c0) * H * W;
   if (VEC) {
     // 16-byte loads over the band's contiguous in-range rows, scattered into the padded plane;
     // the zero border (rows outside [0, H), pad columns) is written separately
@@ -373,7 +390,7 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
 #pragma unroll 4
     for (int i = tid; i < C * q4; i += 256) {
       const int c = i / q4, o = (i - c * q4) * 4, r = o / W, ix = o - r * W;
-      float4 v = *reinterpret_cast<const float4*>(xin + ((size_t)c * H + va) * W + o);
+      float4 v = xval4<PREBN>(a.x, xin + ((size_t)c * H + va) * W + o);
       if (PREBN) {
         const float m = sMean[c], iv = sInv[c];
         v.x = (v.x - m) * iv;
@@ -402,12 +419,12 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
     for (int row = wave; row < C * HP; row += 4) {
       const int c = row / HP, r = row - c * HP, iy = iyb + r;
       const bool rok = iy >= 0 && iy < H;
-      const float* src = xin + ((size_t)c * H + (rok ? iy : 0)) * W;
+      const size_t src = xin + ((size_t)c * H + (rok ? iy : 0)) * W;
       for (int q = lane; q < WP; q += 64) {
         const int ix = q - pad;
         float v = 0.f;
         if (rok && ix >= 0 && ix < W) {
-          v = src[ix];
+          v = xval<PREBN>(a.x, src + ix);
           if (PREBN) v = (v - sMean[c]) * sInv[c];
           v = fmaxf(v, 0.f);
         }
@@ -420,8 +437,8 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
 #pragma unroll
   for (int c = 0; c < C; ++c) st1[c] = st2[c] = 0.f;
   const int HWo = Ho * Wo;
-  float* dn = a.d + ((size_t)n * a.C + c0) * HWo;
-  float* zn = a.z + (size_t)n * C * HWo;
+  zt* dn = a.d + ((size_t)n * a.C + c0) * HWo;
+  zt* zn = a.z + (size_t)n * C * HWo;
   for (int p = oy0 * Wo + tid; p < oy1 * Wo; p += 256) {
     const int oy = p / Wo, ox = p - oy * Wo;
     float d[C];
@@ -435,7 +452,7 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
 #pragma unroll
         for (int kx = 0; kx < K; ++kx) acc += wk[ky * K + kx] * src[ky * DIL * WP + kx * DIL];
       d[c] = acc;
-      dn[(size_t)c * HWo + p] = acc;
+      zput(dn + (size_t)c * HWo + p, acc);
     }
     if (!PW) continue;
 #pragma unroll
@@ -443,7 +460,7 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
       float z = 0.f;
 #pragma unroll
       for (int ci = 0; ci < C; ++ci) z += a.pw[co * C + ci] * d[ci];
-      zn[(size_t)co * HWo + p] = z;
+      zput(zn + (size_t)co * HWo + p, z);
       st1[co] += z;
       st2[co] += z * z;
     }
@@ -554,10 +571,15 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
       const int ci = 4 * k + q;
       f4 v;
       if (flat) {
-        v = *reinterpret_cast<const f4*>(a.x + ((size_t)n * CI + ci) * HWo + pp);
-        if (a.relu) v = f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+        const size_t o = ((size_t)n * CI + ci) * HWo + pp;
+        if (a.relu) {  // node state (fp32), relu on the way in
+          v = *reinterpret_cast<const f4*>(static_cast<const float*>(a.x) + o);
+          v = f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+        } else {  // depthwise output d of a wide dw-pw stage
+          v = zld4(static_cast<const zt*>(a.x) + o);
+        }
       } else if (fr2) {
-        const float* plane = a.x + ((size_t)n * CI + ci) * a.H * a.W;
+        const float* plane = static_cast<const float*>(a.x) + ((size_t)n * CI + ci) * a.H * a.W;
         float v0, v1, v2, v3;
         fr2_pair(plane, a.W, Wo, a.off, pp, v0, v1);
         fr2_pair(plane, a.W, Wo, a.off, pp + 2, v2, v3);
@@ -566,7 +588,9 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int p = pp + t, oy = p / Wo, ox = p - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
-          v[t] = (iy < a.H && ix < a.W) ? fmaxf(a.x[(((size_t)n * CI + ci) * a.H + iy) * a.W + ix], 0.f) : 0.f;
+          v[t] = (iy < a.H && ix < a.W)
+                     ? fmaxf(static_cast<const float*>(a.x)[(((size_t)n * CI + ci) * a.H + iy) * a.W + ix], 0.f)
+                     : 0.f;
         }
       }
 #pragma unroll
@@ -580,7 +604,7 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const f4 z = f4{acc[bo][0][r], acc[bo][1][r], acc[bo][2][r], acc[bo][3][r]};
-        *reinterpret_cast<f4*>(a.z + ((size_t)n * a.CoutTotal + a.co_off + cb0 + bo * 16 + 4 * q + r) * HWo + pp) = z;
+        zst4(a.z + ((size_t)n * a.CoutTotal + a.co_off + cb0 + bo * 16 + 4 * q + r) * HWo + pp, z);
         s1[bo][r] += (z.x + z.y) + (z.z + z.w);
         s2[bo][r] += (z.x * z.x + z.y * z.y) + (z.z * z.z + z.w * z.w);
       }
@@ -634,7 +658,10 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdBatch bt) {
       int pp = prem + p, oy = pp / Wo, ox = pp % Wo;
       int iy = oy * a.S + a.off, ix = ox * a.S + a.off;
       float v = 0.f;
-      if (iy < H && ix < W) v = fmaxf(a.x[(((size_t)n * Cin + ci) * H + iy) * W + ix], 0.f);
+      if (iy < H && ix < W) {
+        const size_t xi = (((size_t)n * Cin + ci) * H + iy) * W + ix;
+        v = a.relu ? fmaxf(static_cast<const float*>(a.x)[xi], 0.f) : z2f(static_cast<const zt*>(a.x)[xi]);
+      }
       sX[i] = v;
     }
     __syncthreads();
@@ -643,7 +670,7 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdBatch bt) {
       const float* wrow = a.pw + cou * Cin;
       float v = 0.f;
       for (int ci = 0; ci < Cin; ++ci) v += wrow[ci] * sX[ci * P + lane];
-      a.z[((size_t)n * a.CoutTotal + a.co_off + cou) * HWo + prem + lane] = v;
+      zput(a.z + ((size_t)n * a.CoutTotal + a.co_off + cou) * HWo + prem + lane, v);
       float s = wave_sum(v), s2 = wave_sum(v * v);
       if (lane == 0) {
         sStat[cou] += s;
@@ -692,8 +719,8 @@ __device__ __forceinline__ void pool_fwd_body(const PoolFwdArgs& a, const int bx
         }
       }
       float av = sum / (float)cnt;
-      a.zavg[(size_t)nc * Ho * Wo + o] = av;
-      a.zmax[(size_t)nc * Ho * Wo + o] = mx;
+      zput(a.zavg + (size_t)nc * Ho * Wo + o, av);
+      zput(a.zmax + (size_t)nc * Ho * Wo + o, mx);
       if (a.amax) a.amax[(size_t)nc * Ho * Wo + o] = (unsigned char)arg;
       sa += av;
       sa2 += av * av;
@@ -792,7 +819,7 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
         const CombineFwdArgs& a = bt.e[e < ne ? e : 0];
 #pragma unroll
         for (int k = 0; k < kMaxOps; ++k)
-          if (e < ne && k < a.nops) zv[e][k] = reinterpret_cast<const f4*>(a.z[k])[i4];
+          if (e < ne && k < a.nops) zv[e][k] = zld4(a.z[k] + 4 * i4);
         if (e < ne && a.xid) xv[e] = reinterpret_cast<const f4*>(a.xid)[i4];
       }
       f4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -825,7 +852,7 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
       const float* sw = sW + e * (kMaxOps + 1);
       for (int k = 0; k < a.nops; ++k) {
         const int j = (e * kMaxOps + k) * C + c;
-        acc += sw[k] * ((a.z[k][i] - sMean[j]) * sInv[j]);
+        acc += sw[k] * ((z2f(a.z[k][i]) - sMean[j]) * sInv[j]);
       }
       if (a.xid) acc += sw[kMaxOps] * a.xid[i];
     }
@@ -863,7 +890,7 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdBatch
       f4 zv[kMaxOps];
 #pragma unroll
       for (int k = 0; k < kMaxOps; ++k)
-        if (k < a.nops) zv[k] = reinterpret_cast<const f4*>(a.z[k])[b4];
+        if (k < a.nops) zv[k] = zld4(a.z[k] + 4 * b4);
       f4 xv = {0.f, 0.f, 0.f, 0.f};
       if (a.xid) xv = reinterpret_cast<const f4*>(a.xid)[b4];
       s1 += (g.x + g.y) + (g.z + g.w);
@@ -886,7 +913,7 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdBatch
         s1 += g;
 #pragma unroll
         for (int k = 0; k < kMaxOps; ++k)
-          if (k < a.nops) s2[k] += g * (a.z[k][base + i] - sMean[k]) * sInv[k];
+          if (k < a.nops) s2[k] += g * (z2f(a.z[k][base + i]) - sMean[k]) * sInv[k];
         if (a.xid) sid += g * a.xid[base + i];
       }
     }
@@ -928,7 +955,7 @@ __global__ void __launch_bounds__(256) combine_bwd_reduce_kernel(CombineBwdBatch
 // on-the-fly BN backward: dz = wk * invstd * (g - S1/cnt - zhat * S2/cnt)
 __device__ __forceinline__ float bn_bwd_val(const GradSrc& gs, size_t i, float mean, float inv, float wk, float m1,
                                            float m2) {
-  float zh = (gs.z[i] - mean) * inv;
+  float zh = (z2f(gs.z[i]) - mean) * inv;
   float g = gs.g[i];
   return wk * inv * (g - m1 - zh * m2);  // eval: m1 = m2 = 0
 }
@@ -989,7 +1016,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
       int pp = prem + p;
       float v;
       if (a.mode == 0) {
-        v = a.ain[((size_t)n * Cin + ci) * HWo + pp];
+        v = z2f(a.ain[((size_t)n * Cin + ci) * HWo + pp]);
       } else {
         int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
         v = (iy < a.H && ix < a.W) ? fmaxf(a.x[(((size_t)n * Cin + ci) * a.H + iy) * a.W + ix], 0.f) : 0.f;
@@ -1147,19 +1174,19 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
     // 4 consecutive pixels per thread with 16-byte loads/stores (HWo % 4 == 0; mode 0, or
     // mode 1 at stride 1 / offset 0 where the input plane is the output plane)
     typedef float f4 __attribute__((ext_vector_type(4)));
-    const float* src = a.mode == 0 ? a.ain : a.x;
     for (int t = blockIdx.x * 256 + tid; t < total / 4; t += gridDim.x * 256) {
       const int p = t * 4, n = p / HWo, pp = p - n * HWo;
       f4 dz[CO], av[CI];
 #pragma unroll
       for (int c = 0; c < CO; ++c) {
         const size_t gi = ((size_t)n * a.CoutTotal + a.co_off + c) * HWo + pp;
-        const f4 zz = *reinterpret_cast<const f4*>(a.gs.z + gi), gg = *reinterpret_cast<const f4*>(a.gs.g + gi);
+        const f4 zz = zld4(a.gs.z + gi), gg = *reinterpret_cast<const f4*>(a.gs.g + gi);
         dz[c] = wk * inv[c] * (gg - m1[c] - ((zz - mean[c]) * inv[c]) * m2[c]);
       }
 #pragma unroll
       for (int c = 0; c < CI; ++c) {
-        av[c] = *reinterpret_cast<const f4*>(src + ((size_t)n * CI + c) * HWo + pp);
+        const size_t o = ((size_t)n * CI + c) * HWo + pp;
+        av[c] = a.mode == 0 ? zld4(a.ain + o) : *reinterpret_cast<const f4*>(a.x + o);
         if (a.mode != 0) {
           av[c].x = fmaxf(av[c].x, 0.f);
           av[c].y = fmaxf(av[c].y, 0.f);
@@ -1208,7 +1235,7 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
     bool inb = true;
     if (a.mode == 0) {
 #pragma unroll
-      for (int c = 0; c < CI; ++c) av[c] = a.ain[((size_t)n * CI + c) * HWo + pp];
+      for (int c = 0; c < CI; ++c) av[c] = z2f(a.ain[((size_t)n * CI + c) * HWo + pp]);
     } else {
       const int oy = pp / Wo, ox = pp - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
       inb = iy < a.H && ix < a.W;
@@ -1312,7 +1339,6 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
   const bool flat = a.mode == 0 || (a.S == 1 && a.off == 0 && a.H == a.Ho && a.W == a.Wo);
   const bool fr2 = a.mode != 0 && a.S == 2 && a.H == 2 * a.Ho && a.W == 2 * a.Wo && a.W % 4 == 0 && a.off <= 1 &&
                    ((uintptr_t)a.x & 15) == 0;
-  const float* src = a.mode == 0 ? a.ain : a.x;
   float* sT = smem + wave * CO * RS;
   const int ci0 = ((blockIdx.x * 4 + wave) % NS) * BI * 16;  // the wave's input-channel group (fixed: stride % NS == 0)
   f4 macc[BO][BI];
@@ -1329,7 +1355,7 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
       const size_t gi = ((size_t)n * a.CoutTotal + a.co_off + bo * 16 + c16) * HWo + pq;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const f4 zz = *reinterpret_cast<const f4*>(a.gs.z + gi + 4 * t);
+        const f4 zz = zld4(a.gs.z + gi + 4 * t);
         const f4 gg = *reinterpret_cast<const f4*>(a.gs.g + gi + 4 * t);
         const f4 v = wk * inv[bo] * (gg - m1[bo] - ((zz - mean[bo]) * inv[bo]) * m2[bo]);
         dz[bo][4 * t] = v.x;
@@ -1344,10 +1370,10 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
       for (int bi = 0; bi < BI; ++bi) {
         const int ci = ci0 + bi * 16 + c16;
         if (flat) {
-          const float* s = src + ((size_t)n * CI + ci) * HWo + pq;
+          const size_t so = ((size_t)n * CI + ci) * HWo + pq;
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            f4 v = *reinterpret_cast<const f4*>(s + 4 * t);
+            f4 v = a.mode == 0 ? zld4(a.ain + so + 4 * t) : *reinterpret_cast<const f4*>(a.x + so + 4 * t);
             if (a.mode != 0) v = f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
             av[bi][4 * t] = v.x;
             av[bi][4 * t + 1] = v.y;
@@ -1476,7 +1502,7 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int n = t / tiles, oy0 = (t % tiles) * TR;
     const int iy0 = oy0 * S - pad;
-    const float* xin = a.x + (size_t)n * C * H * W;
+    const size_t xin = (size_t)n * C * H * W;
     const float* ddn = a.dd + (size_t)n * C * Ho * Wo;
     for (int c0 = 0; c0 < C; c0 += a.chunk) {
       const int cn = min(a.chunk, C - c0);
@@ -1493,7 +1519,7 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
           int iy = iy0 + rr, ix = -pad + q, c = c0 + cc;
           float v = 0.f;
           if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-            v = xin[((size_t)c * H + iy) * W + ix];
+            v = xval<PREBN>(a.x, xin + ((size_t)c * H + iy) * W + ix);
             if (PREBN) v = (v - sMean[c]) * sInv[c];
             v = fmaxf(v, 0.f);
           }
@@ -1556,7 +1582,7 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
           if (PREBN) {
             float g = 0.f, gy = 0.f;
             if (ok) {
-              float y = (a.x[xi] - sMean[c]) * sInv[c];
+              float y = (xval<true>(a.x, xi) - sMean[c]) * sInv[c];
               g = y > 0.f ? ga : 0.f;
               gy = g * y;
               a.gout[xi] = g;
@@ -1570,7 +1596,7 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
               }
             }
           } else if (ok) {
-            const float gm = a.x[xi] > 0.f ? ga : 0.f;
+            const float gm = xval<false>(a.x, xi) > 0.f ? ga : 0.f;
             if (a.overwrite) a.gout[xi] = gm;
             else if (gm != 0.f) a.gout[xi] += gm;
           }
@@ -1705,7 +1731,7 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
   // staging with 16-byte loads (the band's rows are contiguous per channel; W, Wo % 4 == 0):
   // many wide loads in flight per wave, which the one-row-per-wave scalar loop lacked
   const float* ddn = a.dd + ((size_t)n * a.C + c0) * Ho * Wo;
-  const float* xn = a.x + ((size_t)n * a.C + c0) * H * W;
+  const size_t xn = ((size_t)n * a.C + c0) * H * W;
   const int va = max(oyA, 0), vb = min(oyB, Ho - 1), vrows = vb - va + 1;  // staged dd rows inside [0, Ho)
   {
     const int q4 = vrows * Wo / 4;  // float4s per channel
@@ -1735,7 +1761,7 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
 #pragma unroll 4
     for (int i = tid; i < C * q4; i += 256) {
       const int c = i / q4, o = (i - c * q4) * 4;
-      float4 v = *reinterpret_cast<const float4*>(xn + ((size_t)c * H + iy0) * W + o);
+      float4 v = xval4<PREBN>(a.x, xn + ((size_t)c * H + iy0) * W + o);
       if (PREBN) {
         const float m = sMean[c], iv = sInv[c];
         v.x = (v.x - m) * iv;
@@ -2569,7 +2595,7 @@ static bool try_pw_bwd_px(const PwBwdBatch& b, hipStream_t st) {
   for (int e = 0; e < b.n && v4; ++e) {
     const PwBwdArgs& x = b.e[e];
     const bool m1ok = x.mode == 0 || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);
-    const uintptr_t bits = (uintptr_t)x.gs.z | (uintptr_t)x.gs.g | (uintptr_t)(x.mode == 0 ? x.ain : x.x) |
+    const uintptr_t bits = (uintptr_t)x.gs.z | (uintptr_t)x.gs.g | (x.mode == 0 ? (uintptr_t)x.ain : (uintptr_t)x.x) |
                            (uintptr_t)(x.mode == 0 ? x.dd : x.gx);
     v4 = m1ok && (bits & 15) == 0 && x.co_off % 4 == 0;
   }
@@ -2586,7 +2612,7 @@ static bool try_pw_bwd_wave(const PwBwdBatch& b, hipStream_t st) {
   for (int e = 0; e < b.n; ++e) {  // 16-byte operand loads
     const PwBwdArgs& x = b.e[e];
     const bool flat = x.mode == 0 || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);
-    const uintptr_t bits = (uintptr_t)x.gs.z | (uintptr_t)x.gs.g | (uintptr_t)(flat ? (x.mode == 0 ? x.ain : x.x) : nullptr);
+    const uintptr_t bits = (uintptr_t)x.gs.z | (uintptr_t)x.gs.g | (flat ? (x.mode == 0 ? (uintptr_t)x.ain : (uintptr_t)x.x) : (uintptr_t)0);
     if (bits & 15) return false;
   }
   constexpr int BI = CI / 16;

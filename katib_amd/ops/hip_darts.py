@@ -49,6 +49,10 @@ except ImportError as e:  # pragma: no cover - machines without the build
 
 F64 = torch.float64
 REP = int(_K.REP)
+# storage of the per-op intermediates (depthwise outputs d, pre-BN op outputs z): bf16 in the
+# _hipkern_zbf16 build variant (KATIB_AMD_HIPKERN), fp32 otherwise; node states, gradients, BN
+# statistics and weights stay fp32 either way
+ZDT = torch.bfloat16 if bool(getattr(_K, "ZBF16", False)) else torch.float32
 # FOLD=1 (default): a fold_f64 launch sums the REP replicas of each cross-workgroup reduction
 # before its consumers (which then read rep=1); FOLD=0 (KATIB_HIP_FOLD=0): consumers sum the
 # replicas themselves and the fold launches disappear. Measured on MI355X (B5 step): 13.3 ms
@@ -320,8 +324,8 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
     def st(e, i):
         return stats[(e.slot0 + i) * slot:(e.slot0 + i + 1) * slot] if training else None
 
-    def new():
-        return torch.empty(N, C, Ho, Wo, device=dev)
+    def new():  # a per-op intermediate (d or z)
+        return torch.empty(N, C, Ho, Wo, device=dev, dtype=ZDT)
 
     # ---- stage 1: grouped by (K, dilation, stride, pad)
     dw_groups = defaultdict(list)
@@ -459,7 +463,7 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
     pwd, dd_of = [], {}
     for e, k, prim in dils:
         d, z = e.saved[prim]
-        dd = torch.empty_like(d)
+        dd = torch.empty(d.shape, device=dev)  # gradients stay fp32
         dd_of[(e.i, prim)] = dd
         g, gst = sink(e, prim + ".pw")
         pwd.append((src(e, k, z), e.P[prim + ".pw"], d, e.x, dd, None, g, 0, 0, gst))
@@ -473,10 +477,10 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
         for n, (e, k, prim) in enumerate(seps):
             K = int(prim[-1])
             d1, z1, d2, z2 = e.saved[prim]
-            dd2 = torch.empty_like(d2)
+            dd2 = torch.empty(d2.shape, device=dev)
             g, gst = sink(e, prim + ".1.pw")
             pw2.append((src(e, k, z2), e.P[prim + ".1.pw"], d2, z1, dd2, None, g, 0, 0, gst))
-            g1 = torch.empty_like(z1)
+            g1 = torch.empty(z1.shape, device=dev)
             r1 = red1[n * REP * 2 * C:(n + 1) * REP * 2 * C] if training else None
             g, gst = sink(e, prim + ".1.dw")
             dw2[K].append((z1, e.refs[e.spec.slots[prim][0]], e.P[prim + ".1.dw"], dd2, g1, g, r1, gst, False))
@@ -499,7 +503,7 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
             g1, r1 = e.saved[prim + "/g1"]
             b1 = e.refs[e.spec.slots[prim][0]]
             gs1 = (g1, z1, r1[:C] if training else None, r1[C:2 * C] if training else None, b1, None, 0, _R, 2 * C)
-            dd1 = torch.empty_like(d1)
+            dd1 = torch.empty(d1.shape, device=dev)
             e.saved[prim + "/dd1"] = dd1
             g, gst = sink(e, prim + ".0.pw")
             pw1.append((gs1, e.P[prim + ".0.pw"], d1, e.x, dd1, None, g, 0, 0, gst))
@@ -676,7 +680,7 @@ def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2):
     Ho, Wo = (H // 2, W // 2) if fr else (H, W)
     cnt = N * Ho * Wo
     stats = zeros64(REP * 2 * Cout, x.device) if training else None
-    z = torch.empty(N, Cout, Ho, Wo, device=x.device)
+    z = torch.empty(N, Cout, Ho, Wo, device=x.device, dtype=ZDT)
     if fr:
         _K.pw_fwd([(x, w1, z, stats, 0, 0), (x, w2, z, stats, Cout // 2, 1)], 2)
     else:
@@ -684,7 +688,7 @@ def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2):
     if training:
         _fold64([(stats, 2 * Cout, 2 * Cout)], x.device)
     bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
-    out = torch.empty_like(z)
+    out = torch.empty(z.shape, device=x.device)
     _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], None, None, out, momentum, training, False)
     return out, (x, z, w1, w2, bn, fr, Cout, training)
 
@@ -915,21 +919,22 @@ class _StemConvBN(torch.autograd.Function):
         _K.fold_f64([(stats, 2 * C, 2 * C)])  # always folded: the weight-gradient kernel reads replica 0
         bn = _bn(stats, rm, rv, N * H * W, True, eps, C)
         out = torch.empty_like(z)
-        _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], gamma, beta, out, momentum, True, False)
+        zs = z if ZDT == z.dtype else z.to(ZDT)  # the combine kernels read z in the intermediates' type
+        _K.combine_fwd([([zs], [bn], [0], None, -1, None, [])], gamma, beta, out, momentum, True, False)
         ctx.bn, ctx.eps, ctx.stats = bn, eps, stats
-        ctx.save_for_backward(x, w, gamma, beta, z)
+        ctx.save_for_backward(x, w, gamma, beta, z, zs)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, w, gamma, beta, z = ctx.saved_tensors
+        x, w, gamma, beta, z, zs = ctx.saved_tensors
         bn, eps, stats = ctx.bn, ctx.eps, ctx.stats
         ctx.bn = ctx.stats = None
         dout = dout.contiguous()
         C = w.shape[0]
         nred = 2 * C + 1
         red = zeros64(REP * nred, x.device)
-        _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
+        _K.combine_bwd_reduce([(dout, [zs], [bn], None, red, [0], -1, None)])
         if not _selffold(x.device):
             _K.fold_f64([(red, nred, nred)])
         need = ctx.needs_input_grad
@@ -966,8 +971,9 @@ def stem_bn_eval(z, gamma, beta, rm, rv, eps=1e-5):
     """Inference BatchNorm of the stem output with the running statistics (one combine_fwd)."""
     z = z.contiguous()
     N, C, H, W = z.shape
-    out = torch.empty_like(z)
-    _K.combine_fwd([([z], [_bn(None, rm, rv, N * H * W, False, eps, C)], [0], None, -1, None, [])], gamma, beta, out,
+    out = torch.empty(z.shape, device=z.device)
+    zs = z if z.dtype == ZDT else z.to(ZDT)
+    _K.combine_fwd([([zs], [_bn(None, rm, rv, N * H * W, False, eps, C)], [0], None, -1, None, [])], gamma, beta, out,
                    0.0, False, False)
     return out
 
