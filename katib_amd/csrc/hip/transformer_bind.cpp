@@ -4,6 +4,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include "gemm_bf16.h"
 #include "transformer.h"
 
 namespace py = pybind11;
@@ -207,9 +208,38 @@ void attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& dout, const Tens
      "attn_bwd");
 }
 
+// C[M][N] = A[M][K] . W[N][K]^T (+ bias[N]); G given: C = pre-activation, G = gelu_tanh(C)
+void gemm_nt(const Tensor& A, const Tensor& W, const c10::optional<Tensor>& bias, const Tensor& C,
+             const c10::optional<Tensor>& G) {
+  TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && C.dim() == 2, "gemm_nt: 2-D operands");
+  const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_nt: shapes");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm_nt: dims");
+  TORCH_CHECK(katib_hip::gemm::supported((int)M, (int)N, (int)K), "gemm_nt: M, N % 128 and K % 64 required");
+  chk(A, at::kBFloat16, M * K, "A");
+  chk(W, at::kBFloat16, N * K, "W");
+  chk(C, at::kBFloat16, M * N, "C");
+  const void* bp_ = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    chk(*bias, at::kBFloat16, N, "bias");
+    bp_ = bias->data_ptr();
+  }
+  void* gp = nullptr;
+  if (G.has_value() && G->defined()) {
+    chk(*G, at::kBFloat16, M * N, "G");
+    gp = G->data_ptr();
+  }
+  ok(katib_hip::gemm::launch_nt(A.data_ptr(), W.data_ptr(), bp_, C.data_ptr(), gp, (int)M, (int)N, (int)K, stream()),
+     "gemm_nt");
+}
+
 }  // namespace
 
 void register_transformer(py::module& m) {
+  m.def("gemm_nt", &gemm_nt, "bf16 C = A W^T (+ bias) (+ GELU) on MFMA (gemm_bf16.hip)");
+  m.def("gemm_nt_supported", [](int64_t M, int64_t N, int64_t K) {
+    return M < (1 << 30) && N < (1 << 30) && K < (1 << 30) && katib_hip::gemm::supported((int)M, (int)N, (int)K);
+  });
   m.def("ln_fwd", &ln_fwd, "residual add + LayerNorm forward (fp32 stream, bf16 out)");
   m.def("ln_bwd", &ln_bwd, "LayerNorm backward (+ residual grad), per-block dgamma/dbeta partials");
   m.def("ln_bwd_blocks", &ln_bwd_blocks);

@@ -144,7 +144,7 @@ class GPT2Flat:
 
     # ---------------------------------------------------------------- forward
     def _lin(self, x, name):
-        return torch.addmm(self.w[name + ".bias"], x, self.w[name + ".weight"].t())
+        return self.ops.linear(x, self.w[name + ".weight"], self.w[name + ".bias"])
 
     def _embed(self, idx):
         B, T = idx.shape
@@ -166,14 +166,13 @@ class GPT2Flat:
             o, lse = ops.attn_fwd(qkv, B, T, H, c.d // H)
             a = self._lin(o, pre + "proj")
             sb, h2, mu2, rs2 = ops.ln_fwd(sa, a, self.w[pre + "ln2.weight"], self.w[pre + "ln2.bias"])
-            u = self._lin(h2, pre + "fc")
-            gl = ops.gelu_fwd(u)
+            u, gl = ops.linear_gelu(h2, self.w[pre + "fc.weight"], self.w[pre + "fc.bias"])  # GELU in the epilogue
             pending = self._lin(gl, pre + "fc2")
             resid = sb
             if save:
                 acts.append((sa, h1, mu1, rs1, qkv, o, lse, sb, h2, mu2, rs2, u, gl))
         sf, hf, muf, rsf = ops.ln_fwd(resid, pending, self.w["ln_f.weight"], self.w["ln_f.bias"])
-        logits = torch.mm(hf, self.w["wte.weight"].t())
+        logits = ops.linear(hf, self.w["wte.weight"], None)  # tied LM head
         if save:
             self._saved = (acts, sf, hf, muf, rsf)
         return logits

@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import importlib
 import math
+import os
 
 import torch
 
@@ -121,6 +122,15 @@ class TorchOps:
         return logits
 
     # ---------------------------------------------------------------- GEMM helpers
+    def linear(self, x, w, b):
+        """x [M, K] . w[N, K]^T (+ b)."""
+        return torch.addmm(b, x, w.t()) if b is not None else torch.mm(x, w.t())
+
+    def linear_gelu(self, x, w, b):
+        """(u, gelu_tanh(u)) with u = x . w^T + b."""
+        u = self.linear(x, w, b)
+        return u, self.gelu_fwd(u)
+
     def colsum(self, x, out):
         torch.sum(x, 0, out=out)
 
@@ -151,6 +161,39 @@ class HipOps:
         self.k = _kern()
         self.eps = eps
         self._bmm_f32 = True
+        # forward projections on the hand-written MFMA GEMM (gemm_bf16.hip, bias / GELU fused into the
+        # epilogue) for the shapes where it measured faster than hipBLASLt on MI355X, hipBLASLt
+        # (torch.addmm) for the rest (profiles/gemm_bf16_r03.log: at M = 8192 the 128x128-tile kernel
+        # wins the d x d projection 1.23-1.37x and loses qkv 0.87x, fc + GELU 0.96x, fc2 0.80x, the LM
+        # head 0.61x). KATIB_HIP_GEMM=all: every supported shape (tests), =0: hipBLASLt only.
+        self.gemm = os.environ.get("KATIB_HIP_GEMM", "auto")
+
+    # (N, K) classes where gemm_bf16 beat hipBLASLt in the measured table
+    GEMM_WINS = {(768, 768), (256, 256), (512, 512), (1024, 1024)}
+
+    def _gemm_ok(self, x, w):
+        if self.gemm in ("0", "off") or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or x.dim() != 2:
+            return False
+        if self.gemm != "all" and (w.shape[0], w.shape[1]) not in self.GEMM_WINS:
+            return False
+        return x.is_contiguous() and w.is_contiguous() and bool(self.k.gemm_nt_supported(x.shape[0], w.shape[0],
+                                                                                        x.shape[1]))
+
+    def linear(self, x, w, b):
+        if not self._gemm_ok(x, w):
+            return torch.addmm(b, x, w.t()) if b is not None else torch.mm(x, w.t())
+        c = torch.empty((x.shape[0], w.shape[0]), device=x.device, dtype=torch.bfloat16)
+        self.k.gemm_nt(x, w, b, c, None)
+        return c
+
+    def linear_gelu(self, x, w, b):
+        if not self._gemm_ok(x, w):
+            u = torch.addmm(b, x, w.t())
+            return u, self.gelu_fwd(u)
+        u = torch.empty((x.shape[0], w.shape[0]), device=x.device, dtype=torch.bfloat16)
+        g = torch.empty_like(u)
+        self.k.gemm_nt(x, w, b, u, g)
+        return u, g
 
     def ln_fwd(self, x32, r, gamma, beta):
         M, D = x32.shape
