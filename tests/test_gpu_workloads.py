@@ -101,7 +101,9 @@ def test_pytorchjob_gpu_replicas(tmp_path):
         trials = m.list_trials(e.metadata.name)
         assert EC.is_succeeded(done), [t.status.conditions[-1].message[-2000:] for t in trials]
         mm = {x.name: x for x in done.status.current_optimal_trial.observation.metrics}
-        assert float(mm["loss"].latest) > 0
+        # the loss was collected from the Master's log (printed with 4 decimals: a well-fitted last
+        # batch can read 0.0000, so check it parsed and that the run started from a real loss)
+        assert float(mm["loss"].latest) >= 0 and float(mm["loss"].max) > 0.1
     finally:
         m.shutdown()
 
