@@ -500,58 +500,66 @@ void pw_bwd(std::vector<py::tuple> calls, int64_t S, int64_t mode, bool need_dx)
 }
 
 // (x, inbn|None, dw, dd, gout, gW|None, red|None, gstride, overwrite)
-void dw_bwd_fill(std::vector<py::tuple>& calls, DwBwdBatch& bt, const int64_t* Ks, int64_t dil, int64_t S,
-                 bool& prebn);
+void dw_bwd_fill(std::vector<py::tuple>& calls, DwBwdBatch& bt, const int64_t* Ks, const int64_t* dils,
+                 const int64_t* Ss, bool& prebn);
 
 void dw_bwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, int64_t pad) {
   check_batch<DwBwdBatch>(calls);
   DwBwdBatch bt{};
-  int64_t Ks[DwBwdBatch::kCap];
-  for (int i = 0; i < DwBwdBatch::kCap; ++i) Ks[i] = K;
+  int64_t Ks[DwBwdBatch::kCap], Ds[DwBwdBatch::kCap], Ss[DwBwdBatch::kCap];
+  for (int i = 0; i < DwBwdBatch::kCap; ++i) Ks[i] = K, Ds[i] = dil, Ss[i] = S;
   TORCH_CHECK(pad == (K - 1) / 2 * dil, "dw_bwd padding must be 'same'");
   bool prebn = false;
-  dw_bwd_fill(calls, bt, Ks, dil, S, prebn);
+  dw_bwd_fill(calls, bt, Ks, Ds, Ss, prebn);
   tail_close(bt.tail);
   launch_dw_bwd(bt, K, dil, S, prebn, cur_stream());
 }
 
-// separable second stages of one node, mixed 3x3 / 5x5 (stride 1, input BN, distinct outputs):
-// entries (x, inbn, dw, dd, gout, gW|None, red|None, gstride, overwrite, K); one launch when the
-// plane kernel fits, else one launch per kernel size
+// Depthwise backward entries of mixed kernel size / dilation / stride that write DISTINCT outputs,
+// in one launch: (x, inbn, dw, dd, gout, gW|None, red|None, gstride, overwrite, K[, dil, S]) -
+// a node's separable second stages (input BN), or its stage-1 separable and dilated convolutions
+// each writing its own input-gradient buffer (overwrite). One launch when the plane kernel fits,
+// else one launch per (K, dil, S) group.
 void dw_bwd_multi(std::vector<py::tuple> calls) {
   check_batch<DwBwdBatch>(calls);
   DwBwdBatch bt{};
-  int64_t Ks[DwBwdBatch::kCap];
+  int64_t Ks[DwBwdBatch::kCap], Ds[DwBwdBatch::kCap], Ss[DwBwdBatch::kCap];
   for (size_t i = 0; i < calls.size(); ++i) {
-    TORCH_CHECK(calls[i].size() == 10, "dw_bwd_multi entry: (x, inbn, dw, dd, gout, gW, red, gstride, overwrite, K)");
+    TORCH_CHECK(calls[i].size() == 10 || calls[i].size() == 12,
+                "dw_bwd_multi entry: (x, inbn, dw, dd, gout, gW, red, gstride, overwrite, K[, dil, S])");
     Ks[i] = calls[i][9].cast<int64_t>();
-    TORCH_CHECK(Ks[i] == 3 || Ks[i] == 5, "K in {3, 5}");
+    Ds[i] = calls[i].size() == 12 ? calls[i][10].cast<int64_t>() : 1;
+    Ss[i] = calls[i].size() == 12 ? calls[i][11].cast<int64_t>() : 1;
+    TORCH_CHECK((Ks[i] == 3 || Ks[i] == 5) && (Ds[i] == 1 || Ds[i] == 2) && (Ss[i] == 1 || Ss[i] == 2),
+                "K in {3, 5}, dil and S in {1, 2}");
   }
   bool prebn = false;
-  dw_bwd_fill(calls, bt, Ks, 1, 1, prebn);
-  TORCH_CHECK(prebn, "dw_bwd_multi is the separable second stage (input BN)");
+  dw_bwd_fill(calls, bt, Ks, Ds, Ss, prebn);
   for (int i = 0; i < bt.n; ++i) {
-    bt.e[i].variant = (int)Ks[i];
-    bt.e[i].pad = (int)Ks[i] / 2;
+    TORCH_CHECK(prebn || bt.e[i].overwrite, "dw_bwd_multi: input-gradient entries must own (overwrite) their output");
+    TORCH_CHECK(!prebn || (Ds[i] == 1 && Ss[i] == 1), "dw_bwd_multi: input-BN entries are stride-1 separable stages");
+    bt.e[i].variant = dw_bwd_variant((int)Ks[i], (int)Ds[i], (int)Ss[i], prebn);
   }
+  for (int i = 0; i < bt.n; ++i)  // no ordering between entries: distinct outputs
+    for (int j = i + 1; j < bt.n; ++j) TORCH_CHECK(bt.e[i].gout != bt.e[j].gout, "dw_bwd_multi entries share an output");
   tail_close(bt.tail);
-  if (launch_dw_bwd_stage2_multi(bt, cur_stream())) return;
-  for (int64_t K : {3, 5}) {  // fallback: per kernel size, sharing the counter (sequential launches)
+  if (launch_dw_bwd_multi(bt, cur_stream())) return;
+  for (int v = 0; v < 16; ++v) {  // fallback: per variant, sharing the counter (sequential launches)
     DwBwdBatch one{};
     one.tail = bt.tail;
     for (int i = 0; i < bt.n; ++i)
-      if (Ks[i] == K) one.e[one.n++] = bt.e[i];
-    if (one.n) launch_dw_bwd(one, K, 1, 1, true, cur_stream());
+      if (bt.e[i].variant == v) one.e[one.n++] = bt.e[i];
+    if (one.n) launch_dw_bwd(one, dw_variant_k(v), dw_variant_dil(v), dw_variant_s(v), prebn, cur_stream());
   }
 }
 
-void dw_bwd_fill(std::vector<py::tuple>& calls, DwBwdBatch& bt, const int64_t* Ks, int64_t dil, int64_t S,
-                 bool& prebn) {
+void dw_bwd_fill(std::vector<py::tuple>& calls, DwBwdBatch& bt, const int64_t* Ks, const int64_t* dils,
+                 const int64_t* Ss, bool& prebn) {
   bt.n = calls.size();
   bool has_gw = false;
   for (int i = 0; i < bt.n; ++i) {
     const py::tuple& t = calls[i];
-    const int64_t K = Ks[i], pad = (K - 1) / 2 * dil;
+    const int64_t K = Ks[i], dil = dils[i], S = Ss[i], pad = (K - 1) / 2 * dil;
     Tensor x = t[0].cast<Tensor>();
     auto inbn = t[1].cast<c10::optional<py::tuple>>();
     Tensor dw = t[2].cast<Tensor>(), dd = t[3].cast<Tensor>(), gout = t[4].cast<Tensor>();
@@ -585,7 +593,7 @@ void dw_bwd_fill(std::vector<py::tuple>& calls, DwBwdBatch& bt, const int64_t* K
     const int IR = (TR - 1) * S + (K - 1) * dil + 1, IW = (a.Wo - 1) * S + (K - 1) * dil + 1;
     a.chunk = pick_chunk(a.C, OR * a.Wo + IR * IW, 4 * a.C + (a.gW ? a.C * (int)(K * K) : 0));
     if (prebn) a.inbn = make_bn(*inbn, a.C);
-    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, H); SAME_SHAPE(bt, W);
+    SAME_SHAPE(bt, N); SAME_SHAPE(bt, C); SAME_SHAPE(bt, Ho); SAME_SHAPE(bt, Wo);
   }
   tail_begin(bt.tail);
   if (prebn)
@@ -624,6 +632,17 @@ static void pool_bwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
     if (a.dout_id) TORCH_CHECK(dout_id->sizes() == x.sizes(), "identity gradient shape");
     a.id_idx = id_idx; a.gx = gx.data_ptr<float>();
     a.overwrite = t[8].cast<bool>();
+    if (S_all <= 0 && t.size() > 10) {  // (..., S, extras): other input-gradient parts to sum in
+      auto ex = t[10].cast<std::vector<Tensor>>();
+      TORCH_CHECK(ex.size() <= 4, "pool_bwd: at most 4 extra gradient parts");
+      a.nextra = ex.size();
+      for (size_t j = 0; j < ex.size(); ++j) {
+        check_f32(ex[j], "extra");
+        TORCH_CHECK(ex[j].sizes() == gx.sizes(), "extra gradient part shape");
+        TORCH_CHECK(ex[j].data_ptr() != gx.data_ptr(), "extra part aliases gx");
+        a.extra[j] = ex[j].data_ptr<float>();
+      }
+    }
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, C);
     if (S_all > 0) { SAME_SHAPE(bt, H); SAME_SHAPE(bt, W); }
   }

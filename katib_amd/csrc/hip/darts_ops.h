@@ -121,8 +121,15 @@ struct DwBwdArgs {
   int gstride;  // floats between gW replicas (0: single accumulator); red: kRep replicas of [2C]
   int N, C, H, W, Ho, Wo, pad, chunk;
   int overwrite;  // non-PREBN: gout = masked grad (first writer of this input gradient) instead of +=
-  int variant, nbands, nblk;  // dw_bwd_stage2_multi_kernel: kernel size, row bands, workgroups of this entry
+  int variant, nbands, nblk;  // dw_bwd_plane_multi_kernel: dw_bwd_variant, row bands, workgroups of this entry
 };
+constexpr int dw_bwd_variant(int K, int dil, int S, bool prebn) {
+  return (((K == 5) * 4 + (dil == 2) * 2 + (S == 2)) << 1) | (prebn ? 1 : 0);
+}
+constexpr int dw_variant_k(int v) { return (v >> 3) & 1 ? 5 : 3; }
+constexpr int dw_variant_dil(int v) { return (v >> 2) & 1 ? 2 : 1; }
+constexpr int dw_variant_s(int v) { return (v >> 1) & 1 ? 2 : 1; }
+constexpr bool dw_variant_prebn(int v) { return v & 1; }
 
 struct FoldArgs {  // buf[0][i] = sum_r buf[r][i]; rows 1.. zeroed
   float* buf; int n; int rows;
@@ -136,6 +143,7 @@ struct FoldF64Args {  // per segment: p[i] = sum_{r < kRep} p[r*rstride + i]; re
 struct PoolBwdArgs {
   GradSrc ga; GradSrc gm; const float* x; const float* dout_id; const float* w; int id_idx; float* gx;
   const unsigned char* amax;
+  const float* extra[4]; int nextra;  // other input-gradient parts of this edge summed in (conv backward)
   int overwrite;  // gx = result instead of +=
   int N, C, H, W, Ho, Wo;
   int S;          // pool_bwd_multi_kernel: per-entry stride
@@ -202,8 +210,8 @@ static_assert(sizeof(DwPwFwdBatch) <= 4096 && sizeof(CombineFwdBatch) <= 4096 &&
 
 void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st);
 void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st);
-// separable second stages of mixed kernel size (stride 1, input BN); false: not launched
-bool launch_dw_bwd_stage2_multi(DwBwdBatch b, hipStream_t st);
+// mixed-variant depthwise backward (distinct outputs per entry, variant = dw_bwd_variant); false: not launched
+bool launch_dw_bwd_multi(DwBwdBatch b, hipStream_t st);
 void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st);
 void launch_pool_fwd(const PoolFwdBatch& b, int S, hipStream_t st);
 void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st);

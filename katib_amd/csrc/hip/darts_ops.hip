@@ -1671,6 +1671,9 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
       }
     }
     if (a.dout_id) g += wid * a.dout_id[(size_t)nc * H * W + q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // the node's conv input grads (constant indices: a dynamic index into
+      if (j < a.nextra) g += a.extra[j][(size_t)nc * H * W + q];  // the argument copy sends it to scratch)
     if (a.overwrite) a.gx[(size_t)nc * H * W + q] = g;
     else a.gx[(size_t)nc * H * W + q] += g;
   }
@@ -1897,17 +1900,27 @@ __global__ void __launch_bounds__(256) dw_bwd_plane_kernel(DwBwdBatch bt, int nb
   if (bt.tail.ctr) fold_tail(bt.tail);
 }
 
-// a node's separable second stages (3x3 and 5x5, stride 1, input BN) in one launch: each entry
-// carries its kernel size and band count (a.variant = K, a.nbands, a.nblk); distinct outputs
+// Mixed-variant depthwise backward: one launch for entries of different kernel size / dilation /
+// stride / input BN that write DISTINCT outputs - a node's separable second stages (3x3 and 5x5,
+// input BN), or a node's stage-1 separable and dilated convolutions each writing its own
+// (masked) input-gradient buffer that the pool backward then sums into gx. Each entry carries
+// its variant (dw_bwd_variant), band count and workgroup count.
+#define DWB_CASE(KK, DD, SS, PB) \
+  case dw_bwd_variant(KK, DD, SS, PB): dw_bwd_plane_body<KK, DD, SS, PB, C>(a, blockIdx.x, a.nbands, 0); break;
 template <int C>
-__global__ void __launch_bounds__(256) dw_bwd_stage2_multi_kernel(DwBwdBatch bt) {
+__global__ void __launch_bounds__(256) dw_bwd_plane_multi_kernel(DwBwdBatch bt) {
   const DwBwdArgs a = bt.e[blockIdx.y];  // copy: see dwpw_plane_multi_kernel
   if ((int)blockIdx.x < a.nblk) {
-    if (a.variant == 3) dw_bwd_plane_body<3, 1, 1, true, C>(a, blockIdx.x, a.nbands, 0);
-    else dw_bwd_plane_body<5, 1, 1, true, C>(a, blockIdx.x, a.nbands, 0);
+    switch (a.variant) {
+      DWB_CASE(3, 1, 1, true) DWB_CASE(5, 1, 1, true)
+      DWB_CASE(3, 1, 1, false) DWB_CASE(3, 1, 2, false) DWB_CASE(5, 1, 1, false) DWB_CASE(5, 1, 2, false)
+      DWB_CASE(3, 2, 1, false) DWB_CASE(3, 2, 2, false) DWB_CASE(5, 2, 1, false) DWB_CASE(5, 2, 2, false)
+      default: break;
+    }
   }
   if (bt.tail.ctr) fold_tail(bt.tail);
 }
+#undef DWB_CASE
 
 // ------------------------------------------------------------------------------------------------
 // edge_bwd: the whole input gradient of one edge in one pass (cf. dw_bwd_plane_kernel, whose band
@@ -2467,7 +2480,7 @@ static void launch_dw_bwd_t(const DwBwdBatch& b, bool prebn, hipStream_t st) {
   else hipLaunchKernelGGL((dw_bwd_kernel<K, DIL, S, false>), grid, dim3(256), lds, st, b);
 }
 
-bool launch_dw_bwd_stage2_multi(DwBwdBatch b, hipStream_t st) {
+bool launch_dw_bwd_multi(DwBwdBatch b, hipStream_t st) {
   if (b.n < 1) return true;
   const DwBwdArgs& a0 = b.e[0];
   if (!(a0.C == 4 || a0.C == 8 || (a0.C % 16 == 0 && a0.C <= kMaxC)) || !aligned16(b)) return false;
@@ -2478,20 +2491,24 @@ bool launch_dw_bwd_stage2_multi(DwBwdBatch b, hipStream_t st) {
   size_t lds = 0;
   for (int i = 0; i < b.n; ++i) {
     DwBwdArgs& a = b.e[i];
-    const int K = a.variant;
-    if ((K != 3 && K != 5) || a.C != a0.C || a.H != a.Ho || a.W != a.Wo || a.pad != K / 2 || a.Wo % 4) return false;
+    const int K = dw_variant_k(a.variant), DIL = dw_variant_dil(a.variant), S = dw_variant_s(a.variant);
+    const bool prebn = dw_variant_prebn(a.variant);
+    // the plane kernel's layout (dw_plane_ok) and an overwriting (never accumulating) input BN-free entry
+    if (a.C != a0.C || a.H != a.Ho * S || a.W != a.Wo * S || a.pad != (K - 1) / 2 * DIL || a.Wo % 4 ||
+        (prebn && (DIL != 1 || S != 1)) || (!prebn && !a.overwrite))
+      return false;
     int nb = 1;
     const int G = a.C / C;
     while (nb < 8 && a.H % (2 * nb) == 0 &&
-           (dw_plane_floats(a, K, 1, 1, nb, false, C) * 4 > 40 * 1024 || a.N * nb * G * b.n < 1024))
+           (dw_plane_floats(a, K, DIL, S, nb, false, C) * 4 > 40 * 1024 || a.N * nb * G * b.n < 1024))
       nb *= 2;
     a.nbands = nb;
     a.nblk = a.N * nb * G;
     maxblk = std::max(maxblk, a.nblk);
-    lds = std::max(lds, sizeof(float) * dw_plane_floats(a, K, 1, 1, nb, false, C));
+    lds = std::max(lds, sizeof(float) * dw_plane_floats(a, K, DIL, S, nb, false, C));
   }
-  if (C == 4) hipLaunchKernelGGL(dw_bwd_stage2_multi_kernel<4>, dim3(maxblk, b.n), dim3(256), lds, st, b);
-  else hipLaunchKernelGGL(dw_bwd_stage2_multi_kernel<8>, dim3(maxblk, b.n), dim3(256), lds, st, b);
+  if (C == 4) hipLaunchKernelGGL(dw_bwd_plane_multi_kernel<4>, dim3(maxblk, b.n), dim3(256), lds, st, b);
+  else hipLaunchKernelGGL(dw_bwd_plane_multi_kernel<8>, dim3(maxblk, b.n), dim3(256), lds, st, b);
   return true;
 }
 

@@ -189,6 +189,9 @@ def _launch(name: str, calls: List, *args):
 
 
 MULTI = __import__("os").environ.get("KATIB_HIP_MULTI", "1") != "0"  # mixed-variant launches (A/B switch)
+# a node's stage-1 separable + dilated depthwise backward in one mixed-variant launch, each part in
+# its own buffer, summed into gx by the pool-backward launch (A/B switch KATIB_HIP_DWB_MULTI)
+DWB_MULTI = __import__("os").environ.get("KATIB_HIP_DWB_MULTI", "1") != "0"
 # fused per-edge input gradient (edge_bwd_kernel) instead of per-family dw_bwd / pool_bwd launches.
 # Off by default: measured SLOWER on MI355X (B5 step 9.22 vs 8.05 ms; its 4 conv slots run
 # serially inside each workgroup, and fewer / larger bands only narrow the gap: 8.74 ms at 64 KB
@@ -550,7 +553,33 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
                 first[e.i] = False
         elif len(entries) > 4:  # a partial launch cannot be undone: fail loudly
             raise RuntimeError("edge_bwd accepted part of a node's edges")
-    if not EDGE_BWD or not ok:
+    if (not EDGE_BWD or not ok) and MULTI and DWB_MULTI:
+        # every stage-1 separable and dilated depthwise backward of the node in ONE mixed-variant
+        # launch, each into its own buffer (no read-modify-write of gx, so no ordering between
+        # them); the pool-backward launch then forms gx = pools + identity + those parts, once
+        convs, parts = [], defaultdict(list)
+        for e, k, prim in seps + dils:
+            sep = prim.startswith("separable_convolution")
+            K = int(prim[-1])
+            t = torch.empty_like(e.x)
+            parts[e.i].append(t)
+            name = prim + (".0.dw" if sep else ".dw")
+            g, gst = sink(e, name)
+            dd = e.saved[prim + "/dd1"] if sep else dd_of[(e.i, prim)]
+            convs.append((e.x, None, e.P[name], dd, t, g, None, gst, True, K, 1 if sep else 2, e.S))
+        for i in range(0, len(convs), _CAP["dw_bwd"]):
+            _K.dw_bwd_multi(convs[i:i + _CAP["dw_bwd"]])
+        sums = []
+        for e in edges:
+            ga, gm, am = pool_srcs(e) if "pool" in e.saved else (None, None, None)
+            ex = parts.get(e.i, [])
+            if ga is None and gm is None and e.id_idx < 0 and not ex:
+                continue  # only a stride-2 skip (below) or 'none' writes this edge's gradient
+            sums.append((ga, gm, e.x, dout if e.id_idx >= 0 else None, e.w, e.id_idx, gxs[e.i], am, tf(e.i), e.S, ex))
+            e.id_done = True
+        for i in range(0, len(sums), _CAP["pool_bwd"]):
+            _K.pool_bwd_multi(sums[i:i + _CAP["pool_bwd"]])
+    elif not EDGE_BWD or not ok:
         if seps:
             dw1 = defaultdict(list)
             for e, k, prim in seps:
