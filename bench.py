@@ -224,7 +224,9 @@ def main():
                        "global_batch": bs * comm.world_size, "per_gpu_batch": bs, "seq_len": None,
                        "parallelism": "dp%d" % comm.world_size, "epochs": cfg["epochs"],
                        "steps_per_epoch": steps_per_epoch, "ops": args.ops, "hip_graph": bool(search.capture),
-                       "allreduce": ("xgmi-oneshot" if comm.xgmi is not None else "rccl") if comm.distributed else None,
+                       "allreduce": (("xgmi-oneshot" if comm.xgmi is not None else
+                                      ("rccl" if comm.backend == "nccl" else comm.backend))
+                                     if comm.distributed else None),
                        "second_order": True},
             "ms_valid_batch": round(ms_valid, 4),
             "measured_search_wall_s": round(full_s, 3) if full_s is not None else None,
