@@ -105,6 +105,63 @@ __device__ __forceinline__ void gs_means(const GradSrc& gs, int c, float& m1, fl
   m2 = (float)(s2 * (double)gs.bn.inv_count);
 }
 
+// Workgroup-cooperative replica sums for a kernel prologue (called by EVERY thread; the caller
+// barriers before reading the outputs): channel ch of [0, n) of the pair (p1, p2) summed over
+// `rep` replicas (rs doubles apart) by 16 lanes each - every lane's loads in flight at once and
+// a 4-step shuffle tree, instead of one thread walking all replicas. This is what lets a
+// consumer read unfolded statistics at the latency of one global round trip, so the separate
+// fold launch in front of it can go.
+__device__ __forceinline__ void coop_pair_sums(const double* p1, const double* p2, int rep, int rs, int n,
+                                               double scale, float* o1, float* o2, bool bn, float eps) {
+  const int tid = threadIdx.x, j = tid & 15;
+  for (int cb = 0; cb < n; cb += 16) {
+    const int ch = cb + (tid >> 4);
+    double s = 0.0, s2 = 0.0;
+    if (ch < n) {
+#pragma unroll 2
+      for (int r = j; r < rep; r += 16) {
+        s += p1[(size_t)r * rs + ch];
+        s2 += p2[(size_t)r * rs + ch];
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if (ch < n && j == 0) {
+      if (bn) {  // (sum, sum of squares) -> (mean, 1 / std) as bn_coeffs
+        const double m = s * scale;
+        double v = s2 * scale - m * m;
+        if (v < 0) v = 0;
+        o1[ch] = (float)m;
+        o2[ch] = rsqrtf((float)v + eps);
+      } else {  // BN-backward sums -> means as gs_means
+        o1[ch] = (float)(s * scale);
+        o2[ch] = (float)(s2 * scale);
+      }
+    }
+  }
+}
+
+// BN coefficients of channels [c0, c0 + n) into mean[0..n), inv[0..n) (every thread calls)
+__device__ __forceinline__ void bn_coeffs_coop(const BNRef& b, int c0, int n, float* mean, float* inv) {
+  if (b.eval || b.rep == 1) {
+    for (int c = threadIdx.x; c < n; c += blockDim.x) bn_coeffs(b, c0 + c, mean[c], inv[c]);
+    return;
+  }
+  coop_pair_sums(b.sums + c0, b.sums + b.C + c0, b.rep, b.rstride, n, (double)b.inv_count, mean, inv, true, b.eps);
+}
+
+// BN-backward means of channels [c0, c0 + n) into m1[0..n), m2[0..n) (every thread calls)
+__device__ __forceinline__ void gs_means_coop(const GradSrc& gs, int c0, int n, float* m1, float* m2) {
+  if (gs.eval || gs.rep == 1) {
+    for (int c = threadIdx.x; c < n; c += blockDim.x) gs_means(gs, c0 + c, m1[c], m2[c]);
+    return;
+  }
+  coop_pair_sums(gs.S1 + c0, gs.S2 + c0, gs.rep, gs.rstride, n, (double)gs.bn.inv_count, m1, m2, false, 0.f);
+}
+
 __device__ __forceinline__ int rep_slot() { return blockIdx.x % kRep; }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -376,8 +433,8 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
   float* sIn = smem;  // [C][HP][WP]
   __shared__ float sMean[C], sInv[C], sStat[2 * C];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (PREBN) bn_coeffs_coop(a.inbn, c0, C, sMean, sInv);  // the input BN may arrive unfolded (rep > 1)
   if (tid < C) {
-    if (PREBN) bn_coeffs(a.inbn, c0 + tid, sMean[tid], sInv[tid]);
     sStat[tid] = 0.f;
     sStat[C + tid] = 0.f;
   }
@@ -981,10 +1038,8 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
   float* sM2 = sM1 + Cout;
   float* sW = sM2 + Cout;        // [1]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (int c = tid; c < Cout; c += 256) {
-    bn_coeffs(a.gs.bn, a.co_off + c, sMean[c], sInv[c]);
-    gs_means(a.gs, a.co_off + c, sM1[c], sM2[c]);
-  }
+  for (int c = tid; c < Cout; c += 256) bn_coeffs(a.gs.bn, a.co_off + c, sMean[c], sInv[c]);
+  gs_means_coop(a.gs, a.co_off, Cout, sM1, sM2);
   if (tid == 0) sW[0] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
   __syncthreads();
   const float wk = sW[0];
@@ -1147,10 +1202,8 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
   __shared__ float sC[4 * CO + 1];
   __shared__ float sGW[CI * CO];
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int c = tid; c < CO; c += 256) {
-    bn_coeffs(a.gs.bn, a.co_off + c, sC[c], sC[CO + c]);
-    gs_means(a.gs, a.co_off + c, sC[2 * CO + c], sC[3 * CO + c]);
-  }
+  for (int c = tid; c < CO; c += 256) bn_coeffs(a.gs.bn, a.co_off + c, sC[c], sC[CO + c]);
+  gs_means_coop(a.gs, a.co_off, CO, sC + 2 * CO, sC + 3 * CO);  // the BN-backward sums may arrive unfolded
   if (tid == 0) sC[4 * CO] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
   for (int i = tid; i < CI * CO; i += 256) sGW[i] = 0.f;
   __syncthreads();
@@ -1318,10 +1371,8 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
   __shared__ float sC[4 * CO + 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int c16 = lane & 15, q = lane >> 4;
-  for (int c = tid; c < CO; c += 256) {
-    bn_coeffs(a.gs.bn, a.co_off + c, sC[c], sC[CO + c]);
-    gs_means(a.gs, a.co_off + c, sC[2 * CO + c], sC[3 * CO + c]);
-  }
+  for (int c = tid; c < CO; c += 256) bn_coeffs(a.gs.bn, a.co_off + c, sC[c], sC[CO + c]);
+  gs_means_coop(a.gs, a.co_off, CO, sC + 2 * CO, sC + 3 * CO);
   if (tid == 0) sC[4 * CO] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
   __syncthreads();
   const float wk = sC[4 * CO];

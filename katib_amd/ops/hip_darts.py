@@ -189,6 +189,19 @@ def _launch(name: str, calls: List, *args):
 
 
 MULTI = __import__("os").environ.get("KATIB_HIP_MULTI", "1") != "0"  # mixed-variant launches (A/B switch)
+# Deferred folds: the consumers right after a node's first reduction (the separable second stage's
+# input BN in the forward, the second-stage / dilated pointwise backward after combine_bwd_reduce)
+# sum the 32 replicas themselves in their prologue (workgroup-cooperative, one round trip:
+# darts_ops.hip coop_pair_sums), so those fold launches merge into the node's next fold
+# (KATIB_HIP_DEFER_FOLD=0: fold before every consumer, as before)
+DEFER_FOLD = __import__("os").environ.get("KATIB_HIP_DEFER_FOLD", "1") != "0"
+
+
+def _unfolded(bn):
+    """The BN tuple of :func:`_bn` reading all REP replicas (its stats are not folded yet)."""
+    return bn[:6] + (REP, bn[7])
+
+
 # a node's stage-1 separable + dilated depthwise backward in one mixed-variant launch, each part in
 # its own buffer, summed into gx by the pool-backward launch (A/B switch KATIB_HIP_DWB_MULTI)
 DWB_MULTI = __import__("os").environ.get("KATIB_HIP_DWB_MULTI", "1") != "0"
@@ -389,7 +402,8 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
     _pool_multi([(*c, S) for S, calls in pool_groups.items() for c in calls])
     if fr_calls:
         _launch("pw_fwd", fr_calls, 2)
-    if training and stage1:
+    defer = DEFER_FOLD and training and FOLD and not _selffold(dev)
+    if training and stage1 and not defer:
         _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage1))], dev)
     # ---- separable stage 2 (stride 1, input BN-apply prologue)
     s2_groups = defaultdict(list)
@@ -400,14 +414,15 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
                 sl = e.spec.slots[prim]
                 d1, z1 = e.saved[prim]
                 d2, z2 = new(), new()
-                s2_groups[K].append((z1, e.P[prim + ".1.dw"], e.P[prim + ".1.pw"], e.refs[sl[0]], d2, z2,
-                                     st(e, sl[1])))
+                inbn = _unfolded(e.refs[sl[0]]) if defer else e.refs[sl[0]]
+                s2_groups[K].append((z1, e.P[prim + ".1.dw"], e.P[prim + ".1.pw"], inbn, d2, z2, st(e, sl[1])))
                 e.upd.append(e.refs[sl[0]])
                 e.zs[k], e.bns[k] = z2, e.refs[sl[1]]
                 e.saved[prim] = (d1, z1, d2, z2)
     _dwpw_multi([(*c, K, 1, 1, K // 2) for K, calls in s2_groups.items() for c in calls])
-    if training and stage2:
-        _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage2))], dev)
+    if training and (stage2 or (defer and stage1)):  # (deferred: the stage-1 statistics fold here too)
+        _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C)
+                  for i in sorted(set(stage2 + (stage1 if defer else [])))], dev)
     # ---- weighted sums into the node output
     if out is None:
         out = torch.empty(N, C, Ho, Wo, device=dev)
@@ -451,12 +466,17 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
         calls.append((dout, e.zl, e.bl, e.x if e.id_idx >= 0 else None, e.red, e.widx, e.id_idx, e.gw))
         segs += [(e.red, e.nred, e.nred), (e.gw, e.w.numel(), e.w.numel())]
     _launch("combine_bwd_reduce", calls)
-    if not _selffold(dev):
+    # deferred: the pointwise backward right below sums the replicas itself and this fold joins
+    # the separable second stages' fold (or runs after that pointwise launch)
+    defer = DEFER_FOLD and training and FOLD and not _selffold(dev)
+    if not _selffold(dev) and not defer:
         _K.fold_f64(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
 
-    def src(e, k, z):  # GradSrc of a weighted, BN'd op output
+    def src(e, k, z, rep=_R):  # GradSrc of a weighted, BN'd op output
         j = e.widx.index(k)
-        return (dout, z, e.red[:C], e.red[(1 + j) * C:(2 + j) * C], e.bl[j], e.w, k, _R, e.nred)
+        return (dout, z, e.red[:C], e.red[(1 + j) * C:(2 + j) * C], e.bl[j], e.w, k, rep, e.nred)
+
+    r_early = REP if defer else _R  # replicas the pointwise backward below reads
 
     gxs = [gx_of(e.i) for e in edges]
 
@@ -469,11 +489,13 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
         dd = torch.empty(d.shape, device=dev)  # gradients stay fp32
         dd_of[(e.i, prim)] = dd
         g, gst = sink(e, prim + ".pw")
-        pwd.append((src(e, k, z), e.P[prim + ".pw"], d, e.x, dd, None, g, 0, 0, gst))
+        pwd.append((src(e, k, z, r_early), e.P[prim + ".pw"], d, e.x, dd, None, g, 0, 0, gst))
     # ---- separable convs: both second stages, one fold, both first stages
     seps = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("separable_convolution")]
     if not seps and pwd:
         _launch("pw_bwd", pwd, 1, 0, True)
+    if not seps and defer:
+        _K.fold_f64(segs)
     if seps:
         red1 = zeros64(len(seps) * REP * 2 * C, dev) if training else None
         pw2, dw2 = [], defaultdict(list)
@@ -482,7 +504,7 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
             d1, z1, d2, z2 = e.saved[prim]
             dd2 = torch.empty(d2.shape, device=dev)
             g, gst = sink(e, prim + ".1.pw")
-            pw2.append((src(e, k, z2), e.P[prim + ".1.pw"], d2, z1, dd2, None, g, 0, 0, gst))
+            pw2.append((src(e, k, z2, r_early), e.P[prim + ".1.pw"], d2, z1, dd2, None, g, 0, 0, gst))
             g1 = torch.empty(z1.shape, device=dev)
             r1 = red1[n * REP * 2 * C:(n + 1) * REP * 2 * C] if training else None
             g, gst = sink(e, prim + ".1.dw")
@@ -499,7 +521,8 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
             for K, calls in dw2.items():
                 _launch("dw_bwd", calls, K, 1, 1, K // 2)
         if training:
-            _fold64([(red1[n * REP * 2 * C:(n + 1) * REP * 2 * C], 2 * C, 2 * C) for n in range(len(seps))], dev)
+            _fold64([(red1[n * REP * 2 * C:(n + 1) * REP * 2 * C], 2 * C, 2 * C) for n in range(len(seps))]
+                    + (segs if defer else []), dev)
         pw1 = []
         for e, k, prim in seps:
             d1, z1, d2, z2 = e.saved[prim]
