@@ -831,10 +831,15 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
   float* sInv = sMean + ne * kMaxOps * C;              // [ne][kMaxOps][C]
   float* sW = sInv + ne * kMaxOps * C;                 // [ne][kMaxOps + 1]
   // every (edge, op, channel) coefficient in one pass: one round of statistic loads per block
-  for (int i = threadIdx.x; i < ne * kMaxOps * C; i += 256) {
-    const int e = i / (kMaxOps * C), k = (i / C) % kMaxOps, c = i % C;
-    const CombineFwdArgs& a = bt.e[e];
-    if (k < a.nops) bn_coeffs(a.bn[k], c, sMean[i], sInv[i]);
+  if (ne == 1 && a0.nops == 1 && !a0.bn[0].eval && a0.bn[0].rep > 1) {
+    // a preprocess BN whose statistics arrive unfolded (their fold joins the cell's first node's)
+    bn_coeffs_coop(a0.bn[0], 0, C, sMean, sInv);
+  } else {
+    for (int i = threadIdx.x; i < ne * kMaxOps * C; i += 256) {
+      const int e = i / (kMaxOps * C), k = (i / C) % kMaxOps, c = i % C;
+      const CombineFwdArgs& a = bt.e[e];
+      if (k < a.nops) bn_coeffs(a.bn[k], c, sMean[i], sInv[i]);
+    }
   }
   for (int i = threadIdx.x; i < ne * (kMaxOps + 1); i += 256) {
     const int e = i / (kMaxOps + 1), k = i % (kMaxOps + 1);

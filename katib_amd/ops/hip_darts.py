@@ -311,7 +311,7 @@ class _Edge:
         self.id_done = False
 
 
-def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=None):
+def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=None, extra_fold=()):
     """One node's forward (all kernels of every incoming edge); ``out`` may be a preallocated
     contiguous buffer (the cell writes each node straight into its concat slot). Returns
     (out, edges) - ``edges`` is the state :func:`_node_backward` needs."""
@@ -420,9 +420,9 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
                 e.zs[k], e.bns[k] = z2, e.refs[sl[1]]
                 e.saved[prim] = (d1, z1, d2, z2)
     _dwpw_multi([(*c, K, 1, 1, K // 2) for K, calls in s2_groups.items() for c in calls])
-    if training and (stage2 or (defer and stage1)):  # (deferred: the stage-1 statistics fold here too)
+    if training and (stage2 or (defer and stage1) or extra_fold):  # (deferred: the stage-1 statistics too)
         _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C)
-                  for i in sorted(set(stage2 + (stage1 if defer else [])))], dev)
+                 for i in sorted(set(stage2 + (stage1 if defer else [])))] + list(extra_fold), dev)
     # ---- weighted sums into the node output
     if out is None:
         out = torch.empty(N, C, Ho, Wo, device=dev)
@@ -721,9 +721,12 @@ def mixed_edge(x, w, spec: EdgeSpec, bn: List[Tuple[torch.Tensor, torch.Tensor]]
 
 
 # --------------------------------------------------------------------------------- preprocess
-def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2):
+def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2, defer=None):
     """ReLU -> 1x1 conv (ReLUConvBN, operations.py) or FactorizedReduce (two stride-2 1x1
-    convs on offset grids, channel-concatenated) -> BN(affine=False). Returns (out, state)."""
+    convs on offset grids, channel-concatenated) -> BN(affine=False). Returns (out, state).
+    ``defer`` (a list, inside a cell): the BN statistics are not folded here - the BN-apply reads
+    the replicas itself and the fold segment is appended to ``defer`` for the cell's first node's
+    fold; the backward then reads them folded."""
     x = x.contiguous()
     _selffold(x.device)
     N, Cin, H, W = x.shape
@@ -737,11 +740,15 @@ def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2):
         _K.pw_fwd([(x, w1, z, stats, 0, 0), (x, w2, z, stats, Cout // 2, 1)], 2)
     else:
         _K.pw_fwd([(x, w1, z, stats, 0, 0)], 1)
-    if training:
-        _fold64([(stats, 2 * Cout, 2 * Cout)], x.device)
     bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
+    late = defer is not None and DEFER_FOLD and training and FOLD and not _selffold(x.device)
+    if training and not late:
+        _fold64([(stats, 2 * Cout, 2 * Cout)], x.device)
+    if late:
+        defer.append((stats, 2 * Cout, 2 * Cout))
     out = torch.empty(z.shape, device=x.device)
-    _K.combine_fwd([([z], [bn], [0], None, -1, None, [])], None, None, out, momentum, training, False)
+    _K.combine_fwd([([z], [_unfolded(bn) if late else bn], [0], None, -1, None, [])], None, None, out, momentum,
+                   training, False)
     return out, (x, z, w1, w2, bn, fr, Cout, training)
 
 
@@ -751,10 +758,14 @@ def _stdconv_backward(state, dout, need_x, sinks, keys):
     dout = dout.contiguous()
     nred = 2 * Cout + 1
     red = zeros64(REP * nred, x.device)
+    # deferred: the pointwise backward (its only consumer) sums the replicas in its prologue, and
+    # nothing reads them later, so this fold goes away (the arena is re-zeroed every step)
+    late = DEFER_FOLD and training and FOLD and not _selffold(x.device)
     if training:
         _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
-        _fold64([(red, nred, nred)], x.device)
-    gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0, _R, nred)
+        if not late:
+            _fold64([(red, nred, nred)], x.device)
+    gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0, REP if late else _R, nred)
     g1, s1 = sinks.get(w1, keys[0])
     if fr:  # the two stride-2 grids leave 3 of 4 input pixels untouched: start from zeros
         gx = torch.zeros_like(x) if need_x else None
@@ -814,12 +825,14 @@ class _Cell(torch.autograd.Function):
     def forward(ctx, meta, s0, s1, wts, *params):
         spec, bn_of, training, momentum, eps = meta
         P = dict(zip(spec.names, params))
+        late = []  # preprocess BN statistics folded by the first node's fold
+
         def pre(x, p):
             kind, pnames, bname = p
             rm, rv = bn_of(bname)
             if kind == "fr":
-                return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], P[pnames[1]])
-            return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], None)
+                return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], P[pnames[1]], late)
+            return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], None, late)
         t0, st0 = pre(s0, spec.pre0)
         t1, st1 = pre(s1, spec.pre1)
         states = [t0, t1]
@@ -836,7 +849,8 @@ class _Cell(torch.autograd.Function):
             specs = [es for es, _, _, _, _ in node]
             bns = [[bn_of(b) for b in bnames] for _, _, bnames, _, _ in node]
             plist = [[P[n] for n in pnames] for _, pnames, _, _, _ in node]
-            out, edges = _node_forward(xs, ws, specs, bns, plist, training, momentum, eps, out=O[i])
+            out, edges = _node_forward(xs, ws, specs, bns, plist, training, momentum, eps, out=O[i],
+                                       extra_fold=late if i == 0 else ())
             states.append(out)
             node_states.append(edges)
         y = O.permute(1, 0, 2, 3, 4).reshape(N, nn_ * C, Ho, Wo)
