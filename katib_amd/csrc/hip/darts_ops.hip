@@ -1685,9 +1685,10 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
   if (threadIdx.x < 8) sCo[threadIdx.x] = (threadIdx.x & 1) ? 1.f : 0.f;
   __syncthreads();
   if (threadIdx.x == 0 && a.ga.z) bn_coeffs(a.ga.bn, c, sCo[0], sCo[1]);
-  if (threadIdx.x == 64 && a.ga.z) gs_means(a.ga, c, sCo[2], sCo[3]);
   if (threadIdx.x == 128 && a.gm.z) bn_coeffs(a.gm.bn, c, sCo[4], sCo[5]);
-  if (threadIdx.x == 192 && a.gm.z) gs_means(a.gm, c, sCo[6], sCo[7]);
+  // BN-backward means: the reductions may arrive unfolded (workgroup-cooperative replica sums)
+  if (a.ga.z) gs_means_coop(a.ga, c, 1, sCo + 2, sCo + 3);
+  if (a.gm.z) gs_means_coop(a.gm, c, 1, sCo + 6, sCo + 7);
   __syncthreads();
   const float ma = sCo[0], ia = sCo[1], a1 = a.ga.z ? sCo[2] : 0.f, a2 = a.ga.z ? sCo[3] : 0.f;
   const float mm = sCo[4], im = sCo[5], m1 = a.gm.z ? sCo[6] : 0.f, m2 = a.gm.z ? sCo[7] : 0.f;

@@ -437,7 +437,7 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
     return out, edges
 
 
-def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
+def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey, cell_gw=None):
     """One node's backward. ``gx_of(i)`` is the input-gradient buffer of edge i (edges of
     different nodes that read the same state share one buffer); ``take_first(i)`` is True for
     the first kernel that writes it (it overwrites instead of accumulating, so no memset);
@@ -469,14 +469,20 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
     # deferred: the pointwise backward right below sums the replicas itself and this fold joins
     # the separable second stages' fold (or runs after that pointwise launch)
     defer = DEFER_FOLD and training and FOLD and not _selffold(dev)
+    # inside a cell every reader of this node's reductions sums the replicas itself, so the node
+    # folds nothing: the d(alpha) segments go to the cell, which folds them once (if it needs them)
+    nofold = defer and cell_gw is not None and not EDGE_BWD
+    if nofold:
+        cell_gw.extend(segs[1::2])
     if not _selffold(dev) and not defer:
         _K.fold_f64(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
 
-    def src(e, k, z, rep=_R):  # GradSrc of a weighted, BN'd op output
+    r_early = REP if defer else _R  # replicas the pointwise backward below reads
+    r_late = REP if nofold else _R  # ... and the pool / stride-2 skip backward further down
+
+    def src(e, k, z, rep=r_late):  # GradSrc of a weighted, BN'd op output
         j = e.widx.index(k)
         return (dout, z, e.red[:C], e.red[(1 + j) * C:(2 + j) * C], e.bl[j], e.w, k, rep, e.nred)
-
-    r_early = REP if defer else _R  # replicas the pointwise backward below reads
 
     gxs = [gx_of(e.i) for e in edges]
 
@@ -494,7 +500,7 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
     seps = [(e, k, p) for e in edges for k, p in enumerate(e.spec.prims) if p.startswith("separable_convolution")]
     if not seps and pwd:
         _launch("pw_bwd", pwd, 1, 0, True)
-    if not seps and defer:
+    if not seps and defer and not nofold:
         _K.fold_f64(segs)
     if seps:
         red1 = zeros64(len(seps) * REP * 2 * C, dev) if training else None
@@ -520,7 +526,7 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
         else:
             for K, calls in dw2.items():
                 _launch("dw_bwd", calls, K, 1, 1, K // 2)
-        if training:
+        if training and not nofold:
             _fold64([(red1[n * REP * 2 * C:(n + 1) * REP * 2 * C], 2 * C, 2 * C) for n in range(len(seps))]
                     + (segs if defer else []), dev)
         pw1 = []
@@ -528,7 +534,7 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey):
             d1, z1, d2, z2 = e.saved[prim]
             g1, r1 = e.saved[prim + "/g1"]
             b1 = e.refs[e.spec.slots[prim][0]]
-            gs1 = (g1, z1, r1[:C] if training else None, r1[C:2 * C] if training else None, b1, None, 0, _R, 2 * C)
+            gs1 = (g1, z1, r1[:C] if training else None, r1[C:2 * C] if training else None, b1, None, 0, r_late, 2 * C)
             dd1 = torch.empty(d1.shape, device=dev)
             e.saved[prim + "/dd1"] = dd1
             g, gst = sink(e, prim + ".0.pw")
@@ -874,6 +880,7 @@ class _Cell(torch.autograd.Function):
         sinks = _Sinks()
         want_ga = ctx.needs_input_grad[3]
         ga_rows = [None] * nn_
+        cell_gw = []  # the nodes' unfolded d(alpha) replicas
         for i in reversed(range(nn_)):
             node = spec.nodes[i]
             edges = node_states[i]
@@ -888,7 +895,7 @@ class _Cell(torch.autograd.Function):
                 return f
 
             _node_backward(edges, training, C, gS[2 + i], lambda k, srcs=srcs: gS[srcs[k]], take_first, sinks,
-                           lambda e, name, node=node: 4 + spec.index[node[e.i][1][e.spec.pidx[name]]])
+                           lambda e, name, node=node: 4 + spec.index[node[e.i][1][e.spec.pidx[name]]], cell_gw)
             if want_ga:  # a node's alpha rows are consecutive, nodes in row order
                 ga_rows[i] = [e.gw[:wshape[1]] for e in edges]
         for j in (0, 1):
@@ -900,6 +907,8 @@ class _Cell(torch.autograd.Function):
         gs1 = _stdconv_backward(st1, gS[1], need[2], sinks, _pre_keys(spec, spec.pre1))
         grads[1], grads[2] = gs0, gs1
         if want_ga:
+            if cell_gw:
+                _K.fold_f64(cell_gw)
             grads[3] = torch.cat([g for rows in ga_rows for g in rows]).view(wshape).to(torch.float32)
         sinks.finish(grads)
         return tuple(grads)
