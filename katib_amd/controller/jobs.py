@@ -36,9 +36,11 @@ the shape of the corresponding Kubernetes status (``status.conditions[]``).
 
 from __future__ import annotations
 
+import collections
 import json
 import os
 import socket
+import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -133,10 +135,26 @@ def _argv(c: Dict) -> List[str]:
     return [str(a) for a in cmd]
 
 
+_RECENT_PORTS: "collections.deque" = collections.deque(maxlen=512)
+_PORT_LOCK = threading.Lock()
+
+
 def free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """An ephemeral TCP port for a trial's rendezvous / Prometheus endpoint. The port is free
+    when probed but only bound later by the trial, so two launches racing for the same number
+    are possible in principle; within this scheduler a port handed out recently (the last 512)
+    is never handed out again, which removes the race between concurrent trials. A clash with
+    an unrelated process binding the port in between surfaces as the trial's bind error (its
+    retry gets a new port)."""
+    with _PORT_LOCK:
+        for _ in range(64):
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            if port not in _RECENT_PORTS:
+                break
+        _RECENT_PORTS.append(port)
+        return port
 
 
 LAUNCH_MODES = ("ranks", "single")

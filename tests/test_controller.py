@@ -534,3 +534,27 @@ def test_prometheus_exposition_parser():
     assert first == [("1970-01-01T00:00:00Z", "acc", "1")]
     assert sc.observe("acc 1\n", 1.0) == [] and sc.observe("acc 2\n", 1.5)[0][2] == "2"
     assert sc.observe("acc 2 1700000000250\n", 2.0) == [("2023-11-14T22:13:20.25Z", "acc", "2")]
+
+
+def test_free_port_never_repeats_recent_ports():
+    """Concurrent trial launches get distinct rendezvous / Prometheus ports (the
+    port is probed before the trial binds it, so two launches must not be handed the same one)."""
+    import threading
+
+    from katib_amd.controller.jobs import free_port
+
+    got = []
+    lock = threading.Lock()
+
+    def take():
+        for _ in range(25):
+            p = free_port()
+            with lock:
+                got.append(p)
+
+    ts = [threading.Thread(target=take) for _ in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert len(got) == 200 and len(set(got)) == 200
