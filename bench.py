@@ -18,7 +18,7 @@ labelled as such).
 
 The same JSON line also carries
 * ``trials_per_hour``: BASELINE config 2 end to end through the scheduler (TPE over the
-  MNIST MLP, one trial per GPU at a time over all N GPUs, warm workers), run by rank 0
+  MNIST MLP, ``--trial-slots`` trials per GPU at a time over all N GPUs, warm workers), run by rank 0
   in a child process *before* any rank touches the GPU (``bench_trials.py``);
 * ``torch_eager_ms_per_step``: the same search step on the PyTorch op backend launched
   eagerly (MIOpen / hipBLASLt / PyTorch kernels, no HIP graph), a same-node comparator.
@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128, help="global batch (strong) / per-GPU batch (weak)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--trials", type=int, default=3, help="trials per GPU of the trials/hour experiment (0: skip)")
+    ap.add_argument("--trial-slots", type=int, default=1,
+                    help="concurrent trials per GPU in the trials/hour experiment (warm workers per GPU)")
     ap.add_argument("--comparator-steps", type=int, default=5, help="torch-eager comparator steps (0: skip)")
     ap.add_argument("--capture", type=int, default=1)
     ap.add_argument("--ops", default=os.environ.get("KATIB_AMD_DARTS_OPS", "hip"))
@@ -83,7 +85,7 @@ def main():
     # the scheduler's warm workers then own every GPU while the experiment runs
     tph = None
     if args.trials > 0 and int(os.environ.get("RANK", "0")) == 0:
-        tph = trials_per_hour(args.gpus, args.trials)
+        tph = trials_per_hour(args.gpus, args.trials, args.trial_slots)
 
     import torch
 
@@ -241,7 +243,7 @@ def main():
     comm.destroy()
 
 
-def trials_per_hour(gpus: int, per_gpu: int):
+def trials_per_hour(gpus: int, per_gpu: int, slots: int = 1):
     """BASELINE config 2 (TPE over the MNIST MLP, examples/hp-tuning/tpe-mnist-mlp.yaml) end to
     end through the in-process scheduler: parallelTrialCount = one trial per GPU,
     ``per_gpu`` trials per GPU, 3 epochs of 60k rows each. Completed trials per hour of wall
@@ -251,7 +253,7 @@ def trials_per_hour(gpus: int, per_gpu: int):
     trial program (the reference's MXNet MLP image is not in the reference tree)."""
     here = os.path.dirname(os.path.abspath(__file__))
     cmd = [sys.executable, os.path.join(here, "bench_trials.py"), "--trials", str(per_gpu * gpus), "--parallel",
-           str(gpus), "--gpus", str(gpus), "--slots-per-gpu", "1", "--epochs", "3"]
+           str(gpus * slots), "--gpus", str(gpus), "--slots-per-gpu", str(slots), "--epochs", "3"]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -265,8 +267,8 @@ def trials_per_hour(gpus: int, per_gpu: int):
     return {"value": res["value"], "unit": "trials/h", "n_gpus": gpus, "vs_b1": res["vs_baseline"],
             "wall_s": res["wall_s"], "trials_completed": res["trials_completed"],
             "trials_succeeded": res["trials_succeeded"], "best_validation_accuracy": res["best_validation_accuracy"],
-            "config": "tpe-mnist-mlp: %d trials, parallel %d (1 per GPU), 3 epochs x 60k, warm workers"
-                      % (res["trials_completed"], gpus), "b1_trials_per_hour": 36.3}
+            "config": "tpe-mnist-mlp: %d trials, parallel %d (%d per GPU), 3 epochs x 60k, warm workers"
+                      % (res["trials_completed"], gpus * slots, slots), "b1_trials_per_hour": 36.3}
 
 
 if __name__ == "__main__":
