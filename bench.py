@@ -71,7 +71,23 @@ def main():
     ap.add_argument("--full-search", type=int, default=-1,
                     help="also run the whole search (epochs x (steps/epoch train steps + validation)) and report "
                          "its measured wall clock next to the projection (-1: on for the b5 config)")
+    ap.add_argument("--floor", type=int, default=1,
+                    help="N>1: rank 0 also times a dp1 step at the per-rank batch (per_rank_floor_ms)")
+    ap.add_argument("--sync-bn", type=int, default=-1,
+                    help="BatchNorm statistics over the global batch (all ranks) instead of per rank; "
+                         "-1: on for strong scaling (keeps B5's BN over 128 images at every N)")
     args = ap.parse_args()
+    if args.sync_bn < 0:
+        args.sync_bn = 1 if args.scaling == "strong" else 0
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: become N ranks, one per GPU, before anything touches the GPU
+        return self_launch(args.gpus)
+    ws_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws_env != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d; refusing to time a different world size"
+              % (ws_env, args.gpus), file=sys.stderr)
+        return 2
 
     if args.dtype == "bf16" and not os.environ.get("KATIB_AMD_HIPKERN"):
         # the variant extension replaces the fp32 one module-wide: rerun in a child that loads it
@@ -113,7 +129,8 @@ def main():
     cfg = CONFIGS[args.config]
     layout = DartsLayout(PRIMS, init_channels=cfg["init_channels"], num_layers=cfg["num_layers"],
                          num_nodes=cfg["num_nodes"], stem_multiplier=cfg["stem_multiplier"])
-    search = DartsSearch(layout, dev, comm, capture=bool(args.capture) and dev.type == "cuda")
+    sync_bn = bool(args.sync_bn) and comm.distributed
+    search = DartsSearch(layout, dev, comm, capture=bool(args.capture) and dev.type == "cuda", sync_bn=sync_bn)
     n_train = 50000
     ds = cifar10(dev, n=n_train)
     train, valid = ds.subset(0, n_train // 2), ds.subset(n_train // 2, n_train)
@@ -184,6 +201,26 @@ def main():
         sync()
         full_s = comm.allreduce_max(time.perf_counter() - t2)
 
+    # per-rank floor: what one rank's step costs on its own at the per-rank batch (dp1, rank 0's
+    # GPU, the other ranks parked at the barrier) - the best an N-rank step could do without the
+    # all-reduces and BN synchronisation
+    floor_ms = None
+    if comm.distributed and args.floor and dev.type == "cuda":
+        if comm.rank == 0:
+            solo = DartsSearch(layout, dev, Comm(device=dev), capture=bool(args.capture))
+            for i in range(max(args.warmup, 2)):
+                (tx, ty), (vx, vy) = batches[i % len(batches)]
+                solo.step(tx, ty, vx, vy)
+            sync()
+            t4 = time.perf_counter()
+            for i in range(args.steps):
+                (tx, ty), (vx, vy) = batches[i % len(batches)]
+                solo.step(tx, ty, vx, vy)
+            sync()
+            floor_ms = (time.perf_counter() - t4) * 1000.0 / args.steps
+            del solo
+        comm.barrier()
+
     # same-node comparator: the PyTorch op backend, eager (no graph), same config and batch
     torch_ms = None
     if args.comparator_steps > 0 and dev.type == "cuda" and args.dtype == "fp32":
@@ -204,12 +241,15 @@ def main():
         sync()
         torch_ms = comm.allreduce_max((time.perf_counter() - t3) * 1000.0 / args.comparator_steps)
         dops.set_backend(args.ops)
+    allreduce = (("xgmi-oneshot" if comm.xgmi is not None else ("rccl" if comm.backend == "nccl" else comm.backend))
+                 if comm.distributed else None)
     if comm.rank == 0:
         out = {
             "metric": "darts_cifar10_search_wall_clock_s",
             "value": round(wall, 3),
             "unit": "s",
-            "n_gpus": comm.world_size,
+            "n_gpus": args.gpus,
+            "ranks_seen": comm.world_size,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
@@ -226,10 +266,12 @@ def main():
                        "global_batch": bs * comm.world_size, "per_gpu_batch": bs, "seq_len": None,
                        "parallelism": "dp%d" % comm.world_size, "epochs": cfg["epochs"],
                        "steps_per_epoch": steps_per_epoch, "ops": args.ops, "hip_graph": bool(search.capture),
-                       "allreduce": (("xgmi-oneshot" if comm.xgmi is not None else
-                                      ("rccl" if comm.backend == "nccl" else comm.backend))
-                                     if comm.distributed else None),
+                       "allreduce": allreduce, "sync_bn": sync_bn,
                        "second_order": True},
+            "allreduce": allreduce,
+            "batchnorm": ("global batch (sync-bn)" if sync_bn else
+                          ("per rank" if comm.distributed else "global batch")),
+            "per_rank_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,
             "ms_valid_batch": round(ms_valid, 4),
             "measured_search_wall_s": round(full_s, 3) if full_s is not None else None,
             "train_images_per_s": round(bs * comm.world_size * 1000.0 / ms_step, 1),
@@ -241,6 +283,28 @@ def main():
         }
         print(json.dumps(out), flush=True)
     comm.destroy()
+
+
+def self_launch(n: int) -> int:
+    """Run this same command as ``n`` ranks under ``torch.distributed.run`` (a CHILD process:
+    this one never touches the GPU, so nothing is exec'd after GPU init) and relay rank 0's JSON
+    line. The driver's form (torchrun around bench.py) skips this: WORLD_SIZE is then set."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from katib_amd.controller.jobs import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    for ln in r.stdout.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if r.returncode != 0 or len(lines) != 1:
+        print("bench.py: %d-rank run failed (rc %d, %d JSON lines)" % (n, r.returncode, len(lines)), file=sys.stderr)
+        return r.returncode or 1
+    print(lines[0], flush=True)
+    return 0
 
 
 def trials_per_hour(gpus: int, per_gpu: int, slots: int = 1):

@@ -29,6 +29,24 @@ def _newer(target: str, sources) -> bool:
     return any(os.path.getmtime(s) > t for s in sources)
 
 
+def _local_includes(src: str, root: str, seen=None):
+    """Headers of ``root`` that ``src`` includes with ``#include "..."``, transitively: a
+    translation unit is recompiled only when one of ITS headers changes."""
+    seen = set() if seen is None else seen
+    try:
+        lines = open(src, errors="replace").read().splitlines()
+    except OSError:
+        return seen
+    for ln in lines:
+        ln = ln.strip()
+        if ln.startswith("#include") and '"' in ln:
+            h = os.path.join(root, ln.split('"')[1])
+            if os.path.exists(h) and h not in seen:
+                seen.add(h)
+                _local_includes(h, root, seen)
+    return seen
+
+
 def native_target() -> str:
     return os.path.join(PKG_DIR, "_native" + EXT_SUFFIX)
 
@@ -109,11 +127,10 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", 
               "-fno-gpu-rdc", "-Wno-unused-result", "-Wno-deprecated-declarations"] + ["-D" + d for d in defines]
     inc = [f"-I{p}" for p in torch_inc + [py_inc, HIP_SRC]]
     objs, cmds = [], []
-    headers = sorted(glob.glob(os.path.join(HIP_SRC, "*.h")))
     for s in srcs:
         o = os.path.join(build_dir, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer(o, [s] + headers):
+        if force or _newer(o, [s] + sorted(_local_includes(s, HIP_SRC))):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
             cmds.append([hipcc] + common + inc + lang + ["-c", s, "-o", o])
     # One hipcc per translation unit, run concurrently (bounded by MAX_JOBS / CPU count).

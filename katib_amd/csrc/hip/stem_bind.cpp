@@ -76,8 +76,9 @@ void fwd_stats(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& 
 // weight gradient through the affine BN backward (dy = gradient of the BN output)
 void wgrad_bn(const Tensor& x, const Tensor& dy, const Tensor& z, const Tensor& red, const Tensor& stats,
               const Tensor& gamma, double eps, std::optional<Tensor> dgamma, std::optional<Tensor> dbeta,
-              const Tensor& partial, const Tensor& dw) {
+              const Tensor& partial, const Tensor& dw, int64_t world) {
   check_shapes(x, dw);
+  TORCH_CHECK(world >= 1, "stem: world must be >= 1");
   chk(dy, "dy");
   chk(z, "z");
   chk(partial, "partial");
@@ -97,7 +98,9 @@ void wgrad_bn(const Tensor& x, const Tensor& dy, const Tensor& z, const Tensor& 
   bn.red = red.data_ptr<double>();
   bn.stats = stats.data_ptr<double>();
   bn.gamma = gamma.data_ptr<float>();
-  bn.inv_count = static_cast<float>(1.0 / ((double)N * H * W));
+  // SyncBN (world > 1): stats / red are sums over every rank's batch
+  bn.inv_count = static_cast<float>(1.0 / ((double)N * H * W * world));
+  bn.red_scale = static_cast<float>(1.0 / world);
   bn.eps = static_cast<float>(eps);
   if (dgamma) {
     chk(*dgamma, "dgamma");
@@ -119,7 +122,9 @@ void wgrad_bn(const Tensor& x, const Tensor& dy, const Tensor& z, const Tensor& 
 
 void register_stem(py::module& m) {
   m.def("stem_conv_fwd_stats", &fwd_stats, "stem conv forward + BN statistics into kRep fp64 replicas");
-  m.def("stem_conv_wgrad_bn", &wgrad_bn, "stem conv weight gradient through the affine BN backward");
+  m.def("stem_conv_wgrad_bn", &wgrad_bn, "stem conv weight gradient through the affine BN backward",
+        py::arg("x"), py::arg("dy"), py::arg("z"), py::arg("red"), py::arg("stats"), py::arg("gamma"), py::arg("eps"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("partial"), py::arg("dw"), py::arg("world") = 1);
   m.def("stem_conv_fwd", &fwd, "direct 3x3 stem conv forward (fp32 NCHW)");
   m.def("stem_conv_wgrad", &wgrad, "stem conv weight gradient (chunk partials + fixed-order sum)");
 }

@@ -35,6 +35,7 @@ struct BnBwd {
   float eps;
   float* dgamma;         // nullable
   float* dbeta;          // nullable
+  float red_scale;       // 1, or 1 / world under SyncBN (red then sums every rank's dy: d gamma / d beta stay per rank)
 };
 void launch_wgrad_bn(const float* x, const float* dy, const BnBwd& bn, float* partial, float* dw, int N, int Cin,
                      int Cout, int H, int W, int chunks, hipStream_t s);

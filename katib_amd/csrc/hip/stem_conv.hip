@@ -130,8 +130,8 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const float* __res
     m1 = (float)(bn.red[co] * (double)bn.inv_count);
     m2 = (float)(bn.red[Cout + co] * (double)bn.inv_count);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-      if (bn.dgamma) bn.dgamma[co] += (float)bn.red[Cout + co];
-      if (bn.dbeta) bn.dbeta[co] += (float)bn.red[co];
+      if (bn.dgamma) bn.dgamma[co] += (float)(bn.red[Cout + co] * (double)bn.red_scale);
+      if (bn.dbeta) bn.dbeta[co] += (float)(bn.red[co] * (double)bn.red_scale);
     }
   }
   float acc[K];

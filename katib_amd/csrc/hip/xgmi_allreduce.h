@@ -4,6 +4,8 @@
 
 #include <cstdint>
 
+#include "darts_ops.h"  // FoldF64Args (SyncBN: fold + cross-rank sum of the DARTS BN reductions)
+
 namespace katib_hip {
 namespace xgmi {
 
@@ -28,6 +30,12 @@ struct AllReduceArgs {
 };
 
 hipError_t launch_oneshot(const AllReduceArgs& a, int blocks, bool vec4, hipStream_t stream);
+// SyncBN for the DARTS supernet: fold the kRep replicas of every segment (as fold_f64) and, for
+// the segments whose bit is set in sync_mask (BN statistics / BN-backward sums), also sum the folded
+// values over the ranks in rank order (fp64, identical bits on every rank); the other segments
+// (d alpha) stay local. a.in / a.out / a.n / a.scale are unused; staging holds cap / 2 doubles.
+hipError_t launch_fold_sync(const AllReduceArgs& a, const FoldF64Args& f, uint64_t sync_mask, int blocks,
+                            hipStream_t stream);
 
 }  // namespace xgmi
 }  // namespace katib_hip

@@ -128,7 +128,77 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(AllReduceArgs a) {
   if (tid == 0) st_sys(mysig + kSigEpoch + b, e);
 }
 
+// fold + cross-rank sum of f64 segments (SyncBN), same hand-off protocol as oneshot_kernel
+__global__ __launch_bounds__(kThreads) void fold_sync_kernel(AllReduceArgs a, FoldF64Args f, uint64_t mask) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  uint32_t* mysig = a.sig[a.rank];
+  __shared__ uint32_t s_e;
+  if (tid == 0) s_e = ld_sys(mysig + kSigEpoch + b) + 1u;
+  __syncthreads();
+  const uint32_t e = s_e;
+  const int64_t half = (int64_t)(e & 1u) * (a.cap / 2);  // in doubles
+  const int per = (f.total + nb - 1) / nb;
+  const int lo = min(f.total, b * per), hi = min(f.total, lo + per);
+  double* mine = reinterpret_cast<double*>(a.buf[a.rank]) + half;
+
+  // 1. fold my slice: local segments are final, synchronised ones are published
+  for (int g = lo + tid; g < hi; g += kThreads) {
+    int seg = 0, i = g;
+    while (seg < f.nseg - 1 && i >= f.n[seg]) i -= f.n[seg++];
+    double* p = f.p[seg] + i;
+    const int rs = f.rstride[seg];
+    double v[kRep];
+#pragma unroll
+    for (int r = 0; r < kRep; ++r) v[r] = p[(size_t)r * rs];
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < kRep; ++r) acc += v[r];
+#pragma unroll
+    for (int r = 1; r < kRep; ++r) p[(size_t)r * rs] = 0.0;
+    if ((mask >> seg) & 1ull) mine[g] = acc;
+    else p[0] = acc;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // write L2 back: peers read over xGMI
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int p = 0; p < a.world; ++p)
+      if (p != a.rank) st_sys(a.sig[p] + b * kMaxRanks + a.rank, e);
+  }
+  // 2. wait for every peer's block b (bounded)
+  if (tid < a.world && tid != a.rank) {
+    const uint32_t* fl = mysig + b * kMaxRanks + tid;
+    const uint64_t t0 = wall_clock64();
+    while (ld_sys(fl) < e) {
+      if (wall_clock64() - t0 > a.timeout_ticks) {
+        st_sys(mysig + kSigErr, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // 3. synchronised segments: sum in rank order into replica 0
+  for (int g = lo + tid; g < hi; g += kThreads) {
+    int seg = 0, i = g;
+    while (seg < f.nseg - 1 && i >= f.n[seg]) i -= f.n[seg++];
+    if (!((mask >> seg) & 1ull)) continue;
+    double acc = reinterpret_cast<const double*>(a.buf[0])[half + g];
+    for (int p = 1; p < a.world; ++p) acc += reinterpret_cast<const double*>(a.buf[p])[half + g];
+    f.p[seg][i] = acc;
+  }
+  if (tid == 0) st_sys(mysig + kSigEpoch + b, e);
+}
+
 }  // namespace
+
+hipError_t launch_fold_sync(const AllReduceArgs& a, const FoldF64Args& f, uint64_t sync_mask, int blocks,
+                            hipStream_t stream) {
+  hipLaunchKernelGGL(fold_sync_kernel, dim3(blocks), dim3(kThreads), 0, stream, a, f, sync_mask);
+  return hipGetLastError();
+}
 
 hipError_t launch_oneshot(const AllReduceArgs& a, int blocks, bool vec4, hipStream_t stream) {
   if (vec4)

@@ -122,6 +122,31 @@ class XgmiWorkspace {
     XG_CHECK(launch_oneshot(a, blocks_, vec4, c10::hip::getCurrentHIPStream(device_).stream()));
   }
 
+  // SyncBN: fold_f64 segments (f64 tensor holding kRep replicas, n, rstride[, sync]); segments with
+  // sync (default true) are also summed over the ranks
+  void fold_sync(std::vector<py::tuple> segs) {
+    TORCH_CHECK(world_ > 0, "workspace not opened");
+    TORCH_CHECK(!segs.empty() && (int)segs.size() <= katib_hip::kMaxSeg, "1..kMaxSeg segments");
+    katib_hip::FoldF64Args f{};
+    uint64_t mask = 0;
+    f.nseg = segs.size();
+    for (int k = 0; k < f.nseg; ++k) {
+      at::Tensor t = segs[k][0].cast<at::Tensor>();
+      const int n = segs[k][1].cast<int>(), rs = segs[k][2].cast<int>();
+      TORCH_CHECK(t.is_cuda() && t.get_device() == device_ && t.scalar_type() == at::kDouble && t.is_contiguous(),
+                  "fold segment must be a contiguous f64 tensor on the workspace's device");
+      TORCH_CHECK(n >= 1 && rs >= n && t.numel() >= (int64_t)(katib_hip::kRep - 1) * rs + n, "fold segment size");
+      f.p[k] = t.data_ptr<double>();
+      f.n[k] = n;
+      f.rstride[k] = rs;
+      f.total += n;
+      const bool sync = segs[k].size() < 4 || segs[k][3].cast<bool>();
+      if (sync) mask |= (1ull << k);
+    }
+    TORCH_CHECK((int64_t)f.total <= cap_ / 2, "fold_sync: segments exceed the workspace capacity");
+    XG_CHECK(launch_fold_sync(args_, f, mask, blocks_, c10::hip::getCurrentHIPStream(device_).stream()));
+  }
+
   int error() const {
     DeviceGuard g(device_);
     uint32_t e = 0;
@@ -157,6 +182,7 @@ void register_xgmi(py::module& m) {
       .def("open", &XgmiWorkspace::open, py::arg("rank"), py::arg("world"), py::arg("handles"),
            py::arg("timeout_s") = 10.0)
       .def("allreduce", &XgmiWorkspace::allreduce, py::arg("x"), py::arg("out"), py::arg("scale") = 1.0)
+      .def("fold_sync", &XgmiWorkspace::fold_sync, "SyncBN: fold f64 replicas, sum synchronised segments over ranks")
       .def("error", &XgmiWorkspace::error)
       .def("clear_error", &XgmiWorkspace::clear_error)
       .def_property_readonly("capacity", &XgmiWorkspace::capacity)

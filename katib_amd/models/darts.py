@@ -236,10 +236,20 @@ class DartsNetwork:
         self.ops = ops
         self.momentum, self.eps = momentum, eps
         self._specs = {}
+        # data-parallel SyncBN (a Comm): training BN statistics over every rank's batch
+        # (parallel/syncbn.py; the HIP cells use ops/hip_darts.py SyncBN under DartsSearch)
+        self.sync = None
+
+    def _batch_norm(self, x, rm, rv, w, b, training):
+        if training and self.sync is not None and self.sync.distributed:
+            from ..parallel.syncbn import sync_batch_norm
+
+            return sync_batch_norm(x, rm, rv, w, b, self.momentum, self.eps, self.sync)
+        return F.batch_norm(x, rm, rv, w, b, training, self.momentum, self.eps)
 
     def _bn(self, x, name, bn: BNState, training, w=None, b=None):
         rm, rv = bn.get(name)
-        return F.batch_norm(x, rm, rv, w, b, training, self.momentum, self.eps)
+        return self._batch_norm(x, rm, rv, w, b, training)
 
     def _hip(self, x, stride=1):
         hd = self.ops.hip_module() if self.ops.hip_enabled(x) else None
@@ -416,7 +426,7 @@ class DartsNetwork:
             if hd is not None and w.shape[0] * w.shape[1] <= 8192:
                 return hd.relu_conv_bn(x, w, rm, rv, training, self.momentum, self.eps)
             t = ops.relu_conv1x1(x, w)
-        return F.batch_norm(t, rm, rv, None, None, training, self.momentum, self.eps)
+        return self._batch_norm(t, rm, rv, None, None, training)
 
     def mixed_node(self, states, edges, P, w, bn, training):
         """Node = sum over incoming edges of MixedOp (model.py:61-71). On the HIP backend all

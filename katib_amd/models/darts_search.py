@@ -54,7 +54,7 @@ class _Leaves:
 
 class DartsSearch:
     def __init__(self, layout: DartsLayout, device, comm: Optional[Comm] = None, seed: int = 2,
-                 settings: Optional[Dict] = None, capture: bool = False, ops=None):
+                 settings: Optional[Dict] = None, capture: bool = False, ops=None, sync_bn: bool = False):
         self.layout = layout
         self.device = torch.device(device)
         self.comm = comm or Comm(device=self.device)
@@ -84,6 +84,17 @@ class DartsSearch:
         self.hd = None
         if self.device.type == "cuda" and self.net.ops.backend() == "hip":
             self.hd = self.net.ops.hip_module()
+        # SyncBN (data parallel): BN statistics over the global batch, so a W-rank step at 128/W
+        # images per rank computes the single-GPU step at batch 128 (the reference's BN,
+        # operations.py:62,96,117,139) instead of per-rank BN over 128/W images
+        self.sync_bn = bool(sync_bn) and self.comm.distributed
+        self._hsync = None
+        if self.sync_bn:
+            self.net.sync = self.comm
+            if self.hd is not None:
+                self._hsync = self.hd.SyncBN(self.comm)  # collective
+                if not self._hsync.capturable:
+                    self.capture = False  # its collectives sit inside the passes
         R = self.hd.REP if self.hd is not None else 1
         self.gW_rep = torch.zeros(R, nW, device=dev)
         self.gWv_rep = torch.zeros(R, nW, device=dev)
@@ -270,11 +281,19 @@ class DartsSearch:
             (lambda: (self._seg_weight_update(), end()), []),
         ]
 
+    def _scope(self):
+        if self.hd is not None:
+            return self.hd.sync_scope(self._hsync)
+        import contextlib
+
+        return contextlib.nullcontext()
+
     def _run_eager(self):
-        for fn, colls in self._segments():
-            fn()
-            for t in colls:
-                self.comm.allreduce_mean_(t)
+        with self._scope():
+            for fn, colls in self._segments():
+                fn()
+                for t in colls:
+                    self.comm.allreduce_mean_(t)
 
     def _build_graphs(self):
         segs = self._segments()
@@ -304,7 +323,7 @@ class DartsSearch:
         graphs = []
         for fns, colls in groups:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g), self._scope():
                 for fn in fns:
                     fn()
             graphs.append((g, colls))
@@ -330,8 +349,9 @@ class DartsSearch:
         """Average the BN running statistics over the ranks (each rank tracks its own shard's
         batch statistics, like DDP without SyncBN) so that every rank validates with the same
         model. The mean of per-rank running variances ignores the spread of the per-rank
-        means, a second-order term at equal shard sizes."""
-        if self.comm.distributed:
+        means, a second-order term at equal shard sizes. (With SyncBN every rank already
+        holds the global-batch running statistics.)"""
+        if self.comm.distributed and not self.sync_bn:
             self.comm.allreduce_mean_(self.bn.mean)
             self.comm.allreduce_mean_(self.bn.var)
 

@@ -95,10 +95,86 @@ def _selffold(dev) -> bool:
     return bool(_K.selffold_ready())
 
 
+# SyncBN state of the step being built / run (set by DartsSearch through :func:`sync_scope`): BN
+# statistics and BN-backward sums are folded AND summed over the ranks (one launch, the
+# fold_sync kernel of parallel/xgmi.py), so every rank normalises with the global batch's
+# statistics; None: per-rank BN
+_SYNC = None
+
+
+class SyncBN:
+    """Global-batch BatchNorm for the DARTS supernet under data parallelism (reference BN over
+    the whole 128-image batch, ``operations.py:62,96,117,139``). Construction is collective.
+
+    With the one-shot xGMI path available the fold of every BN reduction becomes ONE launch that
+    also sums the folded values over the ranks (``XgmiWorkspace.fold_sync``, graph-capturable, its
+    own small workspace so its epochs never interleave with the gradient all-reduces'); otherwise
+    the fold is followed by one ``Comm.allreduce_sum_`` per synchronised segment (RCCL / gloo)."""
+
+    def __init__(self, comm):
+        self.comm, self.world = comm, comm.world_size
+        self.ws = None
+        if comm.xgmi is not None:
+            from ..parallel import xgmi
+
+            ar = xgmi.create(comm, capacity=1 << 16, blocks=16)
+            self.ws = ar.ws if ar is not None else None
+
+    @property
+    def capturable(self) -> bool:
+        return self.ws is not None
+
+    def fold(self, segs):
+        """segs: (f64 replicas, n, rstride[, sync]); sync defaults to True (d alpha segments pass False)."""
+        if self.ws is not None:
+            self.ws.fold_sync(list(segs))
+            return
+        _K.fold_f64([tuple(sg[:3]) for sg in segs])
+        for sg in segs:
+            if len(sg) < 4 or sg[3]:
+                self.comm.allreduce_sum_(sg[0][:sg[1]])
+
+
+class sync_scope:
+    """``with sync_scope(SyncBN or None):`` - the kernels launched inside use global-batch BN."""
+
+    def __init__(self, sync):
+        self.sync = sync
+
+    def __enter__(self):
+        global _SYNC
+        self.prev, _SYNC = _SYNC, self.sync
+        return self
+
+    def __exit__(self, *exc):
+        global _SYNC
+        _SYNC = self.prev
+        return False
+
+
+def _world() -> int:
+    return _SYNC.world if _SYNC is not None else 1
+
+
+def _fold(segs):
+    """Fold the replicas of f64 reductions into replica 0 (under SyncBN: and sum the segments not
+    marked local over the ranks)."""
+    if _SYNC is not None:
+        _SYNC.fold(segs)
+    else:
+        _K.fold_f64([tuple(sg[:3]) for sg in segs])
+
+
+def _defer(dev) -> bool:
+    """Consumers may sum the replicas themselves (deferred folds; never under SyncBN, whose
+    cross-rank sum happens in the fold)."""
+    return DEFER_FOLD and FOLD and _SYNC is None and not _selffold(dev)
+
+
 def _fold64(segs, dev=None):
     """fold_f64 launch between producers and consumers, unless the producers folded themselves."""
     if FOLD and (dev is None or not _selffold(dev)):
-        _K.fold_f64(segs)
+        _fold(segs)
 _CAP = {"combine_fwd": 3, "dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 8,
         "dw_bwd": 8, "pool_bwd": 8}
 _REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
@@ -261,8 +337,8 @@ class EdgeSpec:
 
 def _bn(stats: Optional[torch.Tensor], rm, rv, count: int, training: bool, eps: float, C: int):
     """BN reference tuple for the kernels; ``stats`` ([REP][2C]) is folded before use."""
-    if training:
-        return (stats, rm, rv, 1.0 / count, False, eps, _R, 2 * C)
+    if training:  # under SyncBN the statistics are sums over every rank's batch
+        return (stats, rm, rv, 1.0 / (count * _world()), False, eps, _R, 2 * C)
     return (None, rm, rv, 1.0 / count, True, eps, 1, 2 * C)
 
 
@@ -402,7 +478,7 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
     _pool_multi([(*c, S) for S, calls in pool_groups.items() for c in calls])
     if fr_calls:
         _launch("pw_fwd", fr_calls, 2)
-    defer = DEFER_FOLD and training and FOLD and not _selffold(dev)
+    defer = training and _defer(dev)
     if training and stage1 and not defer:
         _fold64([(stats[i * slot:(i + 1) * slot], 2 * C, 2 * C) for i in sorted(set(stage1))], dev)
     # ---- separable stage 2 (stride 1, input BN-apply prologue)
@@ -464,18 +540,18 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey, cel
         e.gw = buf[o + REP * e.nred:o + sz]
         o += sz
         calls.append((dout, e.zl, e.bl, e.x if e.id_idx >= 0 else None, e.red, e.widx, e.id_idx, e.gw))
-        segs += [(e.red, e.nred, e.nred), (e.gw, e.w.numel(), e.w.numel())]
+        segs += [(e.red, e.nred, e.nred), (e.gw, e.w.numel(), e.w.numel(), False)]  # d alpha stays per rank
     _launch("combine_bwd_reduce", calls)
     # deferred: the pointwise backward right below sums the replicas itself and this fold joins
     # the separable second stages' fold (or runs after that pointwise launch)
-    defer = DEFER_FOLD and training and FOLD and not _selffold(dev)
+    defer = training and _defer(dev)
     # inside a cell every reader of this node's reductions sums the replicas itself, so the node
     # folds nothing: the d(alpha) segments go to the cell, which folds them once (if it needs them)
     nofold = defer and cell_gw is not None and not EDGE_BWD
     if nofold:
         cell_gw.extend(segs[1::2])
     if not _selffold(dev) and not defer:
-        _K.fold_f64(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
+        _fold(segs if FOLD else segs[1::2])  # the d(alpha) segments are always folded
 
     r_early = REP if defer else _R  # replicas the pointwise backward below reads
     r_late = REP if nofold else _R  # ... and the pool / stride-2 skip backward further down
@@ -501,7 +577,7 @@ def _node_backward(edges, training, C, dout, gx_of, take_first, sinks, pkey, cel
     if not seps and pwd:
         _launch("pw_bwd", pwd, 1, 0, True)
     if not seps and defer and not nofold:
-        _K.fold_f64(segs)
+        _fold(segs)
     if seps:
         red1 = zeros64(len(seps) * REP * 2 * C, dev) if training else None
         pw2, dw2 = [], defaultdict(list)
@@ -747,7 +823,7 @@ def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2, defer=None):
     else:
         _K.pw_fwd([(x, w1, z, stats, 0, 0)], 1)
     bn = _bn(stats, rm, rv, cnt, training, eps, Cout)
-    late = defer is not None and DEFER_FOLD and training and FOLD and not _selffold(x.device)
+    late = defer is not None and training and _defer(x.device)
     if training and not late:
         _fold64([(stats, 2 * Cout, 2 * Cout)], x.device)
     if late:
@@ -766,7 +842,7 @@ def _stdconv_backward(state, dout, need_x, sinks, keys):
     red = zeros64(REP * nred, x.device)
     # deferred: the pointwise backward (its only consumer) sums the replicas in its prologue, and
     # nothing reads them later, so this fold goes away (the arena is re-zeroed every step)
-    late = DEFER_FOLD and training and FOLD and not _selffold(x.device)
+    late = training and _defer(x.device)
     if training:
         _K.combine_bwd_reduce([(dout, [z], [bn], None, red, [0], -1, None)])
         if not late:
@@ -908,7 +984,7 @@ class _Cell(torch.autograd.Function):
         grads[1], grads[2] = gs0, gs1
         if want_ga:
             if cell_gw:
-                _K.fold_f64(cell_gw)
+                _K.fold_f64(cell_gw)  # d alpha: per rank
             grads[3] = torch.cat([g for rows in ga_rows for g in rows]).view(wshape).to(torch.float32)
         sinks.finish(grads)
         return tuple(grads)
@@ -991,7 +1067,7 @@ class _StemConvBN(torch.autograd.Function):
         stats = zeros64(REP * 2 * C, x.device)
         z = torch.empty(N, C, H, W, device=x.device, dtype=x.dtype)
         _K.stem_conv_fwd_stats(x, w, z, stats)
-        _K.fold_f64([(stats, 2 * C, 2 * C)])  # always folded: the weight-gradient kernel reads replica 0
+        _fold([(stats, 2 * C, 2 * C)])  # always folded: the weight-gradient kernel reads replica 0
         bn = _bn(stats, rm, rv, N * H * W, True, eps, C)
         out = torch.empty_like(z)
         zs = z if ZDT == z.dtype else z.to(ZDT)  # the combine kernels read z in the intermediates' type
@@ -1011,7 +1087,7 @@ class _StemConvBN(torch.autograd.Function):
         red = zeros64(REP * nred, x.device)
         _K.combine_bwd_reduce([(dout, [zs], [bn], None, red, [0], -1, None)])
         if not _selffold(x.device):
-            _K.fold_f64([(red, nred, nred)])
+            _fold([(red, nred, nred)])
         need = ctx.needs_input_grad
         grads = [None] * 8
         sinks = _Sinks()
@@ -1021,7 +1097,7 @@ class _StemConvBN(torch.autograd.Function):
             chunks = stem_chunks(x, C)
             partial = torch.empty(chunks, w.numel(), device=x.device, dtype=torch.float32)
             gw = torch.empty_like(w)
-            _K.stem_conv_wgrad_bn(x, dout, z, red, stats, gamma, eps, gg, gb, partial, gw)
+            _K.stem_conv_wgrad_bn(x, dout, z, red, stats, gamma, eps, gg, gb, partial, gw, _world())
             grads[1] = gw if need[1] else None
         if need[0]:  # never for the input image; plain formula for completeness
             m = stats[:C] / z[:, 0].numel()

@@ -126,16 +126,17 @@ class XgmiAllReduce:
         return self._agree(ok)
 
 
-def create(comm, group=None) -> Optional[XgmiAllReduce]:
+def create(comm, group=None, capacity: Optional[int] = None, blocks: Optional[int] = None) -> Optional[XgmiAllReduce]:
     """The fast path for a :class:`~katib_amd.parallel.comm.Comm`, or None (RCCL only).
 
     Enabled for multi-rank jobs on GPUs of one node (``LOCAL_WORLD_SIZE == WORLD_SIZE``,
-    at most 8 ranks) unless ``KATIB_AMD_XGMI=0``."""
+    at most 8 ranks) unless ``KATIB_AMD_XGMI=0``. ``capacity`` (floats) / ``blocks`` size a
+    workspace of its own (e.g. the SyncBN fold of ``ops/hip_darts.py``)."""
     if os.environ.get("KATIB_AMD_XGMI", "1") == "0" or comm.world_size < 2 or comm.device.type != "cuda":
         return None
     if int(os.environ.get("LOCAL_WORLD_SIZE", str(comm.world_size))) != comm.world_size or comm.world_size > 8:
         return None
     if group is None:
         group = dist.new_group(backend="gloo")
-    ar = XgmiAllReduce(comm.rank, comm.world_size, comm.device, group=group)
+    ar = XgmiAllReduce(comm.rank, comm.world_size, comm.device, group=group, capacity=capacity, blocks=blocks)
     return ar if ar.ok else None

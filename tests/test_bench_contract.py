@@ -21,13 +21,24 @@ def _free_port():
     return p
 
 
-def _run(nproc, *extra):
+BENCH_ARGS = ["--steps", "2", "--warmup", "1", "--trials", "0", "--comparator-steps", "0", "--full-search", "0",
+              "--valid-batches", "2"]
+
+
+def _run(nproc, *extra, torchrun=True, gpus=None, rc=0):
     env = dict(os.environ, OMP_NUM_THREADS="2")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--trials", "0", "--comparator-steps", "0",
-           "--full-search", "0", "--valid-batches", "2", *extra]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    bench = [os.path.join(ROOT, "bench.py"), "--gpus", str(gpus or nproc)] + BENCH_ARGS + list(extra)
+    if torchrun:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + bench
+    else:  # the plain `python bench.py --gpus N` form: bench.py launches its N ranks itself
+        cmd = [sys.executable] + bench
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    if rc != 0:
+        assert out.returncode != 0, out.stdout[-2000:]
+        return out
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]  # rank 0 only
@@ -38,7 +49,8 @@ def test_bench_two_ranks_strong_scaling():
     r = _run(2)
     assert KEYS <= set(r)
     assert r["metric"] == "darts_cifar10_search_wall_clock_s" and r["higher_is_better"] is False
-    assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1 and r["scaling"] == "strong"
+    assert r["n_gpus"] == 2 and r["ranks_seen"] == 2 and r["steps"] == 2 and r["warmup"] == 1
+    assert r["scaling"] == "strong" and r["allreduce"] == "gloo" and r["batchnorm"] == "global batch (sync-bn)"
     c = r["config"]
     assert c["global_batch"] == 128 and c["per_gpu_batch"] == 64 and c["parallelism"] == "dp2"
     assert c["steps_per_epoch"] == 196 and c["second_order"] is True and c["allreduce"] == "gloo"
@@ -54,3 +66,23 @@ def test_bench_two_ranks_weak_scaling_label():
     assert r["scaling"] == "weak"
     assert r["config"]["global_batch"] == 256 and r["config"]["per_gpu_batch"] == 128
     assert r["config"]["steps_per_epoch"] == 98
+
+
+def test_bench_self_launches_n_ranks():
+    """plain `python bench.py --gpus 2` (no torchrun around it) runs 2 ranks and
+    relays rank 0's single JSON line; n_gpus == ranks_seen == 2."""
+    r = _run(2, torchrun=False)
+    assert r["n_gpus"] == 2 and r["ranks_seen"] == 2 and r["config"]["parallelism"] == "dp2"
+    assert r["config"]["per_gpu_batch"] == 64 and r["allreduce"] == "gloo"
+
+
+def test_bench_refuses_world_size_mismatch():
+    """Under torchrun, --gpus must equal WORLD_SIZE: a 2-rank launch told --gpus 4 exits non-zero
+    instead of timing (and labelling) a different world size."""
+    out = _run(2, torchrun=True, gpus=4, rc=1)
+    assert "WORLD_SIZE=2 but --gpus 4" in out.stderr
+
+
+def test_bench_per_rank_bn_label():
+    r = _run(2, "--sync-bn", "0")
+    assert r["batchnorm"] == "per rank" and r["config"]["sync_bn"] is False

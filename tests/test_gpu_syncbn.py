@@ -1,0 +1,46 @@
+"""SyncBN on the HIP DARTS path: a 2-rank strong-scaling step with half the
+batch per rank and global-batch BN (fused fold + cross-rank sum launch, captured with the rest of
+the step) follows the single-process batch-64 search - genotype equal and alpha drift within 5 %
+of the alphas' displacement after 30 steps - while per-rank BN does not. The ranks share the box's
+GPU through IPC (the same protocol as peers over xGMI)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(sync):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "gpu_syncbn_worker.py")]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", SYNC_BN="1" if sync else "0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("SYNCBN_RESULT ")][-1]
+    return json.loads(line.split(" ", 1)[1])
+
+
+def test_gpu_syncbn_two_ranks_match_single_process():
+    res = _run(True)
+    print(res)
+    assert res["capture"] and res["allreduce"] == "xgmi", res
+    assert res["geno_equal"], res
+    assert res["dA"] <= 0.05 * res["A_disp"], res
+    assert res["dW"] <= 1e-3 * max(1.0, res["W_scale"]), res
+    per_rank = _run(False)
+    print(per_rank)
+    assert per_rank["dA"] > 2 * res["dA"], (per_rank, res)

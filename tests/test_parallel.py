@@ -78,3 +78,27 @@ def test_p2p_handle_file_is_json_roundtrip():
 
     with pytest.raises(KeyError):  # classes / dtypes only through the whitelists
         P._decode_handle([[3], [1], 0, "os.system", "torch.float32", 0, "00", 12, 0, False, None, 0, None, False])
+
+
+def _run_syncbn(sync: bool, nproc: int = 2):
+    port = _free_port()
+    env = dict(os.environ, OMP_NUM_THREADS="1", SYNC_BN="1" if sync else "0")
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dp_syncbn_worker.py")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % nproc,
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), worker],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_darts_dp_syncbn_matches_single_process():
+    """with SyncBN a 2-rank strong-scaling step (half the batch per rank) IS the
+    single-process step on the whole batch - weights, alphas and BN running statistics agree to
+    float rounding; per-rank BN (the old behaviour) visibly diverges."""
+    res = _run_syncbn(True)
+    assert res["dW"] <= 1e-5 * max(1.0, res["W_scale"]), res
+    assert res["dA"] <= 0.01 * res["A_disp"], res
+    assert res["dBN"] <= 1e-5, res
+    assert res["geno_equal"], res
+    per_rank = _run_syncbn(False)
+    assert per_rank["dA"] > 10 * max(res["dA"], 1e-12), (per_rank, res)
