@@ -124,6 +124,21 @@ def cmd_serve(a):
     from .controller.manager import Manager
     from .rpc.server import make_server
 
+    from .controller.apiserver import is_loopback
+
+    token = None
+    if a.token_file:
+        with open(a.token_file) as f:
+            token = f.read().strip()
+    elif os.environ.get("KATIB_AMD_API_TOKEN"):
+        token = os.environ["KATIB_AMD_API_TOKEN"]
+    exposed = [x for x in (a.address, a.grpc) if x and not is_loopback(x)]
+    if exposed and token is None and not a.insecure_listen:
+        # the API accepts Job / LocalProcess trials whose command runs as this user: never open
+        # it to the network without a token
+        print("refusing to listen on %s without --token-file (or --insecure-listen)" % ", ".join(exposed),
+              file=sys.stderr)
+        return 2
     m = Manager(state_dir=a.state_dir, num_devices=a.gpus, journal=True)
     if a.config:
         from .controller.config import KatibConfig
@@ -131,7 +146,7 @@ def cmd_serve(a):
         m.config = KatibConfig.load(a.config)
     restored = m.restore()
     m.start()
-    api = ApiServer(m, a.address, a.port).start()
+    api = ApiServer(m, a.address, a.port, token=token).start()
     grpc_srv = None
     if a.grpc:
         grpc_srv = make_server(a.grpc, store=m.store)
@@ -317,7 +332,7 @@ def cmd_install(a):
     from .deploy import render
 
     files = render(a.profile, a.prefix, python=a.python, user=a.user, state_dir=a.state_dir, gpus=a.gpus,
-                   slots_per_gpu=a.slots_per_gpu)
+                   slots_per_gpu=a.slots_per_gpu, listen=a.listen)
     print(json.dumps({"profile": a.profile, "prefix": os.path.abspath(a.prefix), "files": sorted(files)}))
     return 0
 
@@ -371,7 +386,10 @@ def build_parser():
     s = sub.add_parser("serve", help="run the scheduler daemon with its HTTP API")
     s.add_argument("--address", default="127.0.0.1")
     s.add_argument("--port", type=int, default=8080)
-    s.add_argument("--grpc", default="", help="also serve DBManager gRPC here, e.g. 0.0.0.0:6789")
+    s.add_argument("--grpc", default="", help="also serve DBManager gRPC here, e.g. 127.0.0.1:6789")
+    s.add_argument("--token-file", default="", help="bearer token required by the HTTP API (needed off loopback)")
+    s.add_argument("--insecure-listen", action="store_true",
+                   help="allow a non-loopback --address / --grpc without a token (not recommended)")
     s.add_argument("--state-dir", default=None)
     s.add_argument("--gpus", type=int, default=None)
     s.add_argument("--config", default="", help="katib-config.yaml")
@@ -400,17 +418,17 @@ def build_parser():
 
     g = sub.add_parser("suggestion-server", help="serve one algorithm over gRPC (port 6789)")
     g.add_argument("--algorithm", required=True)
-    g.add_argument("--address", default="0.0.0.0:6789")
+    g.add_argument("--address", default="127.0.0.1:6789")
     g.add_argument("--data-root", default="/opt/katib/data")
     g.set_defaults(fn=cmd_suggestion_server)
 
     es = sub.add_parser("earlystopping-server", help="serve medianstop over gRPC (port 6788)")
-    es.add_argument("--address", default="0.0.0.0:6788")
+    es.add_argument("--address", default="127.0.0.1:6788")
     es.add_argument("--db-manager", default="")
     es.set_defaults(fn=cmd_earlystopping_server)
 
     d = sub.add_parser("db-manager", help="DBManager gRPC server on the native observation store")
-    d.add_argument("--address", default="0.0.0.0:6789")
+    d.add_argument("--address", default="127.0.0.1:6789")
     d.add_argument("--journal", default="", help="append-only journal file for persistence")
     d.add_argument("--db", default="", help="native (default) | sqlite | mysql | postgres (else $DB_NAME)")
     d.add_argument("--connect-timeout", type=float, default=60.0, help="seconds to wait for the database")
@@ -435,6 +453,8 @@ def build_parser():
     ins.add_argument("--state-dir", default="/var/lib/katib-amd")
     ins.add_argument("--gpus", type=int, default=None)
     ins.add_argument("--slots-per-gpu", type=int, default=1)
+    ins.add_argument("--listen", default="127.0.0.1",
+                     help="bind address of the API and gRPC services (non-loopback: a token file is generated)")
     ins.set_defaults(fn=cmd_install)
 
     oa = sub.add_parser("openapi", help="print the v1beta1 Swagger 2.0 document (reference swagger.json layout)")

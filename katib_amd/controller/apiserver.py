@@ -68,9 +68,23 @@ def _best_values(trial, logs):
     return best
 
 
+def is_loopback(address: str) -> bool:
+    """True for addresses only this host can reach (127.0.0.0/8, ::1, localhost, unix sockets)."""
+    host = address.rsplit(":", 1)[0] if address.count(":") == 1 else address
+    host = host.strip("[]")
+    if address.startswith("unix:") or host in ("localhost", "::1"):
+        return True
+    return host.startswith("127.")
+
+
 class ApiServer:
-    def __init__(self, manager, address: str = "127.0.0.1", port: int = 8080):
+    """HTTP API + UI. ``token``: when set, every request except the health probes must carry
+    ``Authorization: Bearer <token>`` (the reference sits behind cluster auth / ingress; a node
+    daemon that accepts trial commands must not be open to the network)."""
+
+    def __init__(self, manager, address: str = "127.0.0.1", port: int = 8080, token: Optional[str] = None):
         self.m = manager
+        self.token = token or None
         handler = self._make_handler()
         self.httpd = ThreadingHTTPServer((address, port), handler)
         self.port = self.httpd.server_address[1]
@@ -334,11 +348,21 @@ class ApiServer:
             def log_message(self, fmt, *args):  # quiet
                 pass
 
+            def _authorized(self, path) -> bool:
+                if server.token is None or path in ("/healthz", "/readyz"):
+                    return True
+                import hmac
+
+                got = self.headers.get("Authorization") or ""
+                return hmac.compare_digest(got.encode(), ("Bearer " + server.token).encode())
+
             def _do(self, method):
                 u = urlparse(self.path)
                 n = int(self.headers.get("Content-Length") or 0)
                 body = self.rfile.read(n) if n else b""
                 try:
+                    if not self._authorized(u.path):
+                        raise _Err(401, "Unauthorized", "missing or wrong bearer token")
                     code, ctype, data = server.handle(method, u.path, parse_qs(u.query), body)
                 except _Err as e:
                     code, ctype = e.code, "application/json"

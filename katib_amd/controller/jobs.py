@@ -79,6 +79,7 @@ class LaunchPlan:
     deadline: float = 0.0
     backoff_limit: int = 0
     share_devices: bool = False  # every replica sees all the trial's devices (rank plans, training jobs)
+    ports_managed: bool = False  # rendezvous ports in the replicas' env are ours: fresh ones per attempt
 
     @property
     def primary(self) -> ReplicaPlan:
@@ -176,6 +177,7 @@ def _ranked(plan: LaunchPlan, base: ReplicaPlan, mode: str) -> LaunchPlan:
         return plan
     port = free_port()
     plan.share_devices = True
+    plan.ports_managed = True
     # split the CPU threads between the ranks (torchrun does the same): N ranks each spinning
     # a full OpenMP pool on a CPU-side collective oversubscribe the host by N x
     threads = max(1, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1) // base.gpus)
@@ -186,6 +188,31 @@ def _ranked(plan: LaunchPlan, base: ReplicaPlan, mode: str) -> LaunchPlan:
         plan.replicas.append(ReplicaPlan("primary" if r == 0 else "rank", r, list(base.argv), env, base.cwd, 1,
                                          r == 0, entrypoint=base.entrypoint, function=base.function))
     return plan
+
+
+def assign_ports(plan: LaunchPlan) -> None:
+    """Fresh rendezvous ports for one launch attempt of a plan whose ports are ours
+    (``ports_managed``): ``MASTER_PORT`` (rank plans, PyTorchJob, XGBoostJob), ``DMLC_PS_ROOT_PORT``
+    (MXJob) and every task address of a TFJob's ``TF_CONFIG`` cluster, all from free_port's ledger.
+    A retry after a backoff or a wait for GPU slots never reuses a port a previous attempt's rank
+    may still hold."""
+    if not plan.ports_managed or not plan.replicas:
+        return
+    master = free_port()
+    cluster = None
+    for rep in plan.replicas:
+        if "TF_CONFIG" in rep.env and cluster is None:
+            old = json.loads(rep.env["TF_CONFIG"])["cluster"]
+            cluster = {role: ["127.0.0.1:%d" % free_port() for _ in addrs] for role, addrs in old.items()}
+    for rep in plan.replicas:
+        if "MASTER_PORT" in rep.env:
+            rep.env["MASTER_PORT"] = str(master)
+        if "DMLC_PS_ROOT_PORT" in rep.env:
+            rep.env["DMLC_PS_ROOT_PORT"] = str(master)
+        if "TF_CONFIG" in rep.env:
+            cfg = json.loads(rep.env["TF_CONFIG"])
+            cfg["cluster"] = cluster
+            rep.env["TF_CONFIG"] = json.dumps(cfg)
 
 
 def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Optional[Dict[str, str]] = None,
@@ -238,12 +265,13 @@ def make_plan(run_spec: Dict, primary_container: str, primary_pod_labels: Option
             primary_role = ordered[0]
         world = sum(int(rspecs[r].get("replicas", 1)) for r in ordered
                     if not (kind == "MPIJob" and r == "Launcher"))
+        plan.ports_managed = True
         port = free_port()
         rank = 0
         cluster = {}
-        for role in ordered:
+        for role in ordered:  # every task address through free_port's ledger (never port arithmetic)
             n = int(rspecs[role].get("replicas", 1))
-            cluster[role.lower()] = ["127.0.0.1:%d" % (port + 1 + len(cluster) * 64 + i) for i in range(n)]
+            cluster[role.lower()] = ["127.0.0.1:%d" % free_port() for _ in range(n)]
         for role in ordered:
             rs = rspecs[role]
             pod = ((rs.get("template") or {}).get("spec")) or {}

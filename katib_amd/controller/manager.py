@@ -49,7 +49,7 @@ from . import gjson
 from . import status_engine as SE
 from .config import KatibConfig
 from .converters import comparison_from_pb, convert_experiment, convert_trials
-from .jobs import JobSpecError, LaunchPlan, job_status, make_plan, map_paths, path_mapping
+from .jobs import JobSpecError, LaunchPlan, assign_ports, job_status, make_plan, map_paths, path_mapping
 from .manifest import ConfigMapStore, Generator
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -757,13 +757,22 @@ class Manager:
                     self._finish_trial(tkey, "Failed", "JobSpecInvalid", str(e))
                     continue
             gpus = run.plan.total_gpus
+            # slots stack on one device only where each slot is its own process (rank plans /
+            # one-GPU replicas); a process that asks for k GPUs gets k different devices
+            distinct = any(rep.gpus > 1 for rep in run.plan.replicas)
             if gpus > 0:
+                if distinct and max(rep.gpus for rep in run.plan.replicas) > self.n_devices:
+                    self._finish_trial(tkey, "Failed", "Unschedulable",
+                                       "0/1 nodes are available: insufficient amd.com/gpu (one process requested %d "
+                                       "GPUs, node has %d)" % (max(rep.gpus for rep in run.plan.replicas),
+                                                                self.n_devices))
+                    continue
                 if gpus > self.slots.capacity():
                     self._finish_trial(tkey, "Failed", "Unschedulable",
                                        "0/1 nodes are available: insufficient amd.com/gpu (requested %d, node has %d)"
                                        % (gpus, self.slots.capacity()))
                     continue
-                devs = self.slots.acquire(gpus)
+                devs = self.slots.acquire(gpus, distinct)
                 if not devs:
                     continue
                 run.devices = list(devs)
@@ -861,6 +870,7 @@ class Manager:
         # jobs see all of them (a rank picks LOCAL_RANK % device_count, parallel/comm.py)
         dev_iter = iter(run.devices)
         plan = run.plan
+        assign_ports(plan)  # fresh rendezvous ports for this attempt (the plan is cached across retries)
         all_devs = sorted(set(run.devices))
         run.attempt += 1
         run.phase = "Launching"

@@ -169,7 +169,7 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<SlotPool, std::shared_ptr<SlotPool>>(m, "SlotPool")
       .def(py::init<int, int>(), py::arg("n_devices"), py::arg("slots_per_device") = 1)
-      .def("acquire", &SlotPool::acquire)
+      .def("acquire", &SlotPool::acquire, py::arg("n"), py::arg("distinct") = false)
       .def("release", &SlotPool::release)
       .def("quarantine", &SlotPool::quarantine)
       .def("record_fault", &SlotPool::record_fault)

@@ -33,7 +33,7 @@ static double mono_now() {
 SlotPool::SlotPool(int n_devices, int slots_per_device)
     : n_(n_devices), per_(std::max(1, slots_per_device)), used_(n_devices, 0), faults_(n_devices, 0) {}
 
-std::vector<int> SlotPool::acquire(int n) {
+std::vector<int> SlotPool::acquire(int n, bool distinct) {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<int> out;
   if (n <= 0) return out;
@@ -49,6 +49,9 @@ std::vector<int> SlotPool::acquire(int n) {
       free_total += per_ - used_[d];
     }
   if (free_total < n) return out;
+  // a single process that drives n GPUs needs n DIFFERENT devices (stacking is for rank plans,
+  // where each slot is its own process)
+  if (distinct && (int)order.size() < n) return out;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return used_[a] < used_[b]; });
   std::vector<int> take(n_, 0);
   int got = 0;

@@ -75,7 +75,8 @@ class SlotPool {
  public:
   SlotPool(int n_devices, int slots_per_device);
   // returns device ids (size n) or empty if not enough free slots
-  std::vector<int> acquire(int n);
+  // n slots (least-loaded devices first); distinct: on n different devices or nothing
+  std::vector<int> acquire(int n, bool distinct = false);
   void release(const std::vector<int>& devices);
   void quarantine(int device);
   void record_fault(int device, int threshold);

@@ -78,8 +78,13 @@ def _unit(description: str, exec_start: List[str], env_file: str, user: str, aft
 
 def render(profile: str, prefix: str, python: str = "", user: str = "katib", state_dir: str = "/var/lib/katib-amd",
            gpus: Optional[int] = None, slots_per_gpu: int = 1, api_port: int = 8080,
-           grpc_port: int = 6789) -> Dict[str, str]:
-    """Write the install of ``profile`` under ``prefix``; returns {relative path: content}."""
+           grpc_port: int = 6789, listen: str = "127.0.0.1") -> Dict[str, str]:
+    """Write the install of ``profile`` under ``prefix``; returns {relative path: content}.
+
+    Every service binds ``listen`` (loopback by default: the API accepts trials whose command
+    runs as the service user). A non-loopback ``listen`` makes the API require a bearer token,
+    generated into ``api-token`` (mode 0600) and passed with ``--token-file``. The env file (DB
+    password) and the token are written 0600 and chowned to the service user by install.sh."""
     if profile not in PROFILES:
         raise ValueError("unknown profile %r (one of %s)" % (profile, ", ".join(PROFILES)))
     python = python or sys.executable
@@ -94,13 +99,23 @@ def render(profile: str, prefix: str, python: str = "", user: str = "katib", sta
         "katib-config.yaml": yaml.safe_dump(katib_config(state_dir, gpus, slots_per_gpu), sort_keys=False),
         "katib-amd.env": "".join("%s=%s\n" % kv for kv in sorted(env.items())),
     }
-    serve = base + ["serve", "--address", "0.0.0.0", "--port", str(api_port), "--state-dir", state_dir,
+    from ..controller.apiserver import is_loopback
+
+    secret = {"katib-amd.env"}
+    serve = base + ["serve", "--address", listen, "--port", str(api_port), "--state-dir", state_dir,
                     "--config", cfg_path]
+    if not is_loopback(listen):
+        import secrets
+
+        files["api-token"] = secrets.token_hex(32) + "\n"
+        secret.add("api-token")
+        serve += ["--token-file", os.path.join(prefix, "api-token")]
+    bind = listen + ":%d"
     if gpus is not None:
         serve += ["--gpus", str(gpus)]
     units = []
     if profile == "services":
-        db_mgr = base + ["db-manager", "--address", "0.0.0.0:%d" % grpc_port, "--journal",
+        db_mgr = base + ["db-manager", "--address", bind % grpc_port, "--journal",
                          os.path.join(state_dir, "observations.journal")]
         files["katib-amd-db-manager.service"] = _unit("Katib (MI355X) DBManager gRPC", db_mgr, env_path, user)
         files["katib-amd-suggestion@.service"] = _unit(
@@ -109,14 +124,14 @@ def render(profile: str, prefix: str, python: str = "", user: str = "katib", sta
                                                             os.path.join(state_dir, "suggestions", "%i")],
             env_path, user, extra="RuntimeDirectory=katib-amd\nRuntimeDirectoryPreserve=yes")
         files["katib-amd-earlystopping.service"] = _unit(
-            "Katib (MI355X) median-stop early stopping", base + ["earlystopping-server", "--address", "0.0.0.0:6788",
+            "Katib (MI355X) median-stop early stopping", base + ["earlystopping-server", "--address", bind % 6788,
                                                                "--db-manager", "127.0.0.1:%d" % grpc_port],
             env_path, user, after="katib-amd-db-manager.service")
         units += ["katib-amd-db-manager.service", "katib-amd-earlystopping.service"]
         files["katib-amd.service"] = _unit("Katib (MI355X) scheduler, HTTP API and UI", serve, env_path, user,
                                            after="katib-amd-db-manager.service")
     elif db:
-        db_mgr = base + ["db-manager", "--address", "0.0.0.0:%d" % grpc_port, "--db", db]
+        db_mgr = base + ["db-manager", "--address", bind % grpc_port, "--db", db]
         files["katib-amd-db-manager.service"] = _unit("Katib (MI355X) DBManager gRPC on %s" % db, db_mgr, env_path,
                                                       user, after="%s.service" % ("mysqld" if db == "mysql"
                                                                                   else "postgresql"))
@@ -124,11 +139,13 @@ def render(profile: str, prefix: str, python: str = "", user: str = "katib", sta
         files["katib-amd.service"] = _unit("Katib (MI355X) scheduler, HTTP API and UI", serve, env_path, user)
     else:
         files["katib-amd.service"] = _unit("Katib (MI355X) scheduler, HTTP API, UI and DBManager gRPC",
-                                           serve + ["--grpc", "0.0.0.0:%d" % grpc_port], env_path, user)
+                                           serve + ["--grpc", bind % grpc_port], env_path, user)
     units.append("katib-amd.service")
     files["install.sh"] = "\n".join([
         "#!/bin/sh", "# %s install of katib-amd (rendered by 'katib-amd install')" % profile, "set -e",
         "install -d -o %s %s" % (shlex.quote(user), shlex.quote(state_dir)),
+        *["chown %s %s && chmod 0600 %s" % (shlex.quote(user), shlex.quote(os.path.join(prefix, f)),
+                                             shlex.quote(os.path.join(prefix, f))) for f in sorted(secret)],
         *["install -m 0644 %s /etc/systemd/system/" % shlex.quote(os.path.join(prefix, u))
           for u in sorted(f for f in files if f.endswith(".service"))],
         "systemctl daemon-reload",
@@ -136,8 +153,9 @@ def render(profile: str, prefix: str, python: str = "", user: str = "katib", sta
     os.makedirs(prefix, exist_ok=True)
     for name, text in files.items():
         path = os.path.join(prefix, name)
-        with open(path, "w") as f:
+        mode = 0o600 if name in secret else (0o755 if name.endswith(".sh") else 0o644)
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, mode)
+        with os.fdopen(fd, "w") as f:
             f.write(text)
-        if name.endswith(".sh"):
-            os.chmod(path, 0o755)
+        os.chmod(path, mode)  # also when the file existed with other permissions
     return files

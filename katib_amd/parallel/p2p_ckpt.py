@@ -107,7 +107,11 @@ def publish(state: Any, ckpt_dir: str, key: Optional[str] = None) -> bool:
     from torch.multiprocessing.reductions import reduce_tensor
 
     tensors: List[torch.Tensor] = []
-    skeleton = _flatten(state, tensors)
+    try:
+        skeleton = _flatten(state, tensors)
+        json.dumps(skeleton)  # the handle file is data-only JSON: check before touching the cache / files
+    except (TypeError, ValueError):
+        return False  # e.g. numpy scalars, dtypes, sets: the caller falls back to torch.save files
     if not tensors or not all(t.is_cuda for t in tensors):
         return False
     dev = tensors[0].device

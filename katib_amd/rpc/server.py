@@ -130,7 +130,7 @@ def _handler(service_name, servicer):
     return grpc.method_handlers_generic_handler(api.PKG + "." + service_name, methods)
 
 
-def make_server(address: str = "0.0.0.0:6789", store=None, suggestion_service=None, early_stopping_service=None,
+def make_server(address: str = "127.0.0.1:6789", store=None, suggestion_service=None, early_stopping_service=None,
                 max_workers: int = 10) -> grpc.Server:
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers),
                          options=[("grpc.max_send_message_length", MAX_MSG),

