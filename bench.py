@@ -62,7 +62,12 @@ def main():
     ap.add_argument("--trials", type=int, default=3, help="trials per GPU of the trials/hour experiment (0: skip)")
     ap.add_argument("--trial-slots", type=int, default=1,
                     help="concurrent trials per GPU in the trials/hour experiment (warm workers per GPU)")
-    ap.add_argument("--comparator-steps", type=int, default=5, help="torch-eager comparator steps (0: skip)")
+    ap.add_argument("--comparator-steps", type=int, default=5,
+                    help="steps of each same-GPU comparator (torch ops eager / torch ops in a HIP graph / the "
+                         "nn.Module trainer eager; 0: skip)")
+    ap.add_argument("--b1", type=int, default=1,
+                    help="also run the B1-shaped experiment (examples/hp-tuning/b1-random-mnist-mlp.yaml: random "
+                         "search, 12 cold batch/v1 Job trials, 3 in parallel) -> b1_trials_per_hour")
     ap.add_argument("--capture", type=int, default=1)
     ap.add_argument("--ops", default=os.environ.get("KATIB_AMD_DARTS_OPS", "hip"))
     ap.add_argument("--valid-batches", type=int, default=10)
@@ -99,9 +104,11 @@ def main():
 
     # trials/hour (BASELINE config 2) first, from rank 0, before this process touches the GPU:
     # the scheduler's warm workers then own every GPU while the experiment runs
-    tph = None
+    tph = b1 = None
     if args.trials > 0 and int(os.environ.get("RANK", "0")) == 0:
         tph = trials_per_hour(args.gpus, args.trials, args.trial_slots)
+    if args.b1 and int(os.environ.get("RANK", "0")) == 0:
+        b1 = b1_trials_per_hour(args.gpus)
 
     import torch
 
@@ -221,26 +228,42 @@ def main():
             del solo
         comm.barrier()
 
-    # same-node comparator: the PyTorch op backend, eager (no graph), same config and batch
-    torch_ms = None
-    if args.comparator_steps > 0 and dev.type == "cuda" and args.dtype == "fp32":
+    # same-GPU comparators (rank 0 of a 1-rank run): the same search step on the PyTorch op backend
+    # launched eagerly (MIOpen / hipBLASLt / PyTorch kernels), the same PyTorch ops captured in a HIP
+    # graph (isolates kernel quality from launch overhead), and the reference-shaped nn.Module
+    # trainer (models/darts_module.py) run eagerly
+    comp = {"torch_eager": None, "torch_graph": None, "module_eager": None}
+    if args.comparator_steps > 0 and dev.type == "cuda" and args.dtype == "fp32" and not comm.distributed:
+        def timed(obj, warm):
+            for i in range(warm):
+                (tx, ty), (vx, vy) = batches[i % len(batches)]
+                obj.step(tx, ty, vx, vy)
+            sync()
+            t3 = time.perf_counter()
+            for i in range(args.comparator_steps):
+                (tx, ty), (vx, vy) = batches[i % len(batches)]
+                obj.step(tx, ty, vx, vy)
+            sync()
+            return (time.perf_counter() - t3) * 1000.0 / args.comparator_steps
+
         dops.set_backend("torch")
-        ref = DartsSearch(layout, dev, comm, capture=False)
-        for i in range(2):
-            (tx, ty), (vx, vy) = batches[i % len(batches)]
-            ref.step(tx, ty, vx, vy)
-        sync()
-        comm.barrier()
-        sync()
-        t3 = time.perf_counter()
-        for i in range(args.comparator_steps):
-            (tx, ty), (vx, vy) = batches[i % len(batches)]
-            ref.step(tx, ty, vx, vy)
-        sync()
-        comm.barrier()
-        sync()
-        torch_ms = comm.allreduce_max((time.perf_counter() - t3) * 1000.0 / args.comparator_steps)
+        try:
+            comp["torch_eager"] = timed(DartsSearch(layout, dev, Comm(device=dev), capture=False), 2)
+        except Exception as e:  # noqa: BLE001 - a comparator must not sink the headline
+            print("torch-eager comparator failed: %s" % e, file=sys.stderr)
+        try:
+            comp["torch_graph"] = timed(DartsSearch(layout, dev, Comm(device=dev), capture=True), 3)
+        except Exception as e:  # noqa: BLE001
+            print("torch-graph comparator failed: %s" % e, file=sys.stderr)
         dops.set_backend(args.ops)
+        try:
+            from katib_amd.models.darts_module import ModuleSearch
+
+            comp["module_eager"] = timed(ModuleSearch(PRIMS, cfg["init_channels"], cfg["num_layers"],
+                                                      cfg["num_nodes"], cfg["stem_multiplier"], dev), 2)
+        except Exception as e:  # noqa: BLE001
+            print("module comparator failed: %s" % e, file=sys.stderr)
+    torch_ms = comp["torch_eager"]
     allreduce = (("xgmi-oneshot" if comm.xgmi is not None else ("rccl" if comm.backend == "nccl" else comm.backend))
                  if comm.distributed else None)
     if comm.rank == 0:
@@ -279,7 +302,12 @@ def main():
             "baseline_b5_s": B5_SECONDS,
             "torch_eager_ms_per_step": round(torch_ms, 3) if torch_ms is not None else None,
             "speedup_vs_torch_eager": round(torch_ms / ms_step, 2) if torch_ms else None,
+            "torch_graph_ms_per_step": round(comp["torch_graph"], 3) if comp["torch_graph"] else None,
+            "speedup_vs_torch_graph": round(comp["torch_graph"] / ms_step, 2) if comp["torch_graph"] else None,
+            "module_eager_ms_per_step": round(comp["module_eager"], 3) if comp["module_eager"] else None,
+            "speedup_vs_module_eager": round(comp["module_eager"] / ms_step, 2) if comp["module_eager"] else None,
             "trials_per_hour": tph,
+            "b1_trials_per_hour": b1,
         }
         print(json.dumps(out), flush=True)
     comm.destroy()
@@ -305,6 +333,30 @@ def self_launch(n: int) -> int:
         return r.returncode or 1
     print(lines[0], flush=True)
     return 0
+
+
+def b1_trials_per_hour(gpus: int):
+    """The reference's B1 experiment shape (docs/workflow-design.md:39-108): random search, 12 trials,
+    3 in parallel, lr / num-layers / optimizer of an MNIST MLP at batch 64, each trial a cold
+    batch/v1 Job process (examples/hp-tuning/b1-random-mnist-mlp.yaml), on ``gpus`` GPUs."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    cmd = [sys.executable, os.path.join(here, "bench_trials.py"), "--experiment",
+           os.path.join(here, "examples", "hp-tuning", "b1-random-mnist-mlp.yaml"), "--gpus", str(gpus)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=1200)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not line:
+            print("B1 experiment failed: %s" % (r.stderr[-2000:],), file=sys.stderr)
+            return None
+        res = json.loads(line[-1])
+    except (subprocess.TimeoutExpired, ValueError) as e:
+        print("B1 experiment failed: %s" % e, file=sys.stderr)
+        return None
+    return {"value": res["value"], "unit": "trials/h", "vs_b1": res["vs_baseline"], "wall_s": res["wall_s"],
+            "trials_completed": res["trials_completed"], "median_trial_s": res["median_trial_s"],
+            "best_validation_accuracy": res["best_objective"], "n_gpus": gpus,
+            "config": "B1 shape: random, 12 trials, parallel 3, cold batch/v1 Job processes, MLP lr / "
+                      "num-layers / optimizer, batch 64, 3 epochs", "b1_trials_per_hour": 36.3}
 
 
 def trials_per_hour(gpus: int, per_gpu: int, slots: int = 1):

@@ -33,7 +33,12 @@ def main():
     ap.add_argument("--num-train", type=int, default=60000)
     ap.add_argument("--algorithm", default="tpe")
     ap.add_argument("--state-dir", default="")
+    ap.add_argument("--experiment", default="",
+                    help="run this Experiment YAML as is (trials / parallel / epochs from the file unless given); "
+                         "e.g. examples/hp-tuning/b1-random-mnist-mlp.yaml (the reference's B1 shape)")
     args = ap.parse_args()
+    if args.experiment:
+        return run_file(args)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from katib_amd.api.conditions import ExperimentConditions as EC
@@ -85,5 +90,60 @@ def main():
                    "slots_per_gpu": slots}}))
 
 
+def run_file(args):
+    """B1-shaped run: the Experiment file as written (cold batch/v1 Job trials, its own algorithm,
+    parallelism and budget), trials/hour of wall clock from creation to completion."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from katib_amd.api.conditions import ExperimentConditions as EC
+    from katib_amd.api.yaml_io import load_experiment
+    from katib_amd.controller.config import detect_gpus
+    from katib_amd.controller.manager import Manager
+
+    e = load_experiment(args.experiment)
+    n_gpus = args.gpus or detect_gpus()
+    par = e.spec.parallel_trial_count or 3
+    slots = args.slots_per_gpu or (max(1, -(-par // n_gpus)) if n_gpus else 1)
+    state = args.state_dir or tempfile.mkdtemp(prefix="katib-amd-bench-")
+    m = Manager(state_dir=state, num_devices=n_gpus, journal=False)
+    m.config.amd.slots_per_device = slots
+    m.slots = m.N.SlotPool(m.n_devices, slots)
+    if not n_gpus:  # CPU-only node: trials without GPUs
+        c = e.spec.trial_template.trial_spec["spec"]["template"]["spec"]["containers"][0]
+        c.pop("resources", None)
+    t0 = time.time()
+    m.create_experiment(e)
+    done = m.run_until_complete(e.metadata.name, timeout=3 * 3600)
+    wall = time.time() - t0
+    st = done.status
+    completed = sum(int(x or 0) for x in (st.trials_succeeded, st.trials_failed, st.trials_early_stopped,
+                                           st.trials_killed))
+    best = st.current_optimal_trial
+    best_acc = None
+    if best is not None and best.observation is not None:
+        for mt in best.observation.metrics or []:
+            if mt.name == e.spec.objective.objective_metric_name:
+                best_acc = float(mt.max)
+    per_trial = []
+    for t in m.list_trials(e.metadata.name):
+        a, b = t.status.start_time, t.status.completion_time
+        if a and b:
+            if isinstance(a, str):
+                from datetime import datetime
+
+                a, b = (datetime.strptime(v, "%Y-%m-%dT%H:%M:%SZ") for v in (a, b))
+            per_trial.append((b - a).total_seconds())
+    m.shutdown()
+    tph = completed / wall * 3600.0
+    print(json.dumps({
+        "metric": "completed_trials_per_hour", "value": round(tph, 1), "unit": "trials/h", "n_gpus": n_gpus,
+        "higher_is_better": True, "vs_baseline": round(tph / B1_TRIALS_PER_HOUR, 2),
+        "wall_s": round(wall, 2), "trials_completed": completed, "trials_succeeded": st.trials_succeeded,
+        "succeeded": EC.is_succeeded(done), "best_objective": best_acc,
+        "median_trial_s": sorted(per_trial)[len(per_trial) // 2] if per_trial else None,
+        "config": {"experiment": e.metadata.name, "algorithm": e.spec.algorithm.algorithm_name,
+                   "parallel": par, "max_trials": e.spec.max_trial_count, "slots_per_gpu": slots,
+                   "trial_kind": e.spec.trial_template.trial_spec.get("kind")}}))
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -47,7 +47,55 @@ def parse_args(argv):
     p.add_argument("--capture", type=int, default=1)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--impl", default="auto", choices=["auto", "hip", "module"])
+    # the reference's B1 experiment (docs/workflow-design.md:58-108) tunes these two as well
+    p.add_argument("--num-layers", type=int, default=0,
+                   help="hidden layers of width --hidden (0: the 784-h-h/2-10 net of the fused HIP path)")
+    p.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "ftrl"])
     return p.parse_args(argv)
+
+
+class DeepMLP(torch.nn.Module):
+    """784 -> hidden x num_layers -> 10 (the B1 experiment's ``num-layers``)."""
+
+    def __init__(self, hidden: int, num_layers: int):
+        super().__init__()
+        dims = [784] + [hidden] * num_layers
+        self.hidden = torch.nn.ModuleList(torch.nn.Linear(a, b) for a, b in zip(dims[:-1], dims[1:]))
+        self.out = torch.nn.Linear(dims[-1], 10)
+
+    def forward(self, x):
+        for fc in self.hidden:
+            x = F.relu(fc(x))
+        return self.out(x)
+
+
+class Ftrl(torch.optim.Optimizer):
+    """FTRL-proximal (McMahan et al. 2013) as MXNet's ``Ftrl`` optimizer - the B1 experiment's
+    third optimizer choice: z += g - (sqrt(n + g^2) - sqrt(n)) / lr * w; n += g^2;
+    w = (sign(z) * l1 - z) / ((beta + sqrt(n)) / lr + wd) where |z| > l1, else 0. Tensor ops only,
+    so the step is HIP-graph capturable."""
+
+    def __init__(self, params, lr=0.1, lamda1=0.01, beta=1.0, weight_decay=0.0):
+        super().__init__(params, dict(lr=lr, lamda1=lamda1, beta=beta, weight_decay=weight_decay))
+        for g in self.param_groups:
+            for p in g["params"]:
+                st = self.state[p]
+                st["z"] = torch.zeros_like(p)
+                st["n"] = torch.zeros_like(p)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        for g in self.param_groups:
+            lr, l1, beta, wd = g["lr"], g["lamda1"], g["beta"], g["weight_decay"]
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                z, n, grad = st["z"], st["n"], p.grad
+                sq_old = n.sqrt()
+                n.addcmul_(grad, grad)
+                z.add_(grad).sub_((n.sqrt() - sq_old) / lr * p)
+                p.copy_((torch.sign(z) * l1 - z) / ((beta + n.sqrt()) / lr + wd) * (z.abs() > l1))
 
 
 class MLP(torch.nn.Module):
@@ -124,37 +172,56 @@ def main(argv=None):
     x, y = teacher_vectors(args.num_train + args.num_valid, seed=1234, dev=dev)
     tx, ty = x[:args.num_train], y[:args.num_train]
     vx, vy = x[args.num_train:], y[args.num_train:]
-    model = MLP(args.hidden).to(dev)
-    impl = args.impl if args.impl != "auto" else ("hip" if dev.type == "cuda" else "module")
+    custom = args.num_layers > 0 or args.optimizer != "sgd"
+    model = (DeepMLP(args.hidden, args.num_layers or 2) if custom else MLP(args.hidden)).to(dev)
+    impl = args.impl if args.impl != "auto" else ("hip" if dev.type == "cuda" and not custom else "module")
     if impl == "hip":
+        if custom:
+            raise SystemExit("--impl hip runs the 784-h-h/2-10 net with SGD only")
         return _main_hip(args, dev, model, tx, ty, vx, vy)
-    opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=args.momentum)
+    if args.optimizer == "adam":
+        opt = torch.optim.Adam(model.parameters(), lr=args.lr, capturable=dev.type == "cuda")
+    elif args.optimizer == "ftrl":
+        opt = Ftrl(model.parameters(), lr=args.lr)
+    else:
+        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=args.momentum)
     bs = max(1, min(args.batch_size, args.num_train))
     steps = args.num_train // bs
     amp = args.dtype == "bf16" and dev.type == "cuda"
     idx = torch.zeros(bs, dtype=torch.long, device=dev)
     loss_buf = torch.zeros((), device=dev)
+    correct_buf = torch.zeros((), device=dev)
 
     def train_step():
         xb, yb = tx.index_select(0, idx), ty.index_select(0, idx)
         with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=amp):
-            loss = F.cross_entropy(model(xb), yb)
+            logits = model(xb)
+            loss = F.cross_entropy(logits, yb)
         opt.zero_grad(set_to_none=False)
         loss.backward()
         opt.step()
         loss_buf.add_(loss.detach())
+        correct_buf.add_((logits.detach().argmax(1) == yb).sum())
         return loss_buf
 
     step = CapturedStep(train_step, enabled=bool(args.capture))
     # zero grads exist before capture (set_to_none=False keeps the same buffers)
     for p_ in model.parameters():
         p_.grad = torch.zeros_like(p_)
+    if args.optimizer == "adam" and dev.type == "cuda":  # capturable Adam: state on the device before capture
+        opt.step()
+        with torch.no_grad():
+            for p_, st in opt.state.items():
+                for v in st.values():
+                    if torch.is_tensor(v):
+                        v.zero_()
     gen = torch.Generator(device=dev).manual_seed(args.seed)
     timer = Timer()
     acc = 0.0
     for epoch in range(args.epochs):
         perm = torch.randperm(args.num_train, device=dev, generator=gen)[:steps * bs].view(steps, bs)
         loss_buf.zero_()
+        correct_buf.zero_()
         for s in range(steps):
             idx.copy_(perm[s])
             step()
@@ -164,7 +231,8 @@ def main(argv=None):
         loss = float(loss_buf) / max(steps, 1)
         if not math.isfinite(loss):
             loss = float("nan")
-        report(epoch=epoch, loss=loss, **{"Validation-accuracy": acc})
+        report(epoch=epoch, loss=loss, **{"Validation-accuracy": acc,
+                                         "Train-accuracy": float(correct_buf) / max(steps * bs, 1)})
     report(**{"train_seconds": timer.elapsed()})
     return acc
 

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- \
-  python3 bench.py --steps 2 --warmup 1 --capture 0 --valid-batches 1 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
+  python3 bench.py --steps 2 --warmup 1 --capture 0 --valid-batches 1 --trials 0 --b1 0 --comparator-steps 0 --full-search 0 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- \
-  python3 bench.py --steps 2 --warmup 1 --capture 0 --valid-batches 1 > gpurun_out/pmc_write.log 2>&1 || exit $?
+  python3 bench.py --steps 2 --warmup 1 --capture 0 --valid-batches 1 --trials 0 --b1 0 --comparator-steps 0 --full-search 0 > gpurun_out/pmc_write.log 2>&1 || exit $?
 python3 scripts/pmc_bw.py gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/darts_b5_bw.txt || exit 1

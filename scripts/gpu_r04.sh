@@ -26,12 +26,12 @@ for s in "$@"; do
       step pytest-gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider || exit 1
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench) step bench 600 python bench.py || exit 1 ;;
-    quick) step quick 300 python bench.py --trials 0 --comparator-steps 0 --full-search 0 || exit 1 ;;
-    default) step default 400 python bench.py --config default --steps 10 --warmup 3 --trials 0 --comparator-steps 0 --full-search 0 || exit 1 ;;
+    quick) step quick 300 python bench.py --trials 0 --b1 0 --comparator-steps 0 --full-search 0 || exit 1 ;;
+    default) step default 400 python bench.py --config default --steps 10 --warmup 3 --trials 0 --b1 0 --comparator-steps 0 --full-search 0 || exit 1 ;;
     tl)
       rm -rf gpurun_out/prof_tl
       step tl 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_tl -o run -- \
-        python3 bench.py --steps 10 --warmup 3 --trials 0 --comparator-steps 0 --full-search 0 || exit 1
+        python3 bench.py --steps 10 --warmup 3 --trials 0 --b1 0 --comparator-steps 0 --full-search 0 || exit 1
       f=$(find gpurun_out/prof_tl -name '*kernel_trace.csv' | head -n 1)
       python3 scripts/prof_timeline.py "$f" virtual_step_kernel 5 > gpurun_out/darts_b5_timeline.txt || exit 1
       python3 scripts/prof_sequence.py "$f" virtual_step_kernel > gpurun_out/darts_b5_sequence.txt 2>&1 || true

@@ -34,8 +34,11 @@ def main():
         data.append([t.to(dev) for t in (tx, ty, vx, vy)])
     dp = DartsSearch(layout, dev, comm, seed=3, capture=True, sync_bn=sync)
     sl = slice(r * B // W, (r + 1) * B // W)
-    for tx, ty, vx, vy in data:
+    W1 = None
+    for i, (tx, ty, vx, vy) in enumerate(data):
         dp.step(tx[sl], ty[sl], vx[sl], vy[sl])
+        if i == 0:
+            W1 = dp.W.cpu()
     torch.cuda.synchronize()
     if comm.xgmi is not None:
         comm.xgmi.check()
@@ -45,10 +48,20 @@ def main():
     if r == 0:
         single = DartsSearch(layout, dev, Comm(device=dev), seed=3, capture=True)
         A0 = single.A.clone()
-        for tx, ty, vx, vy in data:
+        dW1 = None
+        for i, (tx, ty, vx, vy) in enumerate(data):
             single.step(tx, ty, vx, vy)
+            if i == 0:
+                dW1 = float((W1 - single.W.cpu()).abs().max())
         torch.cuda.synchronize()
-        out = {"dW": float((res["W"] - single.W.cpu()).abs().max()), "W_scale": float(single.W.abs().max()),
+        # run-to-run noise of the single-process search itself (float atomics: summation order
+        # varies between runs; Adam turns near-zero alpha gradients' rounding into O(lr) steps)
+        again = DartsSearch(layout, dev, Comm(device=dev), seed=3, capture=True)
+        for tx, ty, vx, vy in data:
+            again.step(tx, ty, vx, vy)
+        torch.cuda.synchronize()
+        out = {"dA_ss": float((again.A - single.A).abs().max()), "dW_ss": float((again.W - single.W).abs().max()),
+               "dW1": dW1, "dW": float((res["W"] - single.W.cpu()).abs().max()), "W_scale": float(single.W.abs().max()),
                "dA": float((res["A"] - single.A.cpu()).abs().max()),
                "A_disp": float((single.A - A0).abs().max()), "dBN": float((res["bn"] - single.bn.mean.cpu()).abs().max()),
                "geno_equal": res["geno"] == str(single.genotype()), "loss_dp": res["loss"],

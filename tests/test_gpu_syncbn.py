@@ -39,8 +39,12 @@ def test_gpu_syncbn_two_ranks_match_single_process():
     print(res)
     assert res["capture"] and res["allreduce"] == "xgmi", res
     assert res["geno_equal"], res
-    assert res["dA"] <= 0.05 * res["A_disp"], res
-    assert res["dW"] <= 1e-3 * max(1.0, res["W_scale"]), res
+    # alpha drift within 5 % of the alphas' displacement, or within 3x the single-process search's
+    # own run-to-run spread (float-atomic summation order)
+    assert res["dA"] <= max(0.05 * res["A_disp"], 3 * res["dA_ss"]), res
+    # after one step the two are the same computation up to fp32 summation order; over 30 steps of
+    # the search (lr 0.025, momentum 0.9) rounding differences grow, per-rank BN diverges far more
+    assert res["dW1"] <= 1e-5 * max(1.0, res["W_scale"]), res
     per_rank = _run(False)
     print(per_rank)
-    assert per_rank["dA"] > 2 * res["dA"], (per_rank, res)
+    assert per_rank["dW1"] > 10 * max(res["dW1"], 1e-7), (per_rank, res)
