@@ -60,7 +60,8 @@ def main():
         for tx, ty, vx, vy in data:
             again.step(tx, ty, vx, vy)
         torch.cuda.synchronize()
-        out = {"dA_ss": float((again.A - single.A).abs().max()), "dW_ss": float((again.W - single.W).abs().max()),
+        out = {"geno_ss_equal": str(again.genotype()) == str(single.genotype()),
+               "dA_ss": float((again.A - single.A).abs().max()), "dW_ss": float((again.W - single.W).abs().max()),
                "dW1": dW1, "dW": float((res["W"] - single.W.cpu()).abs().max()), "W_scale": float(single.W.abs().max()),
                "dA": float((res["A"] - single.A.cpu()).abs().max()),
                "A_disp": float((single.A - A0).abs().max()), "dBN": float((res["bn"] - single.bn.mean.cpu()).abs().max()),
