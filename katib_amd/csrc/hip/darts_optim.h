@@ -45,6 +45,13 @@ void launch_virtual_step(const VirtualStepArgs& a, hipStream_t st);
 // phase 0: eps = 0.01 / sqrt(sum parts) -> *eps; w += d * eps; ga = 0
 // phase 1: w -= d * (2 eps); gap = ga; ga = 0
 // phase 2: w += d * eps; alpha_grad = gav - lr * (gap - ga) / (2 eps)
+//          [+ BN running statistics of the two concurrent passes merged, below]
+// Concurrent form (the +eps and -eps passes as two independent graph branches):
+// phase 3: eps -> *eps; wp = w + d * eps; wm = wp - d * (2 eps) (the sequential rounding);
+//          ga = gap = 0; bn_plus = bn_zero = bn (running stats [mean | var], nbn floats)
+// phase 2 with n = 0 then leaves w alone and, when nbn > 0, sets
+//          bn = (1 - m) * bn_plus + bn - (1 - m) * bn_zero
+//          = the two sequential momentum updates (+ pass on bn_plus, - pass on bn, both from r0)
 struct HessianArgs {
   float* w;
   const float* d;     // dw' (virtual weight gradient)
@@ -59,6 +66,13 @@ struct HessianArgs {
   const float* lr;
   int na;
   int phase;
+  float* wp = nullptr;       // phase 3 outputs
+  float* wm = nullptr;
+  float* bn = nullptr;       // running statistics merged in phase 2 / snapshotted in phase 3
+  float* bn_plus = nullptr;
+  float* bn_zero = nullptr;
+  int nbn = 0;
+  float bn_momentum = 0.1f;
 };
 void launch_hessian(const HessianArgs& a, hipStream_t st);
 

@@ -74,6 +74,30 @@ __global__ void __launch_bounds__(kThreads) virtual_step_kernel(VirtualStepArgs 
 
 __global__ void __launch_bounds__(kThreads) hessian_kernel(HessianArgs a) {
   float eps;
+  const int stride = gridDim.x * kThreads, i0 = blockIdx.x * kThreads + threadIdx.x;
+  if (a.phase == 3) {  // concurrent form: both perturbed weight vectors at once, w untouched
+    eps = __fdiv_rn(0.01f, static_cast<float>(sqrt(total_of(a.parts, a.nparts))));
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.eps = eps;
+    const float m2 = -__fmul_rn(2.0f, eps);
+    for (int i = i0; i < a.n; i += stride) {
+      const float wp = __fadd_rn(a.w[i], __fmul_rn(a.d[i], eps));
+      a.wp[i] = wp;
+      a.wm[i] = __fadd_rn(wp, __fmul_rn(a.d[i], m2));
+    }
+    for (int i = i0; i < a.nbn; i += stride) {
+      const float v = a.bn[i];
+      a.bn_plus[i] = v;
+      a.bn_zero[i] = v;
+    }
+    if (blockIdx.x == 0)
+      for (int i = threadIdx.x; i < a.na; i += kThreads) a.ga[i] = a.gap[i] = 0.0f;
+    return;
+  }
+  if (a.phase == 2 && a.nbn > 0) {
+    const float k = 1.0f - a.bn_momentum;
+    for (int i = i0; i < a.nbn; i += stride)
+      a.bn[i] = __fsub_rn(__fadd_rn(__fmul_rn(k, a.bn_plus[i]), a.bn[i]), __fmul_rn(k, a.bn_zero[i]));
+  }
   if (a.phase == 0) {
     const float norm = static_cast<float>(sqrt(total_of(a.parts, a.nparts)));
     eps = __fdiv_rn(0.01f, norm);
@@ -147,7 +171,7 @@ void launch_virtual_step(const VirtualStepArgs& a, hipStream_t st) {
 }
 
 void launch_hessian(const HessianArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(hessian_kernel, dim3(grid_for(a.n)), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(hessian_kernel, dim3(grid_for(std::max(a.n, a.nbn))), dim3(kThreads), 0, st, a);
 }
 
 void launch_adam(const AdamArgs& a, hipStream_t st) {

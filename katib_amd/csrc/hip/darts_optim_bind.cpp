@@ -82,6 +82,39 @@ void hessian(int phase, const Tensor& w, const Tensor& d, const Tensor& eps, con
   O_::launch_hessian(p, stream());
 }
 
+// concurrent Hessian passes: phase 3 (wp, wm, eps, zeroed alpha accumulators, BN snapshots) and
+// the final phase 2 without a weight update (alpha gradient + merged BN running statistics)
+void hessian_split(int phase, const Tensor& w, const Tensor& d, const Tensor& eps, const Tensor& parts, int nparts,
+                   const Tensor& ga, const Tensor& gap, const Tensor& gav, const Tensor& alpha_grad, const Tensor& lr,
+                   const Tensor& wp, const Tensor& wm, const Tensor& bn, const Tensor& bn_plus, const Tensor& bn_zero,
+                   double momentum) {
+  TORCH_CHECK(phase == 2 || phase == 3, "hessian_split: phase must be 3 (split) or 2 (merge)");
+  TORCH_CHECK(nparts >= 1 && nparts <= O_::kMaxParts, "hessian_split: bad partial count");
+  const int64_t n = w.numel(), na = ga.numel(), nbn = bn.numel();
+  O_::HessianArgs p;
+  p.w = f32(w, "w", n, w);
+  p.d = f32(d, "d", n, w);
+  p.n = phase == 3 ? static_cast<int>(n) : 0;
+  p.eps = f32(eps, "eps", 1, w);
+  p.parts = parts_ptr(parts, w);
+  p.nparts = nparts;
+  p.ga = f32(ga, "ga", na, w);
+  p.gap = f32(gap, "gap", na, w);
+  p.gav = f32(gav, "gav", na, w);
+  p.alpha_grad = f32(alpha_grad, "alpha_grad", na, w);
+  p.lr = f32(lr, "lr", 1, w);
+  p.na = static_cast<int>(na);
+  p.phase = phase;
+  p.wp = f32(wp, "wp", n, w);
+  p.wm = f32(wm, "wm", n, w);
+  p.bn = f32(bn, "bn", nbn, w);
+  p.bn_plus = f32(bn_plus, "bn_plus", nbn, w);
+  p.bn_zero = f32(bn_zero, "bn_zero", nbn, w);
+  p.nbn = static_cast<int>(nbn);
+  p.bn_momentum = static_cast<float>(momentum);
+  O_::launch_hessian(p, stream());
+}
+
 void adam(const Tensor& a, const Tensor& grad, const Tensor& m, const Tensor& v, const Tensor& t, double lr, double b1,
           double b2, double wd, double eps, const Tensor& zero) {
   const int64_t n = a.numel();
@@ -127,6 +160,8 @@ void register_darts_optim(py::module& m) {
   m.attr("OPTIM_MAX_PARTS") = O_::kMaxParts;
   m.def("optim_sumsq", &sumsq, "fp64 sum-of-squares partials (one per workgroup); returns the partial count");
   m.def("optim_virtual_step", &virtual_step, "architect virtual step w' = w - lr (mu m + g + wd w), alpha' = alpha");
+  m.def("optim_hessian_split", &hessian_split,
+        "concurrent finite-difference Hessian passes: split (phase 3) / merge (phase 2)");
   m.def("optim_hessian", &hessian, "finite-difference Hessian perturbation phase 0/1/2");
   m.def("optim_adam", &adam, "Adam (L2 weight decay) on the architecture weights, device step counter");
   m.def("optim_sgd_clip", &sgd_clip, "global-norm clip + momentum SGD with weight decay");

@@ -212,8 +212,11 @@ class BNState:
         for _, c, _ in layout.bn:
             self.offsets.append((off, c))
             off += c
-        self.mean = torch.zeros(off, device=device, dtype=dtype)
-        self.var = torch.ones(off, device=device, dtype=dtype)
+        # one buffer [mean | var]: a kernel can snapshot / merge all running statistics at once
+        self.buf = torch.zeros(2 * off, device=device, dtype=dtype)
+        self.buf[off:] = 1.0
+        self.mean = self.buf[:off]
+        self.var = self.buf[off:]
         self.index = layout.bn_index
 
     def get(self, name):
@@ -221,8 +224,7 @@ class BNState:
         return self.mean[o:o + c], self.var[o:o + c]
 
     def copy_(self, other: "BNState"):
-        self.mean.copy_(other.mean)
-        self.var.copy_(other.var)
+        self.buf.copy_(other.buf)
 
 
 # ----------------------------------------------------------------------------- network

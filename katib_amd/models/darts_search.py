@@ -125,6 +125,21 @@ class DartsSearch:
         self.Aw, self.gAw = self._alpha_leaves(self.A, self.gA)
         self.Avw, _ = self._alpha_leaves(self.Av, self.gAv)
         self.W_detached = layout.views(self.W.detach())
+        # concurrent finite-difference Hessian passes (HIP path): w + eps dw' and w - eps dw' as
+        # two independent graph branches - their own weight copies, alpha-gradient leaves and BN
+        # running statistics, merged by one kernel after the join (KATIB_DARTS_HESS_CONCURRENT=0:
+        # the sequential in-place perturbation)
+        self.hess_concurrent = (self.device.type == "cuda" and self.hd is not None
+                                and __import__("os").environ.get("KATIB_DARTS_HESS_CONCURRENT", "1") != "0")
+        if self.hess_concurrent:
+            self.Wp = torch.empty_like(self.W)
+            self.Wm = torch.empty_like(self.W)
+            self.Wp_views = layout.views(self.Wp)
+            self.Wm_views = layout.views(self.Wm)
+            self.Aw_p, _ = self._alpha_leaves(self.A, self.gAp)
+            self.bn_plus = BNState(layout, dev)
+            self.bn_zero = BNState(layout, dev)
+            self._side = torch.cuda.Stream(device=dev)
         # fused optimizer kernels (csrc/hip/darts_optim.hip) on the HIP path:
         # virtual step, Hessian perturbations, Adam on alphas and clipped SGD are one launch each
         self.K = self.hd._K if self.hd is not None else None
@@ -184,6 +199,24 @@ class DartsSearch:
 
     def _seg_hessian(self, tx, ty):
         """+/- eps perturbations, FWD3/BWD3 and FWD4/BWD4 w.r.t. alphas only."""
+        if self.K is not None and self.hess_concurrent:
+            K, args = self.K, (self.eps, self._parts)
+            nparts = K.optim_sumsq(self.gWv, self._parts)
+            tail = (self.gA, self.gAp, self.gAv, self.alpha_grad, self.lr, self.Wp, self.Wm, self.bn.buf,
+                    self.bn_plus.buf, self.bn_zero.buf, self.net.momentum)
+            # eps = 0.01/||dw'||; Wp = w + eps dw', Wm = Wp - 2 eps dw'; zeroed d(alpha)+-; BN snapshots
+            K.optim_hessian_split(3, self.W, self.gWv, *args, nparts, *tail)
+            main = torch.cuda.current_stream()
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):  # the +eps pass on its own branch
+                loss, _ = self._loss(tx, ty, self.Wp_views, *self._arch(self.Aw_p), self.bn_plus)
+                loss.backward(inputs=self.Aw_p)
+            loss, _ = self._loss(tx, ty, self.Wm_views, *self._arch(self.Aw), self.bn)
+            loss.backward(inputs=self.Aw)
+            main.wait_stream(self._side)
+            # alpha grad = d(alpha) - xi (d+ - d-) / (2 eps); BN running stats as after both sequential passes
+            K.optim_hessian_split(2, self.W, self.gWv, *args, nparts, *tail)
+            return
         if self.K is not None:
             K, args = self.K, (self.eps, self._parts)
             nparts = K.optim_sumsq(self.gWv, self._parts)
