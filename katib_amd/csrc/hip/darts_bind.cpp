@@ -287,7 +287,11 @@ void pw_fwd(std::vector<py::tuple> calls, int64_t S) {
     OptT stats = t[3].cast<OptT>();
     const int co_off = t[4].cast<int>(), off = t[5].cast<int>();
     check_f32(x, "x"); check_f32(pw, "pw"); check_z(z, "z");
-    const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+    // a 5-D x is node-major [nodes][N][C / nodes][H][W] (a DARTS cell output kept as its nodes' buffers)
+    const bool nm = x.dim() == 5;
+    const int xnodes = nm ? x.size(0) : 1;
+    const int N = nm ? x.size(1) : x.size(0), Cin = nm ? x.size(0) * x.size(2) : x.size(1);
+    const int H = x.size(nm ? 3 : 2), W = x.size(nm ? 4 : 3);
     const int Cout = pw.size(0), Ho = z.size(2), Wo = z.size(3);
     TORCH_CHECK(pw.size(1) == Cin && co_off + Cout <= z.size(1) && z.size(0) == N, "pw shapes");
     TORCH_CHECK((Ho * Wo) % 64 == 0, "Ho*Wo must be a multiple of 64");
@@ -298,7 +302,7 @@ void pw_fwd(std::vector<py::tuple> calls, int64_t S) {
     if (a.stats)
       TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= kRep * 2 * z.size(1), "stats [kRep][2Ctot]");
     a.N = N; a.Cin = Cin; a.Cout = Cout; a.CoutTotal = z.size(1); a.co_off = co_off;
-    a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off; a.relu = 1;
+    a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.S = S; a.off = off; a.relu = 1; a.xnodes = xnodes;
     SAME_SHAPE(bt, N); SAME_SHAPE(bt, Cin); SAME_SHAPE(bt, Cout); SAME_SHAPE(bt, Ho); SAME_SHAPE(bt, Wo);
   }
   tail_begin(bt.tail);
@@ -479,7 +483,15 @@ void pw_bwd(std::vector<py::tuple> calls, int64_t S, int64_t mode, bool need_dx)
     a.gs = make_gs(gs, a.CoutTotal);
     a.Cin = Cin; a.Cout = Cout; a.co_off = co_off; a.S = S; a.off = off; a.mode = mode;
     a.need_dx = need_dx;
-    a.H = x.size(2); a.W = x.size(3);
+    // mode 1 with a 5-D x: node-major [nodes][N][Cin / nodes][H][W] input and input gradient
+    const bool nm = mode != 0 && x.dim() == 5;
+    a.xnodes = nm ? x.size(0) : 1;
+    a.H = x.size(nm ? 3 : 2); a.W = x.size(nm ? 4 : 3);
+    if (mode != 0) {
+      TORCH_CHECK(x.numel() == (int64_t)a.N * Cin * a.H * a.W && (!nm || x.size(1) == a.N),
+                  "pw_bwd: x must be [N][Cin][H][W] or node-major [nodes][N][Cin/nodes][H][W]");
+      if (gx.has_value() && gx->defined()) TORCH_CHECK(gx->sizes() == x.sizes(), "pw_bwd: gx must have the shape of x");
+    }
     TORCH_CHECK(Cin * Cout <= 8192, "pw_bwd supports Cin*Cout <= 8192");
     TORCH_CHECK((a.Ho * a.Wo) % 64 == 0, "Ho*Wo % 64");
     a.pw = pw.data_ptr<float>(); a.x = mode != 0 ? x.data_ptr<float>() : nullptr;

@@ -32,6 +32,7 @@ struct FwdArgs {
   float* dl;          // [N][K]
   float* loss_n;      // [N]
   int N, C, HW, K;
+  int nodes = 1;      // > 1: x is node-major [nodes][N][C / nodes][HW] (a DARTS cell output, never concatenated)
 };
 void launch_fwd(const FwdArgs& a, hipStream_t st);
 void launch_loss(const float* loss_n, int N, float* loss, hipStream_t st);
@@ -47,6 +48,7 @@ struct BwdArgs {
   float* gb;
   int gb_stride;
   int N, C, HW, K;
+  int nodes = 1;      // dx layout, as FwdArgs::nodes
 };
 void launch_bwd(const BwdArgs& a, hipStream_t st);
 

@@ -25,7 +25,6 @@ __global__ void __launch_bounds__(kThreads) head_fwd_kernel(FwdArgs a) {
   __shared__ float sl[kMaxK];
   const int n = blockIdx.x, lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
   const float inv_hw = 1.0f / a.HW;
-  const float* xn = a.x + (size_t)n * a.C * a.HW;
   // kU channels per wave in flight: all loads issue before the first reduction (the chain of
   // one load -> wave sum per channel was latency-bound)
   for (int c0 = wid; c0 < a.C; c0 += kWaves * kU) {
@@ -34,15 +33,17 @@ __global__ void __launch_bounds__(kThreads) head_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int c = c0 + u * kWaves;
-        s[u] = (c < a.C && lane < a.HW) ? xn[(size_t)c * a.HW + lane] : 0.0f;
+        s[u] = (c < a.C && lane < a.HW) ? a.x[plane_off(n, c, a.N, a.C, a.nodes, a.HW) + lane] : 0.0f;
       }
     } else {
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int c = c0 + u * kWaves;
         float v = 0.0f;
-        if (c < a.C)
-          for (int p = lane; p < a.HW; p += kWave) v += xn[(size_t)c * a.HW + p];
+        if (c < a.C) {
+          const float* xc = a.x + plane_off(n, c, a.N, a.C, a.nodes, a.HW);
+          for (int p = lane; p < a.HW; p += kWave) v += xc[p];
+        }
         s[u] = v;
       }
     }
@@ -122,12 +123,12 @@ __global__ void __launch_bounds__(kThreads) head_bwd_kernel(BwdArgs a) {
   __syncthreads();
   if (a.dx != nullptr) {
     const float inv_hw = 1.0f / a.HW;
-    float* dxn = a.dx + (size_t)n * a.C * a.HW;
     for (int c = wid; c < a.C; c += kWaves) {
       float d = 0.0f;
       for (int k = 0; k < a.K; ++k) d += sd[k] * a.w[(size_t)k * a.C + c];
       d *= inv_hw;
-      for (int p = lane; p < a.HW; p += kWave) dxn[(size_t)c * a.HW + p] = d;
+      float* dxc = a.dx + plane_off(n, c, a.N, a.C, a.nodes, a.HW);
+      for (int p = lane; p < a.HW; p += kWave) dxc[p] = d;
     }
   }
   const int rep = n % kRep;

@@ -25,14 +25,17 @@ float* f32(const Tensor& t, const char* name, std::initializer_list<int64_t> sha
 }
 
 struct Dims {
-  int N, C, HW, K;
+  int N, C, HW, K, nodes;
 };
 
+// x: [N][C][H][W], or node-major [nodes][N][C / nodes][H][W] (a DARTS cell output kept as its nodes)
 Dims dims_of(const Tensor& x, const Tensor& w) {
-  TORCH_CHECK(x.dim() == 4, "head: x must be [N][C][H][W]");
-  TORCH_CHECK(w.dim() == 2 && w.size(1) == x.size(1), "head: w must be [K][C]");
-  Dims d{static_cast<int>(x.size(0)), static_cast<int>(x.size(1)), static_cast<int>(x.size(2) * x.size(3)),
-         static_cast<int>(w.size(0))};
+  TORCH_CHECK(x.dim() == 4 || x.dim() == 5, "head: x must be [N][C][H][W] or node-major [nodes][N][C/nodes][H][W]");
+  const bool nm = x.dim() == 5;
+  Dims d{static_cast<int>(nm ? x.size(1) : x.size(0)), static_cast<int>(nm ? x.size(0) * x.size(2) : x.size(1)),
+         static_cast<int>(nm ? x.size(3) * x.size(4) : x.size(2) * x.size(3)), static_cast<int>(w.size(0)),
+         static_cast<int>(nm ? x.size(0) : 1)};
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == d.C, "head: w must be [K][C]");
   TORCH_CHECK(d.N >= 1 && d.C >= 1 && d.HW >= 1 && d.K >= 1, "head: empty operand");
   TORCH_CHECK(d.C <= H_::kMaxC && d.K <= H_::kMaxK, "head: C must be <= ", H_::kMaxC, " and K <= ", H_::kMaxK);
   TORCH_CHECK(x.numel() < (int64_t(1) << 31), "head: x too large");
@@ -43,7 +46,9 @@ void fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y, con
          const Tensor& logits, const Tensor& dl, const Tensor& loss_n) {
   const Dims d = dims_of(x, w);
   H_::FwdArgs a;
-  a.x = f32(x, "x", {d.N, d.C, x.size(2), x.size(3)}, x);
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "head: x must be contiguous fp32");
+  a.x = x.data_ptr<float>();
+  a.nodes = d.nodes;
   a.w = f32(w, "w", {d.K, d.C}, x);
   a.b = f32(b, "b", {d.K}, x);
   TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kLong && y.is_contiguous() && y.dim() == 1 && y.size(0) == d.N &&
@@ -77,7 +82,13 @@ void bwd(const Tensor& x_like, const Tensor& dl, const Tensor& pooled, const Ten
   a.w = f32(w, "w", {d.K, d.C}, x_like);
   TORCH_CHECK(gout.numel() == 1, "head: upstream gradient must be a scalar");
   a.gout = f32(gout, "gout", {}, x_like);
-  a.dx = dx ? f32(*dx, "dx", {d.N, d.C, x_like.size(2), x_like.size(3)}, x_like) : nullptr;
+  if (dx) {
+    TORCH_CHECK(dx->is_cuda() && dx->scalar_type() == at::kFloat && dx->is_contiguous() &&
+                    dx->sizes() == x_like.sizes() && dx->device() == x_like.device(),
+                "head: dx must be a contiguous fp32 tensor shaped like x");
+  }
+  a.dx = dx ? dx->data_ptr<float>() : nullptr;
+  a.nodes = d.nodes;
   // replicated gradient rows: replica r at + r * stride, kRep rows must fit the buffer the view lives in
   auto rep_ptr = [&](const std::optional<Tensor>& g, int64_t stride, int64_t numel, const char* name) -> float* {
     if (!g) return nullptr;

@@ -35,6 +35,14 @@ __device__ __forceinline__ void zst4(__hip_bfloat16* p, zf4 v) {
   *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(b);
 }
 
+// Offset of channel plane (n, c) of an [N][C][HW] tensor, or of a node-major one
+// ([nodes][N][C / nodes][HW]: a DARTS cell output kept as its nodes' buffers instead of a concatenation)
+__host__ __device__ __forceinline__ size_t plane_off(int n, int c, int N, int C, int nodes, size_t HW) {
+  if (nodes <= 1) return ((size_t)n * C + c) * HW;
+  const int Cn = C / nodes, k = c / Cn;
+  return (((size_t)k * N + n) * Cn + (c - k * Cn)) * HW;
+}
+
 constexpr int kMaxOps = 8;
 constexpr int kMaxC = 256;
 // Cross-workgroup sums (BN statistics, BN-backward reductions, weight gradients) go to kRep
@@ -86,6 +94,7 @@ struct PwFwdArgs {
   const float* pw; zt* z; double* stats;  // stats: kRep replicas of [2*CoutTotal]
   int N, Cin, Cout, CoutTotal, co_off, H, W, Ho, Wo, S, off;
   int relu;  // 1: input = relu(x) (StdConv / FactorizedReduce); 0: identity (pointwise half of a dw-pw stage)
+  int xnodes;  // relu: x node-major [xnodes][N][Cin / xnodes][H][W] when > 1 (a cell output kept as its nodes)
 };
 
 struct PoolFwdArgs {
@@ -113,6 +122,7 @@ struct PwBwdArgs {
   int gstride;  // floats between gW replicas (0: single accumulator)
   int N, Cin, Cout, CoutTotal, co_off, H, W, Ho, Wo, S, off, mode, need_dx;
   int overwrite;  // mode 1, stride 1: gx = masked grad instead of += (the kernel covers every pixel)
+  int xnodes;     // mode 1: x and gx node-major [xnodes][N][Cin / xnodes][H][W] (> 1)
 };
 
 struct DwBwdArgs {

@@ -628,15 +628,15 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
       const int ci = 4 * k + q;
       f4 v;
       if (flat) {
-        const size_t o = ((size_t)n * CI + ci) * HWo + pp;
         if (a.relu) {  // node state (fp32), relu on the way in
+          const size_t o = plane_off(n, ci, a.N, CI, a.xnodes, HWo) + pp;
           v = *reinterpret_cast<const f4*>(static_cast<const float*>(a.x) + o);
           v = f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
         } else {  // depthwise output d of a wide dw-pw stage
-          v = zld4(static_cast<const zt*>(a.x) + o);
+          v = zld4(static_cast<const zt*>(a.x) + ((size_t)n * CI + ci) * HWo + pp);
         }
       } else if (fr2) {
-        const float* plane = static_cast<const float*>(a.x) + ((size_t)n * CI + ci) * a.H * a.W;
+        const float* plane = static_cast<const float*>(a.x) + plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W);
         float v0, v1, v2, v3;
         fr2_pair(plane, a.W, Wo, a.off, pp, v0, v1);
         fr2_pair(plane, a.W, Wo, a.off, pp + 2, v2, v3);
@@ -646,7 +646,8 @@ __global__ void __launch_bounds__(256) pw_fwd_wave_kernel(PwFwdBatch bt) {
         for (int t = 0; t < 4; ++t) {
           const int p = pp + t, oy = p / Wo, ox = p - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
           v[t] = (iy < a.H && ix < a.W)
-                     ? fmaxf(static_cast<const float*>(a.x)[(((size_t)n * CI + ci) * a.H + iy) * a.W + ix], 0.f)
+                     ? fmaxf(static_cast<const float*>(a.x)[plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W) +
+                                                             (size_t)iy * a.W + ix], 0.f)
                      : 0.f;
         }
       }
@@ -716,7 +717,8 @@ __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdBatch bt) {
       int iy = oy * a.S + a.off, ix = ox * a.S + a.off;
       float v = 0.f;
       if (iy < H && ix < W) {
-        const size_t xi = (((size_t)n * Cin + ci) * H + iy) * W + ix;
+        const size_t xi = a.relu ? plane_off(n, ci, a.N, Cin, a.xnodes, (size_t)H * W) + (size_t)iy * W + ix
+                                 : (((size_t)n * Cin + ci) * H + iy) * W + ix;
         v = a.relu ? fmaxf(static_cast<const float*>(a.x)[xi], 0.f) : z2f(static_cast<const zt*>(a.x)[xi]);
       }
       sX[i] = v;
@@ -1079,7 +1081,9 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
         v = z2f(a.ain[((size_t)n * Cin + ci) * HWo + pp]);
       } else {
         int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
-        v = (iy < a.H && ix < a.W) ? fmaxf(a.x[(((size_t)n * Cin + ci) * a.H + iy) * a.W + ix], 0.f) : 0.f;
+        v = (iy < a.H && ix < a.W)
+                ? fmaxf(a.x[plane_off(n, ci, a.N, Cin, a.xnodes, (size_t)a.H * a.W) + (size_t)iy * a.W + ix], 0.f)
+                : 0.f;
       }
       sA[ci * PS + p] = v;
     }
@@ -1137,7 +1141,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
               } else {
                 int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
                 if (iy < a.H && ix < a.W) {
-                  size_t xi = (((size_t)n * Cin + ci) * a.H + iy) * a.W + ix;
+                  size_t xi = plane_off(n, ci, a.N, Cin, a.xnodes, (size_t)a.H * a.W) + (size_t)iy * a.W + ix;
                   if (a.overwrite) a.gx[xi] = a.x[xi] > 0.f ? v : 0.f;
                   else if (a.x[xi] > 0.f) a.gx[xi] += v;
                 }
@@ -1156,7 +1160,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
           } else {
             int oy = pp / Wo, ox = pp % Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
             if (iy < a.H && ix < a.W) {
-              size_t xi = (((size_t)n * Cin + ciu) * a.H + iy) * a.W + ix;
+              size_t xi = plane_off(n, ciu, a.N, Cin, a.xnodes, (size_t)a.H * a.W) + (size_t)iy * a.W + ix;
               if (a.overwrite) a.gx[xi] = a.x[xi] > 0.f ? v : 0.f;
               else if (a.x[xi] > 0.f) a.gx[xi] += v;
             }
@@ -1243,7 +1247,7 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
       }
 #pragma unroll
       for (int c = 0; c < CI; ++c) {
-        const size_t o = ((size_t)n * CI + c) * HWo + pp;
+        const size_t o = a.mode == 0 ? ((size_t)n * CI + c) * HWo + pp : plane_off(n, c, a.N, CI, a.xnodes, HWo) + pp;
         av[c] = a.mode == 0 ? zld4(a.ain + o) : *reinterpret_cast<const f4*>(a.x + o);
         if (a.mode != 0) {
           av[c].x = fmaxf(av[c].x, 0.f);
@@ -1267,7 +1271,7 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
           f4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int co = 0; co < CO; ++co) v += wpw[co * CI + ci] * dz[co];
-          const size_t o = ((size_t)n * CI + ci) * HWo + pp;
+          const size_t o = a.mode == 0 ? ((size_t)n * CI + ci) * HWo + pp : plane_off(n, ci, a.N, CI, a.xnodes, HWo) + pp;
           if (a.mode == 0) {
             *reinterpret_cast<f4*>(a.dd + o) = v;
           } else {
@@ -1297,9 +1301,10 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
     } else {
       const int oy = pp / Wo, ox = pp - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
       inb = iy < a.H && ix < a.W;
-      xi0 = ((size_t)n * CI * a.H + iy) * a.W + ix;
+      xi0 = (size_t)iy * a.W + ix;  // pixel inside the channel plane (plane_off below)
 #pragma unroll
-      for (int c = 0; c < CI; ++c) av[c] = inb ? fmaxf(a.x[xi0 + (size_t)c * a.H * a.W], 0.f) : 0.f;
+      for (int c = 0; c < CI; ++c)
+        av[c] = inb ? fmaxf(a.x[plane_off(n, c, a.N, CI, a.xnodes, (size_t)a.H * a.W) + xi0], 0.f) : 0.f;
     }
     if (want_w) {
 #pragma unroll
@@ -1316,9 +1321,9 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
         if (a.mode == 0) {
           a.dd[((size_t)n * CI + ci) * HWo + pp] = v;
         } else if (a.overwrite) {  // stride 1: every input pixel is some thread's own
-          a.gx[xi0 + (size_t)ci * a.H * a.W] = av[ci] > 0.f ? v : 0.f;
+          a.gx[plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W) + xi0] = av[ci] > 0.f ? v : 0.f;
         } else if (inb && av[ci] > 0.f) {  // relu'(x): x > 0  <=>  relu(x) > 0
-          a.gx[xi0 + (size_t)ci * a.H * a.W] += v;
+          a.gx[plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W) + xi0] += v;
         }
       }
     }
@@ -1426,7 +1431,7 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
       for (int bi = 0; bi < BI; ++bi) {
         const int ci = ci0 + bi * 16 + c16;
         if (flat) {
-          const size_t so = ((size_t)n * CI + ci) * HWo + pq;
+          const size_t so = a.mode == 0 ? ((size_t)n * CI + ci) * HWo + pq : plane_off(n, ci, a.N, CI, a.xnodes, HWo) + pq;
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             f4 v = a.mode == 0 ? zld4(a.ain + so + 4 * t) : *reinterpret_cast<const f4*>(a.x + so + 4 * t);
@@ -1437,14 +1442,16 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
             av[bi][4 * t + 3] = v.w;
           }
         } else if (fr2) {
-          const float* plane = a.x + ((size_t)n * CI + ci) * a.H * a.W;
+          const float* plane = a.x + plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W);
 #pragma unroll
           for (int j = 0; j < 16; j += 2) fr2_pair(plane, a.W, Wo, a.off, pq + j, av[bi][j], av[bi][j + 1]);
         } else {  // FactorizedReduce half: relu(x) at (oy*S + off, ox*S + off)
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
             const int pp = pq + j, oy = pp / Wo, ox = pp - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
-            av[bi][j] = (iy < a.H && ix < a.W) ? fmaxf(a.x[(((size_t)n * CI + ci) * a.H + iy) * a.W + ix], 0.f) : 0.f;
+            av[bi][j] = (iy < a.H && ix < a.W)
+                            ? fmaxf(a.x[plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W) + (size_t)iy * a.W + ix], 0.f)
+                            : 0.f;
           }
         }
       }
@@ -1491,7 +1498,7 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
           } else {
             const int oy = pp / Wo, ox = pp - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
             if (iy < a.H && ix < a.W) {
-              const size_t xi = (((size_t)n * CI + ci) * a.H + iy) * a.W + ix;
+              const size_t xi = plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W) + (size_t)iy * a.W + ix;
               if (a.overwrite) a.gx[xi] = a.x[xi] > 0.f ? v : 0.f;
               else if (a.x[xi] > 0.f) a.gx[xi] += v;
             }

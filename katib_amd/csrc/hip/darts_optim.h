@@ -39,6 +39,7 @@ struct VirtualStepArgs {
   float* zero_w;      // zeroed (virtual weight-gradient row), n_zero_w elements
   int n_zero_w;
   float* zero_a;      // zeroed (virtual alpha gradients), na elements
+  float* g_zero = nullptr;  // optional: g's buffer zeroed after use (the model gradient row for the next pass)
 };
 void launch_virtual_step(const VirtualStepArgs& a, hipStream_t st);
 
@@ -100,8 +101,39 @@ struct SgdArgs {
   int nparts;
   float clip, mu, wd;
   int n;
+  int zero_g = 0;  // 1: g left zeroed (for the next step's first pass) instead of holding the clipped gradient
 };
 void launch_sgd_clip(const SgdArgs& a, hipStream_t st);
+
+// Architecture-weight softmax of the DARTS network forward (model.py:147-148): softmax over the
+// primitives of every row of up to two [rows][K] alpha matrices (normal, reduce cells) in one
+// workgroup; the same launch optionally zeroes an f64 buffer (the step's BN-reduction arena), so
+// the step's first two launches become one.
+struct AlphaSoftmaxArgs {
+  const float* a[2];
+  float* w[2];
+  int rows[2];
+  int nmat, K;
+  double* zero;  // optional, nzero doubles
+  long long nzero;
+};
+void launch_alpha_softmax(const AlphaSoftmaxArgs& a, hipStream_t st);
+
+// d(loss)/d(alpha) from the edges' d(loss)/d(softmax weight) (kRep f64 replicas each, summed here)
+// through the softmax Jacobian, d alpha_k = w_k (g_k - sum_j w_j g_j), summed over every edge that
+// shares the row (cells of one type share their alphas) and written or added into the alpha
+// gradient rows: one launch replaces the replica fold, the row concatenation, the dtype copy, the
+// softmax backward and the gradient accumulation of the autograd path. Workgroup per row.
+constexpr int kAlphaGradMax = 64;
+struct AlphaGradArgs {
+  const double* g[kAlphaGradMax];
+  int rstride[kAlphaGradMax];
+  const float* w[kAlphaGradMax];   // softmax weights of the entry's row
+  float* dst[kAlphaGradMax];       // destination rows, K floats each
+  int row_start[kAlphaGradMax + 1];  // entries of destination row r: [row_start[r], row_start[r + 1])
+  int n, nrows, K, accumulate;
+};
+void launch_alpha_grad(const AlphaGradArgs& a, hipStream_t st);
 
 }  // namespace optim
 }  // namespace katib_hip

@@ -2,6 +2,7 @@
 #include <algorithm>
 
 #include "darts_optim.h"
+#include "darts_ops.h"  // kRep
 
 namespace katib_hip {
 namespace optim {
@@ -62,6 +63,7 @@ __global__ void __launch_bounds__(kThreads) virtual_step_kernel(VirtualStepArgs 
     // v = (mu * m + g) + wd * w;  w' = w + (-lr) * v   (architect.py:30-47 operation order)
     const float v = __fadd_rn(__fadd_rn(__fmul_rn(a.mom[i], a.mu), a.g[i]), __fmul_rn(w, a.wd));
     a.wv[i] = __fadd_rn(__fmul_rn(v, -lr), w);
+    if (a.g_zero) a.g_zero[i] = 0.0f;  // same thread, after its read of g[i]
   }
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < a.n_zero_w; i += stride) a.zero_w[i] = 0.0f;
   if (blockIdx.x == 0) {
@@ -151,14 +153,79 @@ __global__ void __launch_bounds__(kThreads) sgd_clip_kernel(SgdArgs a) {
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < a.n; i += gridDim.x * kThreads) {
     const float g = __fmul_rn(a.g[i], coef);
     const float w = a.w[i];
-    a.g[i] = g;
+    a.g[i] = a.zero_g ? 0.0f : g;
     const float m = __fadd_rn(__fmul_rn(a.mom[i], a.mu), __fadd_rn(g, __fmul_rn(w, a.wd)));
     a.mom[i] = m;
     a.w[i] = __fsub_rn(w, __fmul_rn(m, lr));
   }
 }
 
+__global__ void __launch_bounds__(kThreads) alpha_softmax_kernel(AlphaSoftmaxArgs a) {
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < a.nzero; i += (long long)gridDim.x * kThreads)
+    a.zero[i] = 0.0;
+  if (blockIdx.x != 0) return;
+  for (int m = 0; m < a.nmat; ++m) {
+    for (int r = threadIdx.x; r < a.rows[m]; r += kThreads) {
+      const float* x = a.a[m] + (size_t)r * a.K;
+      float mx = x[0];
+      for (int k = 1; k < a.K; ++k) mx = fmaxf(mx, x[k]);
+      float s = 0.0f;
+      for (int k = 0; k < a.K; ++k) s += expf(x[k] - mx);
+      float* w = a.w[m] + (size_t)r * a.K;
+      for (int k = 0; k < a.K; ++k) w[k] = expf(x[k] - mx) / s;
+    }
+  }
+}
+
+// one workgroup per destination row; thread (j, k) = (the row's j-th entry, primitive k): its kRep
+// replica loads all in flight at once (a thread walking them serially waited ~2000 dependent
+// memory round trips per launch), the entry's dot product over k by a 16-lane shuffle, and the
+// entries of the row summed in a fixed order (deterministic)
+__global__ void __launch_bounds__(kThreads) alpha_grad_kernel(AlphaGradArgs a) {
+  constexpr int KP = 16, EP = kThreads / KP;  // lanes per entry, entries per pass
+  __shared__ double sD[EP][KP];
+  const int r = blockIdx.x, t = threadIdx.x, j = t / KP, k = t % KP;
+  const int e0 = a.row_start[r], e1 = a.row_start[r + 1];
+  double acc = 0.0;  // thread k < K of pass-owner j == 0 accumulates the row
+  for (int base = e0; base < e1; base += EP) {
+    const int e = base + j;
+    const bool ok = e < e1 && k < a.K;
+    double g = 0.0, w = 0.0;
+    if (ok) {
+      const double* p = a.g[e] + k;
+      const int rs = a.rstride[e];
+      double v[katib_hip::kRep];
+#pragma unroll
+      for (int q = 0; q < katib_hip::kRep; ++q) v[q] = p[(size_t)q * rs];
+#pragma unroll
+      for (int q = 0; q < katib_hip::kRep; ++q) g += v[q];
+      w = (double)a.w[e][k];
+    }
+    double dot = w * g;
+#pragma unroll
+    for (int o = KP / 2; o > 0; o >>= 1) dot += __shfl_xor(dot, o, KP);
+    sD[j][k] = ok ? w * (g - dot) : 0.0;
+    __syncthreads();
+    if (t < a.K)
+      for (int jj = 0; jj < EP && base + jj < e1; ++jj) acc += sD[jj][t];
+    __syncthreads();
+  }
+  if (t < a.K) {
+    float* d = a.dst[r];
+    d[t] = a.accumulate ? d[t] + (float)acc : (float)acc;
+  }
+}
+
 }  // namespace
+
+void launch_alpha_softmax(const AlphaSoftmaxArgs& a, hipStream_t st) {
+  const int blocks = std::max(1, (int)std::min<long long>((a.nzero + kThreads - 1) / kThreads, 1024));
+  hipLaunchKernelGGL(alpha_softmax_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+}
+
+void launch_alpha_grad(const AlphaGradArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(alpha_grad_kernel, dim3(a.nrows), dim3(kThreads), 0, st, a);
+}
 
 int sumsq_parts(int n) { return std::max(1, std::min((n + kThreads * 8 - 1) / (kThreads * 8), kMaxParts)); }
 

@@ -76,7 +76,7 @@ void fwd_stats(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& 
 // weight gradient through the affine BN backward (dy = gradient of the BN output)
 void wgrad_bn(const Tensor& x, const Tensor& dy, const Tensor& z, const Tensor& red, const Tensor& stats,
               const Tensor& gamma, double eps, std::optional<Tensor> dgamma, std::optional<Tensor> dbeta,
-              const Tensor& partial, const Tensor& dw, int64_t world) {
+              const Tensor& partial, const Tensor& dw, int64_t world, bool accumulate) {
   check_shapes(x, dw);
   TORCH_CHECK(world >= 1, "stem: world must be >= 1");
   chk(dy, "dy");
@@ -115,7 +115,7 @@ void wgrad_bn(const Tensor& x, const Tensor& dy, const Tensor& z, const Tensor& 
   for (const Tensor* t : {&dy, &z, &red, &stats, &gamma, &partial})
     TORCH_CHECK(t->device() == x.device(), "stem: operands on one device");
   S_::launch_wgrad_bn(x.data_ptr<float>(), dy.data_ptr<float>(), bn, partial.data_ptr<float>(), dw.data_ptr<float>(),
-                      N, Cin, Cout, H, W, chunks, stream());
+                      N, Cin, Cout, H, W, chunks, stream(), accumulate);
 }
 
 }  // namespace
@@ -124,7 +124,8 @@ void register_stem(py::module& m) {
   m.def("stem_conv_fwd_stats", &fwd_stats, "stem conv forward + BN statistics into kRep fp64 replicas");
   m.def("stem_conv_wgrad_bn", &wgrad_bn, "stem conv weight gradient through the affine BN backward",
         py::arg("x"), py::arg("dy"), py::arg("z"), py::arg("red"), py::arg("stats"), py::arg("gamma"), py::arg("eps"),
-        py::arg("dgamma"), py::arg("dbeta"), py::arg("partial"), py::arg("dw"), py::arg("world") = 1);
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("partial"), py::arg("dw"), py::arg("world") = 1,
+        py::arg("accumulate") = false);
   m.def("stem_conv_fwd", &fwd, "direct 3x3 stem conv forward (fp32 NCHW)");
   m.def("stem_conv_wgrad", &wgrad, "stem conv weight gradient (chunk partials + fixed-order sum)");
 }

@@ -37,8 +37,9 @@ struct BnBwd {
   float* dbeta;          // nullable
   float red_scale;       // 1, or 1 / world under SyncBN (red then sums every rank's dy: d gamma / d beta stay per rank)
 };
+// accumulate: dw += the weight gradient (a registered gradient row) instead of dw =
 void launch_wgrad_bn(const float* x, const float* dy, const BnBwd& bn, float* partial, float* dw, int N, int Cin,
-                     int Cout, int H, int W, int chunks, hipStream_t s);
+                     int Cout, int H, int W, int chunks, hipStream_t s, bool accumulate = false);
 
 }  // namespace stem
 }  // namespace katib_hip

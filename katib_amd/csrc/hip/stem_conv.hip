@@ -167,13 +167,13 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const float* __res
 // one wave per weight element: lanes stride over the chunk partials, then a shuffle tree
 // (fixed order for a given chunk count -> deterministic)
 __global__ __launch_bounds__(64) void chunk_sum_kernel(const float* __restrict__ partial, float* __restrict__ out,
-                                                        int n, int chunks) {
+                                                        int n, int chunks, int accumulate) {
   const int i = blockIdx.x;
   float s = 0.f;
   for (int c = threadIdx.x; c < chunks; c += 64) s += partial[(size_t)c * n + i];
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (threadIdx.x == 0) out[i] = s;
+  if (threadIdx.x == 0) out[i] = accumulate ? out[i] + s : s;  // accumulate: into a gradient row
 }
 
 }  // namespace
@@ -190,7 +190,7 @@ namespace {
 
 template <bool BN>
 void wgrad_impl(const float* x, const float* dy, const BnBwd& bn, float* partial, float* dw, int N, int Cin, int Cout,
-                int H, int W, int chunks, hipStream_t s) {
+                int H, int W, int chunks, hipStream_t s, bool accumulate = false) {
   const int P = N * H * W;
   const int per_chunk = (P + chunks - 1) / chunks;
   if (Cin == 3)
@@ -200,7 +200,7 @@ void wgrad_impl(const float* x, const float* dy, const BnBwd& bn, float* partial
     hipLaunchKernelGGL((stem_wgrad_kernel<1, BN>), dim3(chunks, Cout), dim3(kThreads), 0, s, x, dy, bn, partial, N,
                        Cout, H, W, per_chunk);
   const int n = Cout * Cin * 9;
-  hipLaunchKernelGGL(chunk_sum_kernel, dim3(n), dim3(64), 0, s, partial, dw, n, chunks);
+  hipLaunchKernelGGL(chunk_sum_kernel, dim3(n), dim3(64), 0, s, partial, dw, n, chunks, accumulate ? 1 : 0);
 }
 
 }  // namespace
@@ -211,8 +211,8 @@ void launch_wgrad(const float* x, const float* dy, float* partial, float* dw, in
 }
 
 void launch_wgrad_bn(const float* x, const float* dy, const BnBwd& bn, float* partial, float* dw, int N, int Cin,
-                     int Cout, int H, int W, int chunks, hipStream_t s) {
-  wgrad_impl<true>(x, dy, bn, partial, dw, N, Cin, Cout, H, W, chunks, s);
+                     int Cout, int H, int W, int chunks, hipStream_t s, bool accumulate) {
+  wgrad_impl<true>(x, dy, bn, partial, dw, N, Cin, Cout, H, W, chunks, s, accumulate);
 }
 
 void launch_fwd_stats(const float* x, const float* w, float* y, double* stats, int N, int Cin, int Cout, int H, int W,

@@ -241,6 +241,9 @@ class DartsNetwork:
         # data-parallel SyncBN (a Comm): training BN statistics over every rank's batch
         # (parallel/syncbn.py; the HIP cells use ops/hip_darts.py SyncBN under DartsSearch)
         self.sync = None
+        # HIP path: the whole network as one Function (hip_darts.network_loss) instead of per-cell
+        # Functions under autograd (KATIB_DARTS_NET_FUNCTION=0: the per-cell path, A/B switch)
+        self.net_function = __import__("os").environ.get("KATIB_DARTS_NET_FUNCTION", "1") != "0"
 
     def _batch_norm(self, x, rm, rv, w, b, training):
         if training and self.sync is not None and self.sync.distributed:
@@ -368,6 +371,18 @@ class DartsNetwork:
         pool, classifier, log-softmax + NLL and their backward - is one fused HIP Function
         (hip_darts.head_loss); the returned logits carry no gradient there."""
         hd = self.ops.hip_module() if self.ops.hip_enabled(x) else None
+        if (hd is not None and self._hip_cells(hd, x) and hasattr(hd, "network_loss") and self.net_function
+                and hd.stem_supported(x, P["stem.conv"]) and P["classifier.weight"].shape[0] <= 64
+                and P["classifier.weight"].shape[1] <= 1024 and y.dtype == torch.int64 and y.dim() == 1):
+            # the whole network as ONE autograd Function (hip_darts._Network): no framework launches
+            L = self.layout
+            an = normal if torch.is_tensor(normal) else torch.cat(list(normal), 0)
+            ar = None
+            if L.has_reduce:
+                ar = reduce if torch.is_tensor(reduce) else torch.cat(list(reduce), 0)
+            spec = self._net_spec(hd)
+            return hd.network_loss(spec, x, y, [P[n] for n in spec.names], an, ar, bn.get, training, self.momentum,
+                                   self.eps)
         if hd is not None and self._hip_cells(hd, x) and hasattr(hd, "head_loss"):
             s1 = self._forward_cells(hd, x, P, normal, reduce, bn, training, features=True)
             if hd.head_supported(s1, P["classifier.weight"], y):
@@ -377,6 +392,16 @@ class DartsNetwork:
         else:
             logits = self.forward(x, P, normal, reduce, bn, training)
         return F.cross_entropy(logits, y), logits
+
+    def _net_spec(self, hd):
+        spec = self._specs.get("__net__")
+        if spec is None:
+            L = self.layout
+            spec = hd.NetSpec(("stem.conv", "stem.bn.weight", "stem.bn.bias", "stem.bn"),
+                              [self._cell_spec(hd, ci) for ci in range(len(L.cells))],
+                              [c["reduction"] for c in L.cells], ("classifier.weight", "classifier.bias"))
+            self._specs["__net__"] = spec
+        return spec
 
     def _forward_cells(self, hd, x, P, normal, reduce, bn, training, features=False):
         L = self.layout

@@ -140,11 +140,13 @@ class DartsSearch:
             self.bn_plus = BNState(layout, dev)
             self.bn_zero = BNState(layout, dev)
             self._side = torch.cuda.Stream(device=dev)
+            self._one_side = torch.ones((), device=dev)  # the side branch's own unit upstream gradient
         # fused optimizer kernels (csrc/hip/darts_optim.hip) on the HIP path:
         # virtual step, Hessian perturbations, Adam on alphas and clipped SGD are one launch each
         self.K = self.hd._K if self.hd is not None else None
         self._parts = (torch.zeros(self.K.OPTIM_MAX_PARTS, dtype=torch.float64, device=dev)
                        if self.K is not None else None)
+        self._one = None
         self.graphs = None
         self.static = None
         self._eval_graphs = {}  # (x shape, y shape, dtypes) -> (graph, static x, static y, [loss, top1, top5])
@@ -172,19 +174,28 @@ class DartsSearch:
         if self.hd is not None:
             self.hd.fold(rep)
 
+    def _backward(self, loss, inputs):
+        """loss.backward(inputs=...) with a preallocated unit upstream gradient (autograd's implicit
+        ones_like would be a fill launch per pass)."""
+        if self._one is None or self._one.device != loss.device:
+            self._one = torch.ones((), device=loss.device)
+        torch.autograd.backward(loss, grad_tensors=self._one, inputs=inputs)
+
     def _seg_virtual(self, tx, ty):
         """FWD1/BWD1 -> gW (not yet reduced)."""
-        self.gW.zero_()
+        if self.K is None:  # the fused optimizer kernels leave gW zeroed after reading it
+            self.gW.zero_()
         loss, _ = self._loss(tx, ty, self.Pw.views, *self._arch(self.Aw), self.bn)
-        loss.backward(inputs=self.Pw.list)
+        self._backward(loss, self.Pw.list)
         self._fold(self.gW_rep)
 
     def _seg_unrolled(self, vx, vy):
         """virtual step + FWD2/BWD2 -> gAv, gWv."""
         s = self.s
         if self.K is not None:  # one launch: w', alpha' and the zeroed virtual gradients
+            # ... and gW zeroed after its read: BWD5 accumulates into it next
             self.K.optim_virtual_step(self.Wv, self.W, self.mom, self.gW, self.lr, s["w_momentum"],
-                                      s["w_weight_decay"], self.Av, self.A, self.gWv, self.gAv)
+                                      s["w_weight_decay"], self.Av, self.A, self.gWv, self.gAv, True)
         else:
             with torch.no_grad():
                 # w' = w - xi*(mu*m + g + wd*w)
@@ -194,7 +205,7 @@ class DartsSearch:
             self.gWv.zero_()
             self.gAv.zero_()
         loss, _ = self._loss(vx, vy, self.Pv.views, *self._arch(self.Avw), self.bn_v)
-        loss.backward(inputs=self.Pv.list + self.Avw)
+        self._backward(loss, self.Pv.list + self.Avw)
         self._fold(self.gWv_rep)
 
     def _seg_hessian(self, tx, ty):
@@ -210,9 +221,9 @@ class DartsSearch:
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):  # the +eps pass on its own branch
                 loss, _ = self._loss(tx, ty, self.Wp_views, *self._arch(self.Aw_p), self.bn_plus)
-                loss.backward(inputs=self.Aw_p)
+                torch.autograd.backward(loss, grad_tensors=self._one_side, inputs=self.Aw_p)
             loss, _ = self._loss(tx, ty, self.Wm_views, *self._arch(self.Aw), self.bn)
-            loss.backward(inputs=self.Aw)
+            self._backward(loss, self.Aw)
             main.wait_stream(self._side)
             # alpha grad = d(alpha) - xi (d+ - d-) / (2 eps); BN running stats as after both sequential passes
             K.optim_hessian_split(2, self.W, self.gWv, *args, nparts, *tail)
@@ -267,12 +278,17 @@ class DartsSearch:
 
     def _seg_weight(self, tx, ty):
         """FWD5/BWD5 -> gW (+ alpha grads ignored), logits/loss kept for metrics."""
-        self.gW.zero_()
         if self.K is None:
+            self.gW.zero_()  # (the fused virtual step left it zeroed)
             self.gA.zero_()  # (the fused Adam launch already zeroed it)
         loss, logits = self._loss(tx, ty, self.Pw.views, *self._arch(self.Aw), self.bn)
-        loss.backward(inputs=self.Pw.list)
+        self._backward(loss, self.Pw.list)
         self._fold(self.gW_rep)
+        if self.hd is not None:
+            # keep the step's own loss / logits tensors (no copies): under graph capture their
+            # memory is fixed, so every replay refreshes them in place
+            self.loss_out, self.logits_out = loss.detach(), logits.detach()
+            return
         with torch.no_grad():
             self.loss_out.copy_(loss.detach())
             if self.logits_out is None or self.logits_out.shape != logits.shape:
@@ -283,8 +299,9 @@ class DartsSearch:
         s = self.s
         if self.K is not None:
             nparts = self.K.optim_sumsq(self.gW, self._parts)
+            # gW left zeroed for the next step's BWD1 (no fill launches at the passes' starts)
             self.K.optim_sgd_clip(self.W, self.gW, self.mom, self.lr, self._parts, nparts, s["w_grad_clip"],
-                                  s["w_momentum"], s["w_weight_decay"])
+                                  s["w_momentum"], s["w_weight_decay"], True)
             return
         with torch.no_grad():
             total = self.gW.norm()
@@ -304,7 +321,7 @@ class DartsSearch:
 
             if dops.backend() == "hip":
                 from ..ops import hip_darts as hd
-        begin = (lambda: hd.arena_begin(self.device)) if hd else (lambda: None)
+        begin = (lambda: hd.arena_begin(self.device, deferred_zero=self.net.net_function)) if hd else (lambda: None)
         end = hd.arena_end if hd else (lambda: None)
         return [
             (lambda: (begin(), self._seg_virtual(self.static["tx"], self.static["ty"])), [self.gW]),

@@ -196,19 +196,26 @@ class _Arena:
         self.used = 0
         self.need = 0
         self.active = False
+        self.pending_zero = False  # the zeroing rides on the step's first network launch (alpha softmax)
 
 
 _ARENA = _Arena()
 
 
-def arena_begin(device):
+def arena_begin(device, deferred_zero: bool = False):
+    """Start a step's arena. ``deferred_zero``: the zeroing is left to the step's first
+    :func:`network_loss` (its alpha-softmax launch zeroes the arena too), else one fill here."""
     a = _ARENA
     if a.need and (a.buf is None or a.buf.numel() < a.need):
         if a.buf is not None:
             a.keep.append(a.buf)
         a.buf = torch.zeros(a.need, dtype=F64, device=device)
+        a.pending_zero = False
     elif a.buf is not None:
-        a.buf.zero_()
+        if deferred_zero:
+            a.pending_zero = True
+        else:
+            a.buf.zero_()
     a.off, a.used, a.active = 0, 0, True
 
 
@@ -216,6 +223,9 @@ def arena_end():
     a = _ARENA
     a.need = max(a.need, a.used)
     a.active = False
+    if a.pending_zero:  # nobody consumed the deferred zeroing: do it now
+        a.buf.zero_()
+        a.pending_zero = False
 
 
 def zeros64(n: int, device) -> torch.Tensor:
@@ -803,6 +813,13 @@ def mixed_edge(x, w, spec: EdgeSpec, bn: List[Tuple[torch.Tensor, torch.Tensor]]
 
 
 # --------------------------------------------------------------------------------- preprocess
+def _dims(x: torch.Tensor):
+    """(N, C, H, W) of an [N][C][H][W] tensor or of a node-major [nodes][N][C/nodes][H][W] one."""
+    if x.dim() == 5:
+        return x.shape[1], x.shape[0] * x.shape[2], x.shape[3], x.shape[4]
+    return tuple(x.shape)
+
+
 def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2, defer=None):
     """ReLU -> 1x1 conv (ReLUConvBN, operations.py) or FactorizedReduce (two stride-2 1x1
     convs on offset grids, channel-concatenated) -> BN(affine=False). Returns (out, state).
@@ -811,7 +828,7 @@ def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2, defer=None):
     fold; the backward then reads them folded."""
     x = x.contiguous()
     _selffold(x.device)
-    N, Cin, H, W = x.shape
+    N, Cin, H, W = _dims(x)
     fr = w2 is not None
     Cout = w1.shape[0] * (2 if fr else 1)
     Ho, Wo = (H // 2, W // 2) if fr else (H, W)
@@ -834,8 +851,10 @@ def _stdconv_forward(x, rm, rv, training, momentum, eps, w1, w2, defer=None):
     return out, (x, z, w1, w2, bn, fr, Cout, training)
 
 
-def _stdconv_backward(state, dout, need_x, sinks, keys):
-    """Returns the input gradient (or None); weight gradients through ``sinks``."""
+def _stdconv_backward(state, dout, need_x, sinks, keys, gx=None, first=True):
+    """Returns the input gradient (or None); weight gradients through ``sinks``. ``gx`` (shaped
+    like the input, maybe node-major): write the input gradient there - overwriting it when
+    ``first``, else adding to it - instead of into a new buffer."""
     x, z, w1, w2, bn, fr, Cout, training = state
     dout = dout.contiguous()
     nred = 2 * Cout + 1
@@ -849,15 +868,20 @@ def _stdconv_backward(state, dout, need_x, sinks, keys):
             _fold64([(red, nred, nred)], x.device)
     gs = (dout, z, red[:Cout], red[Cout:2 * Cout], bn, None, 0, REP if late else _R, nred)
     g1, s1 = sinks.get(w1, keys[0])
-    if fr:  # the two stride-2 grids leave 3 of 4 input pixels untouched: start from zeros
-        gx = torch.zeros_like(x) if need_x else None
+    given = gx is not None
+    if fr:  # the two stride-2 grids leave 2 of 4 input pixels untouched: start from zeros
+        if need_x and not given:
+            gx = torch.zeros_like(x)
+        elif need_x and first:
+            gx.zero_()
         g2, s2 = sinks.get(w2, keys[1])
         _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1), (gs, w2, None, x, None, gx, g2, Cout // 2, 1, s2)],
                   2, 1, need_x)
-    else:  # stride 1 covers every input pixel: the kernel overwrites gx (no fill)
-        gx = torch.empty_like(x) if need_x else None
-        _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1, True)], 1, 1, need_x)
-    return gx
+    else:  # stride 1 covers every input pixel: the first writer overwrites gx (no fill)
+        if need_x and not given:
+            gx = torch.empty_like(x)
+        _K.pw_bwd([(gs, w1, None, x, None, gx, g1, 0, 0, s1, first or not given)], 1, 1, need_x)
+    return gx if need_x else None
 
 
 class _StdConvBN(torch.autograd.Function):
@@ -893,57 +917,112 @@ class CellSpec:
         self.index = {n: i for i, n in enumerate(self.names)}
 
 
+def _cell_fwd(spec, s0, s1, wts, P, bn_of, training, momentum, eps):
+    """A DARTS cell forward on the HIP kernels: preprocess(s0), preprocess(s1) (each input
+    [N][C][H][W] or node-major), every node. Returns (O, state): O = the node outputs,
+    node-major [nodes][N][C][H][W] - the cell output is kept as its nodes' buffers, never
+    concatenated (the next cells' preprocess and the head read it node-major)."""
+    late = []  # preprocess BN statistics folded by the first node's fold
+
+    def pre(x, p):
+        kind, pnames, bname = p
+        rm, rv = bn_of(bname)
+        if kind == "fr":
+            return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], P[pnames[1]], late)
+        return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], None, late)
+    t0, st0 = pre(s0, spec.pre0)
+    t1, st1 = pre(s1, spec.pre1)
+    states = [t0, t1]
+    N, C = t0.shape[0], spec.C
+    nn_ = len(spec.nodes)
+    S = [e[0].stride for e in spec.nodes[0]]
+    Ho = (t0.shape[2] - 1) // max(S) + 1 if S else t0.shape[2]
+    Wo = (t0.shape[3] - 1) // max(S) + 1 if S else t0.shape[3]
+    O = torch.empty(nn_, N, C, Ho, Wo, device=t0.device)
+    node_states = []
+    for i, node in enumerate(spec.nodes):
+        xs = [states[src] for _, _, _, src, _ in node]
+        ws = [wts[row] for _, _, _, _, row in node]
+        specs = [es for es, _, _, _, _ in node]
+        bns = [[bn_of(b) for b in bnames] for _, _, bnames, _, _ in node]
+        plist = [[P[n] for n in pnames] for _, pnames, _, _, _ in node]
+        out, edges = _node_forward(xs, ws, specs, bns, plist, training, momentum, eps, out=O[i],
+                                   extra_fold=late if i == 0 else ())
+        states.append(out)
+        node_states.append(edges)
+    return O, (spec, training, st0, st1, node_states, states, wts)
+
+
+def _cell_bwd(state, gO, sinks, pkey, gx0, first0, gx1, first1, need0, need1, alpha_rows=None):
+    """The cell backward: ``gO`` = gradient of the node outputs (node-major, overwritten by the
+    nodes' input-gradient kernels as scratch), nodes in reverse with one gradient buffer per cell
+    state (the first kernel writing a buffer overwrites it, later ones accumulate), then both
+    preprocess layers into ``gx0`` / ``gx1`` (None: new buffers) - overwriting when ``first0`` /
+    ``first1``. Weight gradients through ``sinks`` under ``pkey(name)``. ``alpha_rows`` (a list):
+    the edges' replicated d(softmax weight) go there as (f64 replicas, rstride, weight row) for the
+    alpha-gradient kernel; otherwise they are folded and returned as a [rows, K] tensor.
+    Returns (gs0, gs1, d softmax weights or None)."""
+    spec, training, st0, st1, node_states, states, wts = state
+    nn_ = len(spec.nodes)
+    gS = [None, None] + [gO[i] for i in range(nn_)]
+    first = [True, True] + [False] * nn_
+    ga_rows = [None] * nn_
+    cell_gw = []  # the nodes' unfolded d(alpha) replicas
+    for i in reversed(range(nn_)):
+        node = spec.nodes[i]
+        edges = node_states[i]
+        srcs = [src for _, _, _, src, _ in node]
+        for src in srcs:
+            if gS[src] is None:
+                gS[src] = torch.empty_like(states[src])
+
+        def take_first(k, srcs=srcs):
+            f = first[srcs[k]]
+            first[srcs[k]] = False
+            return f
+
+        _node_backward(edges, training, spec.C, gS[2 + i], lambda k, srcs=srcs: gS[srcs[k]], take_first, sinks,
+                       lambda e, name, node=node: pkey(node[e.i][1][e.spec.pidx[name]]), cell_gw)
+        if alpha_rows is not None:
+            for e, (_, _, _, _, row) in zip(edges, node):
+                alpha_rows.append((e.gw, e.w.numel(), wts[row], row))
+        else:
+            ga_rows[i] = [e.gw[:wts.shape[1]] for e in edges]
+    for j in (0, 1):
+        if first[j]:  # only "none" primitives read this state
+            gS[j] = torch.zeros_like(states[j])
+    gs0 = _stdconv_backward(st0, gS[0], need0, sinks, tuple(pkey(n) for n in spec.pre0[1]) + (None,), gx0, first0)
+    gs1 = _stdconv_backward(st1, gS[1], need1, sinks, tuple(pkey(n) for n in spec.pre1[1]) + (None,), gx1, first1)
+    gw = None
+    if alpha_rows is None:
+        if cell_gw:
+            _K.fold_f64(cell_gw)  # d alpha: per rank
+        gw = torch.cat([g for rows in ga_rows for g in rows]).view(wts.shape).to(torch.float32)
+    return gs0, gs1, gw
+
+
 class _Cell(torch.autograd.Function):
     """A whole cell - preprocess(s0), preprocess(s1), every node, the concat - as ONE autograd
-    Function with a hand-scheduled backward. Node outputs are written straight into a
-    node-major buffer [nodes][N][C][H][W] (one transpose copy makes the concat), and the
-    backward keeps one gradient buffer per cell state: nodes run in reverse, each edge's input
-    gradient goes into its source state's buffer (the first kernel to touch a buffer
-    overwrites it, later ones accumulate), so the per-consumer gradient buffers, their
-    autograd additions, the concat-slice copies and the zero fills of the per-node path
-    disappear. The alpha gradients of all edges come back as one [rows, K] tensor."""
+    Function with a hand-scheduled backward (:func:`_cell_fwd` / :func:`_cell_bwd`); the whole
+    network runs as one Function in :func:`network_loss`, which also drops this wrapper's concat
+    and transpose copies."""
 
     @staticmethod
     def forward(ctx, meta, s0, s1, wts, *params):
         spec, bn_of, training, momentum, eps = meta
         P = dict(zip(spec.names, params))
-        late = []  # preprocess BN statistics folded by the first node's fold
-
-        def pre(x, p):
-            kind, pnames, bname = p
-            rm, rv = bn_of(bname)
-            if kind == "fr":
-                return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], P[pnames[1]], late)
-            return _stdconv_forward(x, rm, rv, training, momentum, eps, P[pnames[0]], None, late)
-        t0, st0 = pre(s0, spec.pre0)
-        t1, st1 = pre(s1, spec.pre1)
-        states = [t0, t1]
-        N, C = t0.shape[0], spec.C
-        nn_ = len(spec.nodes)
-        S = [e[0].stride for e in spec.nodes[0]]
-        Ho = (t0.shape[2] - 1) // max(S) + 1 if S else t0.shape[2]
-        Wo = (t0.shape[3] - 1) // max(S) + 1 if S else t0.shape[3]
-        O = torch.empty(nn_, N, C, Ho, Wo, device=t0.device)
-        node_states = []
-        for i, node in enumerate(spec.nodes):
-            xs = [states[src] for _, _, _, src, _ in node]
-            ws = [wts[row] for _, _, _, _, row in node]
-            specs = [es for es, _, _, _, _ in node]
-            bns = [[bn_of(b) for b in bnames] for _, _, bnames, _, _ in node]
-            plist = [[P[n] for n in pnames] for _, pnames, _, _, _ in node]
-            out, edges = _node_forward(xs, ws, specs, bns, plist, training, momentum, eps, out=O[i],
-                                       extra_fold=late if i == 0 else ())
-            states.append(out)
-            node_states.append(edges)
+        O, state = _cell_fwd(spec, s0, s1, wts, P, bn_of, training, momentum, eps)
+        nn_, N, C, Ho, Wo = O.shape
         y = O.permute(1, 0, 2, 3, 4).reshape(N, nn_ * C, Ho, Wo)
-        ctx.cell = (spec, training, st0, st1, node_states, states, wts.shape)
+        ctx.cell = state
         ctx.save_for_backward(s0, s1, wts, *params)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        spec, training, st0, st1, node_states, states, wshape = ctx.cell
+        state = ctx.cell
         ctx.cell = None
+        spec = state[0]
         saved = ctx.saved_tensors
         params = saved[3:]
         nn_ = len(spec.nodes)
@@ -951,48 +1030,16 @@ class _Cell(torch.autograd.Function):
         Ho, Wo = dy.shape[2], dy.shape[3]
         # node-major copy of the incoming gradient: one buffer per node state
         gO = dy.reshape(N, nn_, C * Ho * Wo).transpose(0, 1).contiguous().view(nn_, N, C, Ho, Wo)
-        gS = [None, None] + [gO[i] for i in range(nn_)]
-        first = [True, True] + [False] * nn_
         sinks = _Sinks()
-        want_ga = ctx.needs_input_grad[3]
-        ga_rows = [None] * nn_
-        cell_gw = []  # the nodes' unfolded d(alpha) replicas
-        for i in reversed(range(nn_)):
-            node = spec.nodes[i]
-            edges = node_states[i]
-            srcs = [src for _, _, _, src, _ in node]
-            for src in srcs:
-                if gS[src] is None:
-                    gS[src] = torch.empty_like(states[src])
-
-            def take_first(k, srcs=srcs):
-                f = first[srcs[k]]
-                first[srcs[k]] = False
-                return f
-
-            _node_backward(edges, training, C, gS[2 + i], lambda k, srcs=srcs: gS[srcs[k]], take_first, sinks,
-                           lambda e, name, node=node: 4 + spec.index[node[e.i][1][e.spec.pidx[name]]], cell_gw)
-            if want_ga:  # a node's alpha rows are consecutive, nodes in row order
-                ga_rows[i] = [e.gw[:wshape[1]] for e in edges]
-        for j in (0, 1):
-            if first[j]:  # only "none" primitives read this state
-                gS[j] = torch.zeros_like(states[j])
-        grads = [None] * (4 + len(params))
         need = ctx.needs_input_grad
-        gs0 = _stdconv_backward(st0, gS[0], need[1], sinks, _pre_keys(spec, spec.pre0))
-        gs1 = _stdconv_backward(st1, gS[1], need[2], sinks, _pre_keys(spec, spec.pre1))
+        grads = [None] * (4 + len(params))
+        gs0, gs1, gw = _cell_bwd(state, gO, sinks, lambda n: 4 + spec.index[n], None, True, None, True, need[1],
+                                 need[2])
         grads[1], grads[2] = gs0, gs1
-        if want_ga:
-            if cell_gw:
-                _K.fold_f64(cell_gw)  # d alpha: per rank
-            grads[3] = torch.cat([g for rows in ga_rows for g in rows]).view(wshape).to(torch.float32)
+        if need[3]:
+            grads[3] = gw
         sinks.finish(grads)
         return tuple(grads)
-
-
-def _pre_keys(spec, pre):
-    names = pre[1]
-    return tuple(4 + spec.index[n] for n in names) + ((None,) if len(names) == 1 else ())
 
 
 def cell_forward(spec: CellSpec, s0, s1, wts, params: Sequence[torch.Tensor], bn_of, training: bool,
@@ -1052,62 +1099,78 @@ class _StemConv(torch.autograd.Function):
         return gx, gw
 
 
+def _stem_fwd(x, w, gamma, beta, rm, rv, momentum, eps):
+    """Training-mode stem conv + affine BN (batch statistics): the conv accumulates the BN
+    statistics in its epilogue, one fold + one combine_fwd apply the normalisation (running stats
+    updated in the same launch). Returns (out, state)."""
+    x, w = x.contiguous(), w.contiguous()
+    N, _, H, W = x.shape
+    C = w.shape[0]
+    stats = zeros64(REP * 2 * C, x.device)
+    z = torch.empty(N, C, H, W, device=x.device, dtype=x.dtype)
+    _K.stem_conv_fwd_stats(x, w, z, stats)
+    _fold([(stats, 2 * C, 2 * C)])  # always folded: the weight-gradient kernel reads replica 0
+    bn = _bn(stats, rm, rv, N * H * W, True, eps, C)
+    out = torch.empty_like(z)
+    zs = z if ZDT == z.dtype else z.to(ZDT)  # the combine kernels read z in the intermediates' type
+    _K.combine_fwd([([zs], [bn], [0], None, -1, None, [])], gamma, beta, out, momentum, True, False)
+    return out, (x, w, gamma, beta, z, zs, bn, eps, stats)
+
+
+def _stem_bwd(state, dout, sinks, keys, need):
+    """The stem backward: one BN-backward reduction + fold, then the weight-gradient kernel forms
+    the conv-output gradient on the fly and adds d gamma / d beta. ``keys`` = (w, gamma, beta)
+    sink keys, ``need`` = (x, w, gamma, beta) flags; returns (gx or None, gw or None)."""
+    x, w, gamma, beta, z, zs, bn, eps, stats = state
+    dout = dout.contiguous()
+    C = w.shape[0]
+    nred = 2 * C + 1
+    red = zeros64(REP * nred, x.device)
+    _K.combine_bwd_reduce([(dout, [zs], [bn], None, red, [0], -1, None)])
+    if not _selffold(x.device):
+        _fold([(red, nred, nred)])
+    gg, _ = sinks.get(gamma, keys[1]) if need[2] else (None, 0)
+    gb, _ = sinks.get(beta, keys[2]) if need[3] else (None, 0)
+    gw = gx = None
+    if need[1] or need[2] or need[3]:
+        chunks = stem_chunks(x, C)
+        partial = torch.empty(chunks, w.numel(), device=x.device, dtype=torch.float32)
+        if need[1]:  # straight into the weight's gradient row (registered replicated .grad, or a sink temp)
+            gdst, _ = sinks.get(w, keys[0])
+            _K.stem_conv_wgrad_bn(x, dout, z, red, stats, gamma, eps, gg, gb, partial, gdst, _world(), True)
+        else:
+            _K.stem_conv_wgrad_bn(x, dout, z, red, stats, gamma, eps, gg, gb, partial, torch.empty_like(w), _world())
+    if need[0]:  # never for the input image; plain formula for completeness
+        m = stats[:C] / z[:, 0].numel()
+        var = (stats[C:2 * C] / z[:, 0].numel() - m * m).clamp_min(0)
+        istd = torch.rsqrt(var.float() + eps).view(1, C, 1, 1)
+        zhat = (z - m.float().view(1, C, 1, 1)) * istd
+        m1 = (red[:C] / z[:, 0].numel()).float().view(1, C, 1, 1)
+        m2 = (red[C:2 * C] / z[:, 0].numel()).float().view(1, C, 1, 1)
+        dz = gamma.view(1, C, 1, 1) * istd * (dout - m1 - zhat * m2)
+        gx = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1)
+    return gx, gw
+
+
 class _StemConvBN(torch.autograd.Function):
     """Stem Conv2d(Cin, C, 3, padding=1, bias=False) + BatchNorm2d(C) (affine, batch statistics)
-    on the stem kernels (reference ``model.py:90-93``): the conv accumulates the BN statistics
-    in its epilogue, one fold + one combine_fwd launch apply the normalisation (running stats
-    updated in the same launch); the backward is one BN-backward reduction + fold, then the weight
-    gradient kernel forms the conv-output gradient on the fly and adds d gamma / d beta."""
+    on the stem kernels (reference ``model.py:90-93``): :func:`_stem_fwd` / :func:`_stem_bwd`."""
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, rm, rv, momentum, eps):
-        x, w = x.contiguous(), w.contiguous()
-        N, _, H, W = x.shape
-        C = w.shape[0]
-        stats = zeros64(REP * 2 * C, x.device)
-        z = torch.empty(N, C, H, W, device=x.device, dtype=x.dtype)
-        _K.stem_conv_fwd_stats(x, w, z, stats)
-        _fold([(stats, 2 * C, 2 * C)])  # always folded: the weight-gradient kernel reads replica 0
-        bn = _bn(stats, rm, rv, N * H * W, True, eps, C)
-        out = torch.empty_like(z)
-        zs = z if ZDT == z.dtype else z.to(ZDT)  # the combine kernels read z in the intermediates' type
-        _K.combine_fwd([([zs], [bn], [0], None, -1, None, [])], gamma, beta, out, momentum, True, False)
-        ctx.bn, ctx.eps, ctx.stats = bn, eps, stats
-        ctx.save_for_backward(x, w, gamma, beta, z, zs)
+        out, state = _stem_fwd(x, w, gamma, beta, rm, rv, momentum, eps)
+        ctx.stem = state
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, w, gamma, beta, z, zs = ctx.saved_tensors
-        bn, eps, stats = ctx.bn, ctx.eps, ctx.stats
-        ctx.bn = ctx.stats = None
-        dout = dout.contiguous()
-        C = w.shape[0]
-        nred = 2 * C + 1
-        red = zeros64(REP * nred, x.device)
-        _K.combine_bwd_reduce([(dout, [zs], [bn], None, red, [0], -1, None)])
-        if not _selffold(x.device):
-            _fold([(red, nred, nred)])
+        state = ctx.stem
+        ctx.stem = None
         need = ctx.needs_input_grad
         grads = [None] * 8
         sinks = _Sinks()
-        gg, _ = sinks.get(gamma, 2) if need[2] else (None, 0)
-        gb, _ = sinks.get(beta, 3) if need[3] else (None, 0)
-        if need[1] or need[2] or need[3]:
-            chunks = stem_chunks(x, C)
-            partial = torch.empty(chunks, w.numel(), device=x.device, dtype=torch.float32)
-            gw = torch.empty_like(w)
-            _K.stem_conv_wgrad_bn(x, dout, z, red, stats, gamma, eps, gg, gb, partial, gw, _world())
-            grads[1] = gw if need[1] else None
-        if need[0]:  # never for the input image; plain formula for completeness
-            m = stats[:C] / z[:, 0].numel()
-            var = (stats[C:2 * C] / z[:, 0].numel() - m * m).clamp_min(0)
-            istd = torch.rsqrt(var.float() + eps).view(1, C, 1, 1)
-            zhat = (z - m.float().view(1, C, 1, 1)) * istd
-            m1 = (red[:C] / z[:, 0].numel()).float().view(1, C, 1, 1)
-            m2 = (red[C:2 * C] / z[:, 0].numel()).float().view(1, C, 1, 1)
-            dz = gamma.view(1, C, 1, 1) * istd * (dout - m1 - zhat * m2)
-            grads[0] = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1)
+        gx, _ = _stem_bwd(state, dout, sinks, (1, 2, 3), need[:4])
+        grads[0] = gx
         sinks.finish(grads)
         return tuple(grads)
 
@@ -1200,3 +1263,154 @@ def head_supported(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor) -> bool:
 def head_loss(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor):
     """(mean cross-entropy, logits) of ``linear(gap(x))`` against ``y``; logits carry no grad."""
     return _Head.apply(x, w, b, y.contiguous())
+
+
+# --------------------------------------------------------------------------------- network
+class NetSpec:
+    """Static description of the supernet for :func:`network_loss`: the stem ``(conv, bn weight,
+    bn bias, bn name)``, every cell (:class:`CellSpec`, reduction flag) and the head ``(weight,
+    bias)``; ``names`` orders the parameter tensors passed to it."""
+
+    def __init__(self, stem, cells, reduce, head):
+        self.stem, self.cells, self.reduce, self.head = stem, list(cells), list(reduce), head
+        names = list(stem[:3])
+        for c in self.cells:
+            names += c.names
+        names += list(head)
+        self.names = names
+        self.index = {n: i for i, n in enumerate(names)}
+
+
+def _alpha_grad(entries):
+    """alpha_grad launches over (g replicas, rstride, weight row, destination row) entries, each
+    destination row's entries in one launch (the kernel sums them per row, deterministically)."""
+    groups = defaultdict(list)
+    for ent in entries:
+        groups[ent[3].data_ptr()].append(ent)
+    chunk = []
+    for rows in groups.values():
+        if len(chunk) + len(rows) > 64:
+            _K.alpha_grad(chunk, True)
+            chunk = []
+        chunk += rows
+    if chunk:
+        _K.alpha_grad(chunk, True)
+
+
+class _Network(torch.autograd.Function):
+    """The whole supernet - alpha softmax, stem conv + BN, every cell, head (gap, classifier,
+    cross-entropy) - as ONE autograd Function with a hand-scheduled backward, so nothing between
+    the HIP kernels is left to framework launches:
+
+    * cell outputs stay node-major ([nodes][N][C][H][W], the nodes' own buffers): the next cells'
+      preprocess and the head read them in that layout, so the forward concatenation and the
+      backward transpose copies disappear (reference ``model.py:70`` torch.cat);
+    * every cell state has one gradient buffer that its first consumer's kernel overwrites and later
+      ones add to - the stem output's three and a cell output's two consumers need no autograd
+      additions or fills;
+    * the alpha softmax of both cell types is one launch (which also zeroes the step's f64 arena),
+      and d(alpha) is one launch that sums the edges' replicated d(softmax weight) rows through the
+      softmax Jacobian straight into the alpha leaves' gradient rows (no fold, cat, dtype copy,
+      softmax backward or accumulation launches);
+    * weight gradients go to the registered replicated buffers as before (:class:`_Sinks`).
+    """
+
+    @staticmethod
+    def forward(ctx, meta, x, y, an, ar, *params):
+        spec, bn_of, training, momentum, eps = meta
+        P = dict(zip(spec.names, params))
+        dev = x.device
+        mats, outs = [an], [torch.empty_like(an)]
+        if ar is not None:
+            mats.append(ar)
+            outs.append(torch.empty_like(ar))
+        zero = None
+        a = _ARENA
+        if training and a.pending_zero and a.buf is not None and a.buf.device == dev:
+            zero, a.pending_zero = a.buf, False
+        _K.alpha_softmax(mats, outs, zero)
+        wn, wr = outs[0], (outs[1] if ar is not None else None)
+        conv, gamma, beta, bname = spec.stem
+        rm, rv = bn_of(bname)
+        if training:
+            s, st_stem = _stem_fwd(x, P[conv], P[gamma], P[beta], rm, rv, momentum, eps)
+        else:
+            s, st_stem = stem_bn_eval(stem_conv(x, P[conv]), P[gamma], P[beta], rm, rv, eps), None
+        tensors = [s]
+        cells = []
+        i0 = i1 = 0
+        for cspec, red in zip(spec.cells, spec.reduce):
+            O, st = _cell_fwd(cspec, tensors[i0], tensors[i1], wr if red else wn, P, bn_of, training, momentum, eps)
+            tensors.append(O)
+            cells.append((st, i0, i1, len(tensors) - 1, red))
+            i0, i1 = i1, len(tensors) - 1
+        feat = tensors[i1]
+        hw, hb = spec.head
+        N, C = _dims(feat)[:2]
+        K = P[hw].shape[0]
+        pooled = torch.empty(N, C, device=dev)
+        logits = torch.empty(N, K, device=dev)
+        dl = torch.empty(N, K, device=dev)
+        loss_n = torch.empty(N, device=dev)
+        loss = torch.empty((), device=dev)
+        _K.head_fwd(feat, P[hw], P[hb], y, pooled, logits, dl, loss_n)
+        _K.head_loss(loss_n, loss)
+        ctx.net = (spec, P, training, st_stem, cells, tensors, i1, dl, pooled, an, ar)
+        ctx.mark_non_differentiable(logits)
+        ctx.set_materialize_grads(False)
+        return loss, logits
+
+    @staticmethod
+    def backward(ctx, gloss, _glogits):
+        spec, P, training, st_stem, cells, tensors, last, dl, pooled, an, ar = ctx.net
+        ctx.net = None
+        grads = [None] * (5 + len(spec.names))
+        if gloss is None:
+            return tuple(grads)
+        need = ctx.needs_input_grad
+        sinks = _Sinks()
+
+        def key(n):
+            return 5 + spec.index[n]
+        g, first = {last: torch.empty_like(tensors[last])}, {last: False}
+        hw, hb = spec.head
+        gw, sw = sinks.get(P[hw], key(hw)) if need[key(hw)] else (None, 0)
+        gb, sb = sinks.get(P[hb], key(hb)) if need[key(hb)] else (None, 0)
+        _K.head_bwd(tensors[last], dl, pooled, P[hw], gloss.reshape(()).contiguous().float(), g[last], gw, sw, gb, sb)
+        rows = []
+        for st, i0, i1, io, red in reversed(cells):
+            for i in (i0, i1):
+                if i not in g:
+                    g[i], first[i] = torch.empty_like(tensors[i]), True
+            f0 = first[i0]
+            f1 = first[i1] and i1 != i0  # the first cell's two inputs are both the stem output
+            cell_rows = []
+            _cell_bwd(st, g[io], sinks, key, g[i0], f0, g[i1], f1, True, True, cell_rows)
+            first[i0] = first[i1] = False
+            rows += [(r, red) for r in cell_rows]
+        # d(alpha) straight into the leaves' gradient rows (or into returned tensors)
+        dst = {}
+        for red, leaf, idx in ((False, an, 3), (True, ar, 4)):
+            if leaf is None or not need[idx]:
+                continue
+            if leaf.is_leaf and leaf.grad is not None and leaf.grad.is_contiguous() and leaf.grad.dtype == torch.float32:
+                dst[red] = leaf.grad
+            else:
+                dst[red] = grads[idx] = torch.zeros_like(leaf)
+        ents = [(gw_, rs, wrow, dst[red][row]) for (gw_, rs, wrow, row), red in rows if red in dst]
+        if ents:
+            _alpha_grad(ents)
+        conv, gamma, beta, _ = spec.stem
+        if training and st_stem is not None and 0 in g:
+            flags = (False, need[key(conv)], need[key(gamma)], need[key(beta)])
+            _stem_bwd(st_stem, g[0], sinks, (key(conv), key(gamma), key(beta)), flags)
+        sinks.finish(grads)
+        return tuple(grads)
+
+
+def network_loss(spec: NetSpec, x, y, params: Sequence[torch.Tensor], an, ar, bn_of, training: bool,
+                 momentum: float = 0.1, eps: float = 1e-5):
+    """(mean cross-entropy, logits) of the DARTS supernet on the HIP kernels as one Function
+    (:class:`_Network`); ``an`` / ``ar``: the [rows, K] alpha matrices of the normal / reduction
+    cells (``ar`` None for a one-layer net); ``params`` ordered as ``spec.names``."""
+    return _Network.apply((spec, bn_of, training, momentum, eps), x, y, an, ar, *params)

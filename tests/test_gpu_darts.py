@@ -525,3 +525,50 @@ def test_selffold_and_edge_bwd_paths_match_torch(selffold, edge):
     assert max(abs(a - b) for a, b in zip(lt, lh)) < 1e-3
     _close(Wh, Wt, "W", rtol=1e-3, atol=1e-4)
     _close(Ah, At, "alpha", rtol=5e-2, atol=5e-5)
+
+
+@pytest.mark.parametrize("leaf_alphas", [True, False])
+def test_network_function_matches_per_cell_path(leaf_alphas):
+    """The whole-network Function (hip_darts.network_loss: node-major cell outputs, first-writer
+    gradient buffers, fused alpha softmax / alpha gradient) computes what the per-cell Functions
+    under autograd compute: loss, logits, weight and alpha gradients, BN running statistics; with
+    leaf alpha matrices (DartsSearch) the alpha gradient is written into the leaves' .grad, with
+    per-node alpha rows it flows back through autograd."""
+    from katib_amd.models.darts import BNState, DartsLayout, DartsNetwork
+    from katib_amd.ops import darts as dops
+
+    dops.set_backend("hip")
+    dev = torch.device("cuda", 0)
+    layout = DartsLayout(ALL, init_channels=4, num_layers=3, num_nodes=3, stem_multiplier=1)
+    g = torch.Generator().manual_seed(3)
+    W = torch.zeros(layout.n_weights)
+    layout.init_weights(W, g)
+    A = 1e-1 * torch.randn(layout.n_alphas, generator=g)
+    x = torch.randn(32, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (32,), generator=g).to(dev)
+    out = {}
+    for mode in (True, False):
+        net = DartsNetwork(layout, ops=dops)
+        net.net_function = mode
+        Wl = W.to(dev).requires_grad_(True)
+        P = layout.views(Wl)
+        Al = A.to(dev)
+        rows, K = layout.n_alpha_rows, len(layout.prims)
+        an = Al[:rows * K].view(rows, K).clone().requires_grad_(True)
+        ar = Al[rows * K:].view(rows, K).clone().requires_grad_(True)
+        if leaf_alphas:
+            an.grad, ar.grad = torch.zeros_like(an), torch.zeros_like(ar)
+            na, ra = an, ar
+        else:
+            na, ra = list(an.split([2 + i for i in range(layout.N)])), list(ar.split([2 + i for i in range(layout.N)]))
+        bn = BNState(layout, dev)
+        loss, logits = net.forward_loss(x, y, P, na, ra, bn, training=True)
+        loss.backward(inputs=[Wl, an, ar])
+        torch.cuda.synchronize()
+        out[mode] = (loss.detach(), logits.detach(), Wl.grad.clone(), an.grad.clone(), ar.grad.clone(), bn.buf.clone())
+        dops.set_backend("hip")
+    # both paths sum float atomics in a run-dependent order (and the gradient of a cell state in a
+    # different order: first-writer buffers vs autograd additions): fp32 rounding-level differences
+    for name_, a, b in zip(["loss", "logits", "gW", "ga_n", "ga_r", "bn"], out[True], out[False]):
+        _close(a, b, name_, rtol=5e-3, atol=1e-5)
+    dops.set_backend("torch")
