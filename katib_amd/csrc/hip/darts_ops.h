@@ -87,6 +87,7 @@ struct DwPwFwdArgs {
   int N, C, H, W, Ho, Wo, pad, chunk, use_mfma;
   int variant;  // dwpw_plane_multi_kernel: ((K == 5) * 4 + (dil == 2) * 2 + (S == 2)) * 4 + prebn * 2 + vec
   int nblk;     // dwpw_plane_multi_kernel: workgroups of this entry (grid.x is the max over entries)
+  int vout = 0; // dwpw_plane: 4 output pixels per thread, 16-byte stores (host: vec_mask())
 };
 
 struct PwFwdArgs {
@@ -132,6 +133,7 @@ struct DwBwdArgs {
   int N, C, H, W, Ho, Wo, pad, chunk;
   int overwrite;  // non-PREBN: gout = masked grad (first writer of this input gradient) instead of +=
   int variant, nbands, nblk;  // dw_bwd_plane_multi_kernel: dw_bwd_variant, row bands, workgroups of this entry
+  int vin = 0;  // dw_bwd_plane, stride 1: 4 input pixels per thread, 16-byte stores (host: vec_mask())
 };
 constexpr int dw_bwd_variant(int K, int dil, int S, bool prebn) {
   return (((K == 5) * 4 + (dil == 2) * 2 + (S == 2)) << 1) | (prebn ? 1 : 0);

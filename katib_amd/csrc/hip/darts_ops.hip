@@ -46,6 +46,15 @@ int max_blocks() {
 }
 void set_max_blocks(int n) { g_max_blocks = n; }
 
+// 4-pixels-per-thread output paths of the plane kernels, per channel group (KATIB_HIP_VEC_MASK,
+// read once): bit 0 dwpw_plane C = 4, bit 1 dwpw_plane C = 8, bit 2 dw_bwd_plane C = 4, bit 3
+// dw_bwd_plane C = 8. Default C = 4 only: at C = 8 the four-pixel register arrays cost more than the
+// wider stores save (profiles/darts_vec_ab_r04.log).
+static int vec_mask() {
+  static const int m = getenv("KATIB_HIP_VEC_MASK") ? atoi(getenv("KATIB_HIP_VEC_MASK")) : 0x5;
+  return m;
+}
+
 // s += p[r*rs], s2 += p[r*rs + off2] over r < rep replicas, 8 replicas (16 loads) in flight per
 // step instead of one dependent load-add per replica
 __device__ __forceinline__ void sum_replicas(const double* p, int rep, int rs, int off2, double& s, double& s2) {
@@ -496,7 +505,45 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
   const int HWo = Ho * Wo;
   zt* dn = a.d + ((size_t)n * a.C + c0) * HWo;
   zt* zn = a.z + (size_t)n * C * HWo;
-  for (int p = oy0 * Wo + tid; p < oy1 * Wo; p += 256) {
+  const bool vout = VEC && Wo % 4 == 0 && a.vout;
+  if (vout) {
+    // 4 consecutive output pixels (one row: Wo % 4 == 0) per thread: d and z leave as one 16-byte
+    // (bf16: 8-byte) store per channel instead of four 4-byte ones
+    for (int p = oy0 * Wo + 4 * tid; p < oy1 * Wo; p += 1024) {
+      const int oy = p / Wo, ox0 = p - oy * Wo;
+      zf4 d[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float* src = sIn + c * PL + ((oy - oy0) * S) * WP + ox0 * S;
+        const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
+        zf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx) {
+            const float w = wk[ky * K + kx];
+            const float* q = src + ky * DIL * WP + kx * DIL;
+            acc.x += w * q[0];
+            acc.y += w * q[S];
+            acc.z += w * q[2 * S];
+            acc.w += w * q[3 * S];
+          }
+        d[c] = acc;
+        zst4(dn + (size_t)c * HWo + p, acc);
+      }
+      if (!PW) continue;
+#pragma unroll
+      for (int co = 0; co < C; ++co) {
+        zf4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ci = 0; ci < C; ++ci) z += a.pw[co * C + ci] * d[ci];
+        zst4(zn + (size_t)co * HWo + p, z);
+        st1[co] += (z.x + z.y) + (z.z + z.w);
+        st2[co] += (z.x * z.x + z.y * z.y) + (z.z * z.z + z.w * z.w);
+      }
+    }
+  }
+  for (int p = oy0 * Wo + tid; p < (vout ? 0 : oy1 * Wo); p += 256) {
     const int oy = p / Wo, ox = p - oy * Wo;
     float d[C];
 #pragma unroll
@@ -1678,7 +1725,7 @@ __global__ void __launch_bounds__(256) dw_bwd_kernel(DwBwdBatch bt) {
 // ------------------------------------------------------------------------------------------------
 // pool_bwd: gx += avg^T(dz_avg) + max^T(dz_max) + wid * dout (identity skip), per (n,c) plane
 // ------------------------------------------------------------------------------------------------
-template <int S>
+template <int S, bool V4 = false>
 __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx) {
   const int C = a.C, H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, HWo = Ho * Wo;
   const int nc = bx, c = nc % C;
@@ -1702,6 +1749,64 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
   const float wa = a.ga.w ? a.ga.w[a.ga.widx] : 0.f;
   const float wm = a.gm.w ? a.gm.w[a.gm.widx] : 0.f;
   const float wid = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+  if constexpr (V4) {
+    // 4 consecutive outputs / input pixels per thread: every operand one 16-byte (amax: 4-byte)
+    // access instead of four 4-byte ones - a quarter of the memory requests in flight for the
+    // same bytes (HWo, H*W % 4 == 0 and every operand 16-byte aligned: host-checked)
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const float* gsrc = a.ga.z ? a.ga.g : a.gm.g;  // both pools read the edge's dout
+    for (int o4 = threadIdx.x * 4; o4 < HWo; o4 += 1024) {
+      const f4 g = *reinterpret_cast<const f4*>(gsrc + ob + o4);
+      if (a.ga.z) {
+        const f4 z = zld4(a.ga.z + ob + o4);
+        const f4 d = wa * ia * (g - a1 - ((z - ma) * ia) * a2);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int o = o4 + t, oy = o / Wo, ox = o - oy * Wo;
+          const int y0 = max(oy * S - 1, 0), y1 = min(oy * S + 1, H - 1);
+          const int x0 = max(ox * S - 1, 0), x1 = min(ox * S + 1, W - 1);
+          sGa[o] = d[t] / (float)((y1 - y0 + 1) * (x1 - x0 + 1));
+        }
+      } else {
+        *reinterpret_cast<f4*>(sGa + o4) = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (a.gm.z) {
+        const f4 z = zld4(a.gm.z + ob + o4);
+        *reinterpret_cast<f4*>(sGm + o4) = wm * im * (g - m1 - ((z - mm) * im) * m2);
+        *reinterpret_cast<unsigned*>(sArg + o4) = *reinterpret_cast<const unsigned*>(a.amax + ob + o4);
+      } else {
+        *reinterpret_cast<f4*>(sGm + o4) = f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<unsigned*>(sArg + o4) = 0xffffffffu;
+      }
+    }
+    __syncthreads();
+    const size_t pb = (size_t)nc * H * W;
+    for (int q4 = threadIdx.x * 4; q4 < H * W; q4 += 1024) {
+      f4 g = {0.f, 0.f, 0.f, 0.f};
+      if (a.dout_id) g = wid * *reinterpret_cast<const f4*>(a.dout_id + pb + q4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < a.nextra) g += *reinterpret_cast<const f4*>(a.extra[j] + pb + q4);
+      const int iy = q4 / W, ix0 = q4 - iy * W;  // 4 pixels of one row (W % 4 == 0)
+      const int oy_lo = iy - 1 < 0 ? 0 : (iy - 1 + S - 1) / S, oy_hi = min((iy + 1) / S, Ho - 1);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int ix = ix0 + t;
+        const int ox_lo = ix - 1 < 0 ? 0 : (ix - 1 + S - 1) / S, ox_hi = min((ix + 1) / S, Wo - 1);
+        float v = 0.f;
+        for (int oy = oy_lo; oy <= oy_hi; ++oy)
+          for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+            const int o = oy * Wo + ox;
+            v += sGa[o];
+            if (sArg[o] == (iy - oy * S + 1) * 3 + (ix - ox * S + 1)) v += sGm[o];
+          }
+        g[t] += v;
+      }
+      f4* dst = reinterpret_cast<f4*>(a.gx + pb + q4);
+      *dst = a.overwrite ? g : *dst + g;
+    }
+    return;
+  }
   for (int o = threadIdx.x; o < HWo; o += 256) {
     int oy = o / Wo, ox = o % Wo;
     if (a.ga.z) {
@@ -1748,11 +1853,12 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(PoolBwdBatch bt) {
 }
 
 // stride-1 and stride-2 pool backward of a node in one launch (different edges: different gx)
+template <bool V4>
 __global__ void __launch_bounds__(256) pool_bwd_multi_kernel(PoolBwdBatch bt) {
   const PoolBwdArgs a = bt.e[blockIdx.y];  // copy: see dwpw_plane_multi_kernel
   if ((int)blockIdx.x >= a.N * a.C) return;
-  if (a.S == 1) pool_bwd_body<1>(a, blockIdx.x);
-  else pool_bwd_body<2>(a, blockIdx.x);
+  if (a.S == 1) pool_bwd_body<1, V4>(a, blockIdx.x);
+  else pool_bwd_body<2, V4>(a, blockIdx.x);
 }
 
 
@@ -1858,7 +1964,51 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
 #pragma unroll
   for (int c = 0; c < C; ++c) st1[c] = st2[c] = 0.f;
   float* gn = a.gout + ((size_t)n * a.C + c0) * H * W;
-  for (int p = tid; p < ((dbg & 1) ? 0 : NP); p += 256) {
+  if (S == 1 && a.vin) {
+    // stride 1: 4 consecutive input pixels of one row per thread (W % 4 == 0, as the staging
+    // assumes): the taps' column offsets are shared, and the gradient leaves as one 16-byte store
+    // per channel instead of four 4-byte ones
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    for (int p = 4 * tid; p < ((dbg & 1) ? 0 : NP); p += 1024) {
+      const int r = p / W, ix = p - r * W, iy = iy0 + r;
+      int srow[K], scol[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        srow[k] = (iy + PAD - k * DIL - oyA) * ODW;
+        scol[k] = ix + PAD - k * DIL + PO;
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
+        const float* dd = sDD + c * ODR * ODW;
+        f4 ga = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx) {
+            const float w = wk[ky * K + kx];
+            const float* q = dd + srow[ky] + scol[kx];
+            ga.x += w * q[0];
+            ga.y += w * q[1];
+            ga.z += w * q[2];
+            ga.w += w * q[3];
+          }
+        const int li = (c * nrow + r) * W + ix;
+        const f4 act = *reinterpret_cast<const f4*>(sIn + li);
+        const f4 g = {act.x > 0.f ? ga.x : 0.f, act.y > 0.f ? ga.y : 0.f, act.z > 0.f ? ga.z : 0.f,
+                      act.w > 0.f ? ga.w : 0.f};
+        f4* dst = reinterpret_cast<f4*>(gn + ((size_t)c * H + iy) * W + ix);
+        if (PREBN) {
+          *dst = g;
+          st1[c] += (g.x + g.y) + (g.z + g.w);
+          st2[c] += (g.x * act.x + g.y * act.y) + (g.z * act.z + g.w * act.w);
+        } else {
+          *dst = accum ? *reinterpret_cast<const f4*>(sOld + li) + g : g;
+        }
+      }
+    }
+  }
+  for (int p = tid; p < ((dbg & 1) || (S == 1 && a.vin) ? 0 : NP); p += 256) {
     const int r = p / W, ix = p - r * W, iy = iy0 + r;
     int srow[K], scol[K];
     float mrow[K], mcol[K];
@@ -2420,6 +2570,7 @@ bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st) {
     a.nblk = N * nb * G;
     const bool vec = a.W % 4 == 0 && (((uintptr_t)a.x) & 15) == 0;
     a.variant = (a.variant & ~1) | (vec ? 1 : 0);
+    a.vout = (vec_mask() >> (CG == 4 ? 0 : 1)) & 1;
     maxblk = std::max(maxblk, a.nblk);
     lds = std::max(lds, band_bytes(nb));
   }
@@ -2474,12 +2625,19 @@ void launch_pool_fwd_multi(PoolFwdBatch b, hipStream_t st) {
 void launch_pool_bwd_multi(const PoolBwdBatch& b, hipStream_t st) {
   int maxblk = 0;
   size_t lds = 0;
+  bool v4 = !getenv("KATIB_HIP_POOL_BWD_SCALAR");
+  auto al = [](const void* p, uintptr_t m) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & (m - 1)) == 0; };
   for (int i = 0; i < b.n; ++i) {
     const PoolBwdArgs& a = b.e[i];
     maxblk = std::max(maxblk, a.N * a.C);
     lds = std::max(lds, sizeof(float) * 2 * a.Ho * a.Wo + a.Ho * a.Wo + 16);
+    v4 = v4 && (a.Ho * a.Wo) % 4 == 0 && (a.H * a.W) % 4 == 0 && a.W % 4 == 0 && al(a.ga.g, 16) && al(a.gm.g, 16) &&
+         al(a.ga.z, 4 * sizeof(zt)) && al(a.gm.z, 4 * sizeof(zt)) && al(a.amax, 4) && al(a.dout_id, 16) &&
+         al(a.gx, 16) && (!a.ga.z || !a.gm.z || a.ga.g == a.gm.g);
+    for (int j = 0; j < a.nextra; ++j) v4 = v4 && al(a.extra[j], 16);
   }
-  hipLaunchKernelGGL(pool_bwd_multi_kernel, dim3(maxblk, b.n), dim3(256), lds, st, b);
+  if (v4) hipLaunchKernelGGL(pool_bwd_multi_kernel<true>, dim3(maxblk, b.n), dim3(256), lds, st, b);
+  else hipLaunchKernelGGL(pool_bwd_multi_kernel<false>, dim3(maxblk, b.n), dim3(256), lds, st, b);
 }
 
 // LDS floats of one dw_bwd_plane band (nb bands per image)
@@ -2568,6 +2726,7 @@ bool launch_dw_bwd_multi(DwBwdBatch b, hipStream_t st) {
       nb *= 2;
     a.nbands = nb;
     a.nblk = a.N * nb * G;
+    a.vin = (vec_mask() >> (C == 4 ? 2 : 3)) & 1;
     maxblk = std::max(maxblk, a.nblk);
     lds = std::max(lds, sizeof(float) * dw_plane_floats(a, K, DIL, S, nb, false, C));
   }
