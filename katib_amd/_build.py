@@ -15,6 +15,7 @@ import os
 import subprocess
 import sys
 import sysconfig
+import time
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 NATIVE_SRC = os.path.join(PKG_DIR, "csrc", "native")
@@ -114,6 +115,7 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", 
         return ""
     if not force and not _newer(out, deps):
         return out
+    t_start = time.time()
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
     hipcc = os.path.join(rocm, "bin", "hipcc")
     torch_inc = ce.include_paths()  # torch + torch/csrc/api
@@ -141,12 +143,16 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", 
             cmd = pending.pop(0)
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
-            running.append((cmd, subprocess.Popen(cmd)))
-        cmd, proc = running.pop(0)
+            running.append((cmd, subprocess.Popen(cmd), time.time()))
+        cmd, proc, t0 = running.pop(0)
         if proc.wait() != 0:
-            for _, p in running:
+            for _, p, _ in running:
                 p.wait()
             raise subprocess.CalledProcessError(proc.returncode, cmd)
+        # date the object to when its compile STARTED: a source edited while hipcc ran (whose
+        # device and host passes may then have read different versions) stays newer than the
+        # object, so the next build recompiles it instead of linking a torn object
+        os.utime(cmd[-1], (t0, t0))
     link = [hipcc, "-shared", "-fPIC", f"--offload-arch={arch}"] + objs + [
         f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
         f"-Wl,-rpath,{torch_lib}", "-o", out + ".tmp"]
@@ -154,6 +160,7 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", 
         print(" ".join(link), file=sys.stderr)
     subprocess.check_call(link)
     os.replace(out + ".tmp", out)
+    os.utime(out, (t_start, t_start))
     return out
 
 

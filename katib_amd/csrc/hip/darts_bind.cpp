@@ -250,12 +250,10 @@ void dwpw_fwd(std::vector<py::tuple> calls, int64_t K, int64_t dil, int64_t S, i
 // Mixed (K, dil, S, input-BN) entries of one node stage in one launch:
 // (x, dw, pw, inbn|None, d, z, stats|None, K, dil, S, pad) per entry. Entries that do not fit the
 // plane kernels (channel counts, alignment) run as per-group launches instead.
-void dwpw_fwd_multi(std::vector<py::tuple> calls) {
+static void fill_dwpw_multi(const std::vector<py::tuple>& calls, DwPwMultiBatch& bt, int64_t* kk, int64_t* dd,
+                            int64_t* ss, int64_t* pp, bool* pre) {
   TORCH_CHECK(!calls.empty() && (int)calls.size() <= DwPwMultiBatch::kCap, "1..", DwPwMultiBatch::kCap, " entries");
-  DwPwMultiBatch bt{};
   bt.n = calls.size();
-  int64_t kk[DwPwMultiBatch::kCap], dd[DwPwMultiBatch::kCap], ss[DwPwMultiBatch::kCap], pp[DwPwMultiBatch::kCap];
-  bool pre[DwPwMultiBatch::kCap];
   for (int i = 0; i < bt.n; ++i) {
     const py::tuple& t = calls[i];
     TORCH_CHECK(t.size() == 11, "dwpw_fwd_multi entry: (x, dw, pw, inbn, d, z, stats, K, dil, S, pad)");
@@ -266,6 +264,13 @@ void dwpw_fwd_multi(std::vector<py::tuple> calls) {
   tail_begin(bt.tail);
   for (int i = 0; i < bt.n; ++i) tail_add(bt.tail, bt.e[i].stats, 2 * bt.e[i].C, 2 * bt.e[i].C);
   tail_close(bt.tail);
+}
+
+void dwpw_fwd_multi(std::vector<py::tuple> calls) {
+  DwPwMultiBatch bt{};
+  int64_t kk[DwPwMultiBatch::kCap], dd[DwPwMultiBatch::kCap], ss[DwPwMultiBatch::kCap], pp[DwPwMultiBatch::kCap];
+  bool pre[DwPwMultiBatch::kCap];
+  fill_dwpw_multi(calls, bt, kk, dd, ss, pp, pre);
   if (launch_dwpw_multi(bt, cur_stream())) return;
   for (int i = 0; i < bt.n; ++i) {  // fallback: one launch per entry (the plane path's band count is per batch)
     DwPwFwdBatch one{};
@@ -312,9 +317,8 @@ void pw_fwd(std::vector<py::tuple> calls, int64_t S) {
 }
 
 // (x, zavg, zmax, stats_avg|None, stats_max|None, amax|None[, S]); S < 0: per-entry S (7th field)
-static void pool_fwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
+static void fill_pool_fwd(const std::vector<py::tuple>& calls, int64_t S_all, PoolFwdBatch& bt) {
   check_batch<PoolFwdBatch>(calls);
-  PoolFwdBatch bt{};
   bt.n = calls.size();
   for (int i = 0; i < bt.n; ++i) {
     const py::tuple& t = calls[i];
@@ -344,6 +348,11 @@ static void pool_fwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
     tail_add(bt.tail, bt.e[i].stats_max, 2 * bt.e[i].C, 2 * bt.e[i].C);
   }
   tail_close(bt.tail);
+}
+
+static void pool_fwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
+  PoolFwdBatch bt{};
+  fill_pool_fwd(calls, S_all, bt);
   if (S_all > 0) launch_pool_fwd(bt, S_all, cur_stream());
   else launch_pool_fwd_multi(bt, cur_stream());
 }
@@ -351,6 +360,20 @@ static void pool_fwd_impl(std::vector<py::tuple> calls, int64_t S_all) {
 void pool_fwd(std::vector<py::tuple> calls, int64_t S) { pool_fwd_impl(calls, S); }
 // stride-1 and stride-2 pools of a node in one launch: (..., amax|None, S) per entry
 void pool_fwd_multi(std::vector<py::tuple> calls) { pool_fwd_impl(calls, -1); }
+
+// a node's stage-1 dw-pw entries and its pools (both read only the node inputs) in ONE launch
+// when the fused narrow-layer plane path applies; otherwise the two launches above
+void dwpw_pool_fwd_multi(std::vector<py::tuple> dcalls, std::vector<py::tuple> pcalls) {
+  DwPwMultiBatch bt{};
+  int64_t kk[DwPwMultiBatch::kCap], dd[DwPwMultiBatch::kCap], ss[DwPwMultiBatch::kCap], pp[DwPwMultiBatch::kCap];
+  bool pre[DwPwMultiBatch::kCap];
+  fill_dwpw_multi(dcalls, bt, kk, dd, ss, pp, pre);
+  PoolFwdBatch pb{};
+  fill_pool_fwd(pcalls, -1, pb);
+  if (launch_dwpw_pool_multi(bt, pb, cur_stream())) return;
+  dwpw_fwd_multi(dcalls);
+  launch_pool_fwd_multi(pb, cur_stream());
+}
 
 // calls: per edge (zs, bns, widx, w|None, id_idx, xid|None, upd); all edges summed into `out`
 void combine_fwd(std::vector<py::tuple> calls, OptT gamma, OptT beta, Tensor out, double momentum,
@@ -786,6 +809,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_bwd", &pool_bwd);
   m.def("dwpw_fwd_multi", &dwpw_fwd_multi, "mixed (K, dil, S) dw-pw entries of one node stage in one launch");
   m.def("pool_fwd_multi", &pool_fwd_multi, "stride-1 and stride-2 pools in one launch");
+  m.def("dwpw_pool_fwd_multi", &dwpw_pool_fwd_multi, "a node's stage-1 dw-pw entries and its pools in one launch");
   m.def("pool_bwd_multi", &pool_bwd_multi, "stride-1 and stride-2 pool backward in one launch");
   m.def("edge_bwd", &edge_bwd, "whole input gradient of a node's edges (convs, pools, identity) in one launch");
   m.def("set_max_blocks", &set_max_blocks);

@@ -230,6 +230,14 @@ void launch_pool_bwd(const PoolBwdBatch& b, int S, hipStream_t st);
 // mixed-variant launches: one launch for entries with different kernel size / dilation / stride
 bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st);
 void launch_pool_fwd_multi(PoolFwdBatch b, hipStream_t st);
+// a node's pool entries beside its stage-1 dw-pw entries in one launch (no fold tail)
+struct PoolFwdEntries {
+  PoolFwdArgs e[PoolFwdBatch::kCap];
+  int n;
+};
+static_assert(sizeof(DwPwMultiBatch) + sizeof(PoolFwdEntries) <= 4096, "kernarg segment");
+// false: nothing launched (not the fused narrow-layer plane path, or a self-fold tail is on)
+bool launch_dwpw_pool_multi(DwPwMultiBatch b, const PoolFwdBatch& pb, hipStream_t st);
 void launch_pool_bwd_multi(const PoolBwdBatch& b, hipStream_t st);
 void launch_combine_fwd(const CombineFwdBatch& b, hipStream_t st);
 // false (nothing launched): shapes / alignment outside the fused kernel's plane layout

@@ -298,6 +298,13 @@ DWB_MULTI = __import__("os").environ.get("KATIB_HIP_DWB_MULTI", "1") != "0"
 EDGE_BWD = __import__("os").environ.get("KATIB_HIP_EDGE_BWD", "0") != "0"
 
 
+# A node's pools launched beside its stage-1 dw-pw entries (one launch instead of two per node).
+# Opt-in (KATIB_HIP_JOINT_POOL=1): measured a wash on the B5 step (6.98 vs 6.96 ms,
+# profiles/darts_vec_ab_r04.log) - the pool workgroups (highest blockIdx.y) dispatch after the dw-pw
+# bands anyway, so only the ~1.6 us launch boundary goes.
+JOINT_POOL = __import__("os").environ.get("KATIB_HIP_JOINT_POOL", "0") != "0"
+
+
 def _dwpw_multi(entries):
     """dw-pw entries (x, dw, pw, inbn, d, z, stats, K, dil, S, pad) of one stage, mixed kernel sizes,
     dilations and strides: one launch per 16 entries (per (K, dil, S) group with MULTI off)."""
@@ -484,8 +491,15 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
     # one): independent entries overlap on the chip instead of running as 4-9 serial launches
     # (forking the groups over side streams - concurrent graph branches - measured slower on
     # MI355X: B5 step 15.4 ms vs 13.05 ms sequential)
-    _dwpw_multi([(*c, K, dil, S, pad) for (K, dil, S, pad), calls in dw_groups.items() for c in calls])
-    _pool_multi([(*c, S) for S, calls in pool_groups.items() for c in calls])
+    dw1 = [(*c, K, dil, S, pad) for (K, dil, S, pad), calls in dw_groups.items() for c in calls]
+    pools = [(*c, S) for S, calls in pool_groups.items() for c in calls]
+    if JOINT_POOL and MULTI and dw1 and pools and len(dw1) <= 16 and len(pools) <= _CAP["pool_fwd"]:
+        # the pools beside the stage-1 dw-pw bands in one launch (both read only the node inputs;
+        # the binding falls back to the two launches where the plane path does not apply)
+        _K.dwpw_pool_fwd_multi(dw1, pools)
+    else:
+        _dwpw_multi(dw1)
+        _pool_multi(pools)
     if fr_calls:
         _launch("pw_fwd", fr_calls, 2)
     defer = training and _defer(dev)
