@@ -128,8 +128,10 @@ class DartsSearch:
         # concurrent finite-difference Hessian passes (HIP path): w + eps dw' and w - eps dw' as
         # two independent graph branches - their own weight copies, alpha-gradient leaves and BN
         # running statistics, merged by one kernel after the join (KATIB_DARTS_HESS_CONCURRENT=0:
-        # the sequential in-place perturbation)
-        self.hess_concurrent = (self.device.type == "cuda" and self.hd is not None
+        # the sequential in-place perturbation). Not with SyncBN: its in-pass fold + cross-rank sums
+        # share one workspace whose calls must pair up in the same order on every rank, which two
+        # concurrently running branches do not guarantee (the ranks deadlock)
+        self.hess_concurrent = (self.device.type == "cuda" and self.hd is not None and not self.sync_bn
                                 and __import__("os").environ.get("KATIB_DARTS_HESS_CONCURRENT", "1") != "0")
         if self.hess_concurrent:
             self.Wp = torch.empty_like(self.W)

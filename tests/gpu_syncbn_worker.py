@@ -35,10 +35,14 @@ def main():
     dp = DartsSearch(layout, dev, comm, seed=3, capture=True, sync_bn=sync)
     sl = slice(r * B // W, (r + 1) * B // W)
     W1 = None
+    verbose = os.environ.get("SYNCBN_VERBOSE") == "1"
     for i, (tx, ty, vx, vy) in enumerate(data):
         dp.step(tx[sl], ty[sl], vx[sl], vy[sl])
         if i == 0:
             W1 = dp.W.cpu()
+        if verbose:
+            torch.cuda.synchronize()
+            print("rank %d step %d" % (r, i), file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if comm.xgmi is not None:
         comm.xgmi.check()
