@@ -183,6 +183,19 @@ __device__ __forceinline__ int wave_scatter_index(int lane) {
   return idx;
 }
 
+// wave sums of M accumulators (any M) added into dst[0 .. M): power-of-two chunks of at most 64
+// through the reduce-scatter (a 96-entry weight-gradient tile is 64 + 32, not 96 separate
+// 6-step wave sums)
+template <int M>
+__device__ __forceinline__ void wave_sums_to_lds(float* acc, float* dst, int lane) {
+  if constexpr (M > 0) {
+    constexpr int P = M >= 64 ? 64 : (M >= 32 ? 32 : (M >= 16 ? 16 : (M >= 8 ? 8 : (M >= 4 ? 4 : (M >= 2 ? 2 : 1)))));
+    const float s = wave_reduce_scatter<P>(acc);
+    if ((lane & (64 / P - 1)) == 0) atomicAdd(dst + wave_scatter_index<P>(lane), s);
+    wave_sums_to_lds<M - P>(acc + P, dst + P, lane);
+  }
+}
+
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

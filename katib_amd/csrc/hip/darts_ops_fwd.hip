@@ -271,29 +271,11 @@ static bool try_pw_fwd_wave(const PwFwdBatch& b, hipStream_t st) {
   return true;
 }
 
-template <int CI, int CO>
-static bool try_pw_fwd_px(const PwFwdBatch& b, hipStream_t st) {
-  static const bool tiled = getenv("KATIB_HIP_PW_FWD_TILED") != nullptr;
-  const PwFwdArgs& a = b.e[0];
-  if (tiled || a.Cin != CI || a.Cout != CO || a.Wo % 4 != 0) return false;
-  for (int e = 0; e < b.n; ++e) {  // 16-byte z stores and flat-input loads
-    const PwFwdArgs& x = b.e[e];
-    const bool flat = !x.relu || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);
-    if ((((uintptr_t)x.z) & (4 * sizeof(zt) - 1)) || (flat && (((uintptr_t)x.x) & (x.relu ? 15 : 4 * sizeof(zt) - 1))))
-      return false;
-  }
-  const int total4 = a.N * a.Ho * a.Wo / 4;
-  const int per_edge = std::max(1, std::min((total4 + 255) / 256, max_blocks() / std::max(b.n, 1)));
-  hipLaunchKernelGGL((pw_fwd_px_kernel<CI, CO>), dim3(per_edge, b.n), dim3(256), 0, st, b);
-  return true;
-}
-
 void launch_pw_fwd(const PwFwdBatch& b, hipStream_t st) {
   const PwFwdArgs& a = b.e[0];
-  // narrow layers (the B5 supernet): pixel-quad per thread
-  if (try_pw_fwd_px<4, 4>(b, st) || try_pw_fwd_px<4, 8>(b, st) || try_pw_fwd_px<12, 8>(b, st) ||
-      try_pw_fwd_px<8, 4>(b, st) || try_pw_fwd_px<8, 8>(b, st))
-    return;
+  // (narrow layers stay on the 64-pixel tiles below: a pixel-quad-per-thread kernel had too few
+  // waves at B5 sizes - 32-128 workgroups - and measured 333 vs 281 us per step,
+  // profiles/darts_vec_ab_r04.log)
   if (try_pw_fwd_wave<48, 16>(b, st) || try_pw_fwd_wave<48, 32>(b, st) || try_pw_fwd_wave<64, 32>(b, st) ||
       try_pw_fwd_wave<32, 16>(b, st) || try_pw_fwd_wave<16, 16>(b, st) || try_pw_fwd_wave<32, 32>(b, st) ||
       try_pw_fwd_wave<64, 64>(b, st) || try_pw_fwd_wave<128, 64>(b, st))  // 128 -> 64: last-cell preprocess

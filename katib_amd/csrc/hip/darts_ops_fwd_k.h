@@ -486,82 +486,6 @@ static __global__ void __launch_bounds__(256) pw_fwd_kernel(PwFwdBatch bt) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// pw_fwd_px: pw_fwd for the narrow layers (the B5 supernet's preprocess 4 -> 4, 4 -> 8, 12 -> 8 and
-// FactorizedReduce halves 8 -> 4): 4 consecutive output pixels of one row per thread with every input
-// channel in registers (one 16-byte load per channel, or two for a stride-2 FR half), Cout x 4
-// outputs as 16-byte stores, BN statistics per thread reduced once per workgroup. The tiled kernel
-// above stages 64-pixel tiles through LDS and runs two 6-step wave sums per output channel and tile.
-// Host-checked: Wo % 4 == 0, z (and a flat x) 16-byte aligned.
-// ------------------------------------------------------------------------------------------------
-template <int CI, int CO>
-__global__ void __launch_bounds__(256) pw_fwd_px_kernel(PwFwdBatch bt) {
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const PwFwdArgs& a = bt.e[blockIdx.y];
-  const int HWo = a.Ho * a.Wo, Wo = a.Wo;
-  const int total4 = a.N * HWo / 4;
-  const bool flat = !a.relu || (a.S == 1 && a.off == 0 && a.H == a.Ho && a.W == a.Wo);
-  const bool fr2 = a.S == 2 && a.H == 2 * a.Ho && a.W == 2 * a.Wo && a.W % 4 == 0 && a.off <= 1 &&
-                   ((uintptr_t)a.x & 15) == 0;
-  __shared__ float sStat[2 * CO];
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (tid < 2 * CO) sStat[tid] = 0.f;
-  __syncthreads();
-  float st[2 * CO];
-#pragma unroll
-  for (int c = 0; c < 2 * CO; ++c) st[c] = 0.f;
-  for (int i4 = blockIdx.x * 256 + tid; i4 < total4; i4 += gridDim.x * 256) {
-    const int pix = i4 * 4, n = pix / HWo, p = pix - n * HWo;
-    f4 v[CI];
-#pragma unroll
-    for (int ci = 0; ci < CI; ++ci) {
-      if (flat) {
-        if (a.relu) {
-          const f4 t = *reinterpret_cast<const f4*>(static_cast<const float*>(a.x) +
-                                                    plane_off(n, ci, a.N, CI, a.xnodes, HWo) + p);
-          v[ci] = f4{fmaxf(t.x, 0.f), fmaxf(t.y, 0.f), fmaxf(t.z, 0.f), fmaxf(t.w, 0.f)};
-        } else {
-          v[ci] = zld4(static_cast<const zt*>(a.x) + ((size_t)n * CI + ci) * HWo + p);
-        }
-      } else if (fr2) {
-        const float* plane = static_cast<const float*>(a.x) + plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W);
-        float v0, v1, v2, v3;
-        fr2_pair(plane, a.W, Wo, a.off, p, v0, v1);
-        fr2_pair(plane, a.W, Wo, a.off, p + 2, v2, v3);
-        v[ci] = f4{v0, v1, v2, v3};
-      } else {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int q = p + t, oy = q / Wo, ox = q - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
-          v[ci][t] = (iy < a.H && ix < a.W)
-                         ? fmaxf(static_cast<const float*>(a.x)[plane_off(n, ci, a.N, CI, a.xnodes, (size_t)a.H * a.W) +
-                                                                 (size_t)iy * a.W + ix], 0.f)
-                         : 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int co = 0; co < CO; ++co) {
-      f4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ci = 0; ci < CI; ++ci) z += a.pw[co * CI + ci] * v[ci];  // uniform weights: scalar loads
-      zst4(a.z + ((size_t)n * a.CoutTotal + a.co_off + co) * HWo + p, z);
-      st[co] += (z.x + z.y) + (z.z + z.w);
-      st[CO + co] += (z.x * z.x + z.y * z.y) + (z.z * z.z + z.w * z.w);
-    }
-  }
-  if (a.stats) {
-    const float s = wave_reduce_scatter<2 * CO>(st);
-    if ((lane & (32 / CO - 1)) == 0) atomicAdd(sStat + wave_scatter_index<2 * CO>(lane), s);
-    __syncthreads();
-    if (tid < 2 * CO) {
-      const int hi = tid >= CO;
-      atomicAdd(a.stats + rep_slot() * 2 * a.CoutTotal + hi * a.CoutTotal + a.co_off + (tid - hi * CO), (double)sStat[tid]);
-    }
-  }
-  if (bt.tail.ctr) fold_tail(bt.tail);
-}
-
-// ------------------------------------------------------------------------------------------------
 // pool_fwd: avg (count_include_pad=False) and max 3x3/pad 1, stride S. One block per (n, c) plane.
 // ------------------------------------------------------------------------------------------------
 template <int S, bool V4 = false>

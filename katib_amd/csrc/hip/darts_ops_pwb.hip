@@ -310,17 +310,7 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
     }
   }
   if (!want_w) return;
-  constexpr int M = CI * CO;
-  if (M <= 64 && (M & (M - 1)) == 0) {
-    const float s = wave_reduce_scatter<(M <= 64 ? M : 64)>(gacc);
-    if ((lane & (64 / M - 1)) == 0) atomicAdd(sGW + wave_scatter_index<(M <= 64 ? M : 64)>(lane), s);
-  } else {
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      const float s = wave_sum(gacc[i]);
-      if (lane == 0) atomicAdd(sGW + i, s);
-    }
-  }
+  wave_sums_to_lds<CI * CO>(gacc, sGW, lane);
   __syncthreads();
   float* gW = a.gW + (size_t)rep_slot() * a.gstride;
   for (int i = tid; i < CI * CO; i += 256) atomicAdd(gW + i, sGW[i]);

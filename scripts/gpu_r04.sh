@@ -27,7 +27,7 @@ step() {  # step <name> <timeout> <cmd...>
 for s in "$@"; do
   case $s in
     tests)
-      step pytest-gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider || exit 1
+      step pytest-gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider || exit 1
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench) step bench 600 python bench.py || exit 1 ;;
     quick) step quick 300 python bench.py --trials 0 --b1 0 --comparator-steps 0 --full-search 0 || exit 1 ;;
