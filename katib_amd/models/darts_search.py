@@ -128,11 +128,19 @@ class DartsSearch:
         # concurrent finite-difference Hessian passes (HIP path): w + eps dw' and w - eps dw' as
         # two independent graph branches - their own weight copies, alpha-gradient leaves and BN
         # running statistics, merged by one kernel after the join (KATIB_DARTS_HESS_CONCURRENT=0:
-        # the sequential in-place perturbation). Not with SyncBN: its in-pass fold + cross-rank sums
-        # share one workspace whose calls must pair up in the same order on every rank, which two
-        # concurrently running branches do not guarantee (the ranks deadlock)
-        self.hess_concurrent = (self.device.type == "cuda" and self.hd is not None and not self.sync_bn
+        # the sequential in-place perturbation). Under SyncBN the side branch folds through a
+        # SyncBN of its own: the one-shot fold + cross-rank sum calls of one workspace must pair up
+        # in the same order on every rank, which two concurrently running branches sharing one
+        # workspace do not guarantee (the ranks deadlock); one workspace per branch keeps each
+        # branch's calls in program order. Without the one-shot path (host-side sums) the passes
+        # stay sequential.
+        self.hess_concurrent = (self.device.type == "cuda" and self.hd is not None
                                 and __import__("os").environ.get("KATIB_DARTS_HESS_CONCURRENT", "1") != "0")
+        self._hsync_side = None
+        if self.hess_concurrent and self.sync_bn:
+            if self._hsync is not None and self._hsync.capturable:
+                self._hsync_side = self.hd.SyncBN(self.comm)  # collective, same order on every rank
+            self.hess_concurrent = self._hsync_side is not None and self._hsync_side.capturable
         if self.hess_concurrent:
             self.Wp = torch.empty_like(self.W)
             self.Wm = torch.empty_like(self.W)
@@ -221,7 +229,7 @@ class DartsSearch:
             K.optim_hessian_split(3, self.W, self.gWv, *args, nparts, *tail)
             main = torch.cuda.current_stream()
             self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):  # the +eps pass on its own branch
+            with torch.cuda.stream(self._side), self._scope(self._hsync_side):  # the +eps pass on its own branch
                 loss, _ = self._loss(tx, ty, self.Wp_views, *self._arch(self.Aw_p), self.bn_plus)
                 torch.autograd.backward(loss, grad_tensors=self._one_side, inputs=self.Aw_p)
             loss, _ = self._loss(tx, ty, self.Wm_views, *self._arch(self.Aw), self.bn)
@@ -333,9 +341,9 @@ class DartsSearch:
             (lambda: (self._seg_weight_update(), end()), []),
         ]
 
-    def _scope(self):
+    def _scope(self, sync=None):
         if self.hd is not None:
-            return self.hd.sync_scope(self._hsync)
+            return self.hd.sync_scope(sync if sync is not None else self._hsync)
         import contextlib
 
         return contextlib.nullcontext()
