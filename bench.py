@@ -174,13 +174,19 @@ def main():
     ms_step = comm.allreduce_max(dt * 1000.0 / args.steps)
     loss = float(search.loss_out)
 
-    # validation pass cost (no_grad forward, BN in eval mode) -- part of every search epoch
-    vbatches = [v for _, v in batches][: args.valid_batches]
-    for vx, vy in vbatches[:2]:
+    # validation pass cost (no_grad forward, BN in eval mode) -- part of every search epoch; the
+    # validation batches go EVAL_GROUP at a time through one captured forward (the same losses and
+    # correct counts: eval-mode BN is per sample), timed per original batch
+    from katib_amd.models.darts_search import EVAL_GROUP, eval_groups
+
+    nv = min(len(batches), -(-max(args.valid_batches, 1) // EVAL_GROUP) * EVAL_GROUP)  # whole groups
+    vbatches = [v for _, v in batches][:nv]
+    vgroups = list(eval_groups(vbatches))
+    for vx, vy in (vgroups[0], vgroups[-1]):  # every group shape captured before timing
         search.evaluate(vx, vy)
     sync()
     t1 = time.perf_counter()
-    for vx, vy in vbatches:
+    for vx, vy in vgroups:
         search.evaluate(vx, vy)
     sync()
     ms_valid = comm.allreduce_max((time.perf_counter() - t1) * 1000.0 / max(len(vbatches), 1))
@@ -200,8 +206,7 @@ def main():
             for i in range(steps_per_epoch):
                 (tx, ty), (vx, vy) = batches[i % len(batches)]
                 search.step(tx, ty, vx, vy)
-            for i in range(steps_per_epoch):
-                vx, vy = vbatches[i % len(vbatches)]
+            for vx, vy in eval_groups(vbatches[i % len(vbatches)] for i in range(steps_per_epoch)):
                 search.evaluate(vx, vy)
         sync()
         comm.barrier()

@@ -54,11 +54,19 @@ def validate(search, comm, batches, max_batches: int = 0):
     of [sum loss*n, sum correct, n] gives ``sum(correct) / sum(n)`` over the whole split."""
     import torch
 
+    from ..models.darts_search import eval_groups
+
     search.sync_bn_stats()
     acc = torch.zeros(3, dtype=torch.float64, device=search.device)
-    for i, (vx, vy) in enumerate(batches):
-        if max_batches and i >= max_batches:
-            break
+
+    def capped():
+        for i, b in enumerate(batches):
+            if max_batches and i >= max_batches:
+                return
+            yield b
+
+    # consecutive batches merged per captured forward (models/darts_search.py EVAL_GROUP)
+    for vx, vy in eval_groups(capped()):
         loss, top1, _ = search.evaluate(vx, vy)
         acc[:2] += torch.stack([loss, top1]).double() * vy.numel()
         acc[2] += vy.numel()

@@ -337,6 +337,40 @@ def test_evaluate_graph_matches_eager():
     dops.set_backend("torch")
 
 
+def test_grouped_validation_matches_per_batch():
+    """Validation batches merged per captured eval forward (models/darts_search.py eval_groups,
+    used by the workload and bench.py) give the per-batch losses and correct counts: eval-mode BN
+    normalises every sample with the running statistics."""
+    from katib_amd.models.darts import DartsLayout
+    from katib_amd.models.darts_search import DartsSearch, eval_groups
+    from katib_amd.ops import darts as dops
+
+    dev = torch.device("cuda", 0)
+    layout = DartsLayout(ALL, init_channels=4, num_layers=2, num_nodes=3, stem_multiplier=1)
+    gen = torch.Generator(device=dev).manual_seed(9)
+    tx = torch.randn(32, 3, 32, 32, device=dev, generator=gen)
+    ty = torch.randint(0, 10, (32,), device=dev, generator=gen)
+    dops.set_backend("hip")
+    s = DartsSearch(layout, dev, capture=True)
+    s.step(tx, ty, tx, ty)
+    batches = [(torch.randn(32, 3, 32, 32, device=dev, generator=gen), torch.randint(0, 10, (32,), device=dev, generator=gen))
+               for _ in range(6)]
+    per = torch.zeros(2, dtype=torch.float64)
+    for vx, vy in batches:
+        loss, top1, _ = s.evaluate(vx, vy)
+        per += torch.tensor([float(loss), float(top1)], dtype=torch.float64) * vy.numel()
+    grouped = torch.zeros(2, dtype=torch.float64)
+    shapes = []
+    for vx, vy in eval_groups(batches, 4):  # groups of 4 and 2
+        shapes.append(vx.shape[0])
+        loss, top1, _ = s.evaluate(vx, vy)
+        grouped += torch.tensor([float(loss), float(top1)], dtype=torch.float64) * vy.numel()
+    assert shapes == [128, 64]
+    assert abs(grouped[1] - per[1]) < 0.5  # correct counts (integers up to rounding of the fractions)
+    assert abs(grouped[0] - per[0]) < 1e-4 * abs(per[0])
+    dops.set_backend("torch")
+
+
 @pytest.mark.parametrize("C,cell_idx,node", [(4, 0, 1), (8, 1, 1), (16, 0, 2), (8, 1, 2)])
 def test_mixed_node_matches_torch(C, cell_idx, node):
     """All edges of a node in one edge-batched Function (mixed strides in reduction cells)."""
