@@ -51,13 +51,13 @@ __global__ void __launch_bounds__(kThreads) head_fwd_kernel(FwdArgs a) {
     for (int u = 0; u < kU; ++u) {
       const int c = c0 + u * kWaves;
       const float v = wave_sum(s[u]) * inv_hw;
-      if (lane == 0 && c < a.C) {
-        sp[c] = v;
-        a.pooled[(size_t)n * a.C + c] = v;
-      }
+      if (lane == 0 && c < a.C) sp[c] = v;
     }
   }
   __syncthreads();
+  // the pooled features leave after the pooling loop: a global store inside it could alias x, which
+  // kept every channel group's loads behind the previous group's stores (a round trip per group)
+  for (int c = threadIdx.x; c < a.C; c += kThreads) a.pooled[(size_t)n * a.C + c] = sp[c];
   for (int k0 = wid; k0 < a.K; k0 += kWaves * kU) {
     float s[kU];
 #pragma unroll
@@ -122,13 +122,21 @@ __global__ void __launch_bounds__(kThreads) head_bwd_kernel(BwdArgs a) {
   if (threadIdx.x < a.K) sd[threadIdx.x] = g * a.dl[(size_t)n * a.K + threadIdx.x];
   __syncthreads();
   if (a.dx != nullptr) {
+    // d[c] = (dl W)[c] / HW for every channel first (weight loads only, all in flight), then the
+    // broadcast stores: interleaving each channel's stores with the next channel's weight loads
+    // (which may alias dx for the compiler) serialised one round trip per channel - 64 per
+    // workgroup on the darts-gpu.yaml head (47.6 us per launch)
+    __shared__ float sdx[kMaxC];
     const float inv_hw = 1.0f / a.HW;
-    for (int c = wid; c < a.C; c += kWaves) {
+    for (int c = threadIdx.x; c < a.C; c += kThreads) {
       float d = 0.0f;
       for (int k = 0; k < a.K; ++k) d += sd[k] * a.w[(size_t)k * a.C + c];
-      d *= inv_hw;
-      float* dxc = a.dx + plane_off(n, c, a.N, a.C, a.nodes, a.HW);
-      for (int p = lane; p < a.HW; p += kWave) dxc[p] = d;
+      sdx[c] = d * inv_hw;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.C * a.HW; i += kThreads) {
+      const int c = i / a.HW, p = i - c * a.HW;
+      a.dx[plane_off(n, c, a.N, a.C, a.nodes, a.HW) + p] = sdx[c];
     }
   }
   const int rep = n % kRep;
