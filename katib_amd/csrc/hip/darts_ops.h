@@ -194,8 +194,8 @@ using CombineFwdBatch = Batch<CombineFwdArgs, 3>;
 using PwFwdBatch = Batch<PwFwdArgs, 16>;
 using PoolFwdBatch = Batch<PoolFwdArgs, 8>;
 using CombineBwdBatch = Batch<CombineBwdArgs, 4>;
-using PwBwdBatch = Batch<PwBwdArgs, 8>;
-using DwBwdBatch = Batch<DwBwdArgs, 8>;
+using PwBwdBatch = Batch<PwBwdArgs, 16>;  // a node's pointwise backward entries (2 sep stages + 2 dil per edge, <= 4 edges)
+using DwBwdBatch = Batch<DwBwdArgs, 16>;  // a node's stage-1 depthwise backward entries (<= 4 edges x 4)
 using PoolBwdBatch = Batch<PoolBwdArgs, 8>;
 using DwPwMultiBatch = Batch<DwPwFwdArgs, 16>;  // a node's stage-1 (or stage-2) dw-pw entries, mixed K/dil/S
 
