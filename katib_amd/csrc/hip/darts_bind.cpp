@@ -405,7 +405,7 @@ void combine_fwd(std::vector<py::tuple> calls, OptT gamma, OptT beta, Tensor out
       a.bn[k] = make_bn(bns[k], C);
       a.widx[k] = widx[k];
     }
-    TORCH_CHECK((int)upd.size() <= kMaxOps, "too many update-only BN layers");
+    TORCH_CHECK((int)upd.size() <= kMaxUpd, "too many update-only BN layers");
     a.nupd = upd.size();
     for (size_t k = 0; k < upd.size(); ++k) a.upd[k] = make_bn(upd[k], C);
     a.w = ptr_or_null<float>(w); a.id_idx = id_idx; a.xid = ptr_or_null<float>(xid);

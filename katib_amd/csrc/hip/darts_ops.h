@@ -44,6 +44,7 @@ __host__ __device__ __forceinline__ size_t plane_off(int n, int c, int N, int C,
 }
 
 constexpr int kMaxOps = 8;
+constexpr int kMaxUpd = 4;  // update-only BN layers per combine entry (the separable convs' first stages)
 constexpr int kMaxC = 256;
 // Cross-workgroup sums (BN statistics, BN-backward reductions, weight gradients) go to kRep
 // replicas of the accumulator, workgroup b adding into replica b % kRep: global float atomics
@@ -106,7 +107,7 @@ struct PoolFwdArgs {
 
 struct CombineFwdArgs {
   const zt* z[kMaxOps]; BNRef bn[kMaxOps]; int widx[kMaxOps]; int nops;
-  BNRef upd[kMaxOps]; int nupd;  // extra BN layers whose running stats are updated here (not summed)
+  BNRef upd[kMaxUpd]; int nupd;  // extra BN layers whose running stats are updated here (not summed)
   const float* w; int id_idx; const float* xid; const float* gamma; const float* beta;
   float* out; int N, C, HW; float momentum; int update_running; int accumulate;
 };
@@ -190,7 +191,7 @@ struct Batch {
   static constexpr int kCap = M;
 };
 using DwPwFwdBatch = Batch<DwPwFwdArgs, 8>;
-using CombineFwdBatch = Batch<CombineFwdArgs, 3>;
+using CombineFwdBatch = Batch<CombineFwdArgs, 4>;  // all edges of a node (B5: up to 4) in one launch
 using PwFwdBatch = Batch<PwFwdArgs, 16>;
 using PoolFwdBatch = Batch<PoolFwdArgs, 8>;
 using CombineBwdBatch = Batch<CombineBwdArgs, 4>;

@@ -175,7 +175,7 @@ def _fold64(segs, dev=None):
     """fold_f64 launch between producers and consumers, unless the producers folded themselves."""
     if FOLD and (dev is None or not _selffold(dev)):
         _fold(segs)
-_CAP = {"combine_fwd": 3, "dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 16,
+_CAP = {"combine_fwd": 4, "dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 16,
         "dw_bwd": 16, "pool_bwd": 8}
 _REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
 
