@@ -196,9 +196,9 @@ using PwFwdBatch = Batch<PwFwdArgs, 16>;
 using PoolFwdBatch = Batch<PoolFwdArgs, 8>;
 using CombineBwdBatch = Batch<CombineBwdArgs, 4>;
 using PwBwdBatch = Batch<PwBwdArgs, 16>;  // a node's pointwise backward entries (2 sep stages + 2 dil per edge, <= 4 edges)
-using DwBwdBatch = Batch<DwBwdArgs, 16>;  // a node's stage-1 depthwise backward entries (<= 4 edges x 4)
+using DwBwdBatch = Batch<DwBwdArgs, 20>;  // a node's stage-1 depthwise backward entries (<= 5 edges x 4: darts-gpu.yaml)
 using PoolBwdBatch = Batch<PoolBwdArgs, 8>;
-using DwPwMultiBatch = Batch<DwPwFwdArgs, 16>;  // a node's stage-1 (or stage-2) dw-pw entries, mixed K/dil/S
+using DwPwMultiBatch = Batch<DwPwFwdArgs, 20>;  // a node's stage-1 (or stage-2) dw-pw entries (<= 5 edges x 4), mixed K/dil/S
 
 // Whole input gradient of one DARTS edge (except the stride-2 skip's FactorizedReduce, which
 // accumulates afterwards): the transposed depthwise convolutions of the separable stage-1 and the

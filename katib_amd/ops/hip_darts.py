@@ -176,7 +176,7 @@ def _fold64(segs, dev=None):
     if FOLD and (dev is None or not _selffold(dev)):
         _fold(segs)
 _CAP = {"combine_fwd": 4, "dwpw_fwd": 8, "pw_fwd": 16, "pool_fwd": 8, "combine_bwd_reduce": 4, "pw_bwd": 16,
-        "dw_bwd": 16, "pool_bwd": 8}
+        "dw_bwd": 20, "pool_bwd": 8}
 _REPLICATED: List[Tuple[weakref.ref, int]] = []  # (buffer [REP][n], n)
 
 
@@ -307,12 +307,12 @@ JOINT_POOL = __import__("os").environ.get("KATIB_HIP_JOINT_POOL", "0") != "0"
 
 def _dwpw_multi(entries):
     """dw-pw entries (x, dw, pw, inbn, d, z, stats, K, dil, S, pad) of one stage, mixed kernel sizes,
-    dilations and strides: one launch per 16 entries (per (K, dil, S) group with MULTI off)."""
+    dilations and strides: one launch per 20 entries (per (K, dil, S) group with MULTI off)."""
     if not entries:
         return
     if MULTI:
-        for i in range(0, len(entries), 16):
-            _K.dwpw_fwd_multi(entries[i:i + 16])
+        for i in range(0, len(entries), 20):
+            _K.dwpw_fwd_multi(entries[i:i + 20])
         return
     groups = defaultdict(list)
     for e in entries:
@@ -493,7 +493,7 @@ def _node_forward(xs, ws, specs, bns, params_list, training, momentum, eps, out=
     # MI355X: B5 step 15.4 ms vs 13.05 ms sequential)
     dw1 = [(*c, K, dil, S, pad) for (K, dil, S, pad), calls in dw_groups.items() for c in calls]
     pools = [(*c, S) for S, calls in pool_groups.items() for c in calls]
-    if JOINT_POOL and MULTI and dw1 and pools and len(dw1) <= 16 and len(pools) <= _CAP["pool_fwd"]:
+    if JOINT_POOL and MULTI and dw1 and pools and len(dw1) <= 20 and len(pools) <= _CAP["pool_fwd"]:
         # the pools beside the stage-1 dw-pw bands in one launch (both read only the node inputs;
         # the binding falls back to the two launches where the plane path does not apply)
         _K.dwpw_pool_fwd_multi(dw1, pools)
