@@ -235,3 +235,34 @@ def test_ui_backend_routes(manager):
         assert json.loads(call("/katib/delete_experiment/?experimentName=random-quadratic&namespace=default")) == []
     finally:
         srv.stop()
+
+
+def test_ui_frontend_endpoints_exist(manager):
+    """Contract between the single-page UI and its backend: every ``/katib/...`` path the page
+    calls is routed by the API server (a request may fail on its arguments or a missing resource,
+    but never with the unrouted-path answer)."""
+    import re
+    import urllib.error
+    import urllib.request
+
+    from katib_amd.controller.apiserver import ApiServer
+
+    page = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "katib_amd", "controller",
+                             "ui", "index.html")).read()
+    paths = sorted(set(re.findall(r"""["'`](/katib/[a-z_]+)""", page)))
+    assert len(paths) >= 10, paths
+    srv = ApiServer(manager, port=0).start()
+    base = "http://127.0.0.1:%d" % srv.port
+    post_only = ("create_experiment", "edit_experiment_budget", "add_template", "edit_template", "delete_template")
+    try:
+        for p in paths:
+            post = any(p.endswith(x) for x in post_only)
+            req = urllib.request.Request(base + p + ("" if post else "?namespace=default"),
+                                         data=b"{}" if post else None, method="POST" if post else "GET")
+            try:
+                code, body = urllib.request.urlopen(req).status, b""
+            except urllib.error.HTTPError as ex:
+                code, body = ex.code, ex.read()
+            assert b"could not find the requested resource" not in body, (p, code, body[:200])
+    finally:
+        srv.stop()
