@@ -371,11 +371,16 @@ def test_grouped_validation_matches_per_batch():
     dops.set_backend("torch")
 
 
-@pytest.mark.parametrize("C,cell_idx,node", [(4, 0, 1), (8, 1, 1), (16, 0, 2), (8, 1, 2)])
-def test_mixed_node_matches_torch(C, cell_idx, node):
-    """All edges of a node in one edge-batched Function (mixed strides in reduction cells)."""
+@pytest.mark.parametrize("C,cell_idx,node,joint", [(4, 0, 1, False), (8, 1, 1, False), (16, 0, 2, False), (8, 1, 2, False),
+                                                  (4, 0, 2, True), (8, 1, 2, True)])
+def test_mixed_node_matches_torch(C, cell_idx, node, joint, monkeypatch):
+    """All edges of a node in one edge-batched Function (mixed strides in reduction cells);
+    ``joint``: the opt-in launch of the pools beside the stage-1 dw-pw bands (KATIB_HIP_JOINT_POOL)."""
     from katib_amd.models.darts import DartsNetwork
     from katib_amd.ops import darts as dops
+    from katib_amd.ops import hip_darts
+
+    monkeypatch.setattr(hip_darts, "JOINT_POOL", joint)
 
     layout, W, dev, BNState = _setup(C, N=3)
     cell = layout.cells[cell_idx]
