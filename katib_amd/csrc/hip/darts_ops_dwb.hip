@@ -972,8 +972,10 @@ static void launch_dw_bwd_t(const DwBwdBatch& b, bool prebn, hipStream_t st) {
   const DwBwdArgs& a = b.e[0];
   if (dw_plane_ok(b, K, DIL, S)) {
     // wide layers run in channel groups of KATIB_HIP_DWB_GROUP (4, 8 or 16) channels: 8 measured
-    // 48.2 vs 50.8 ms per darts-gpu.yaml step against 16 (half the LDS per band: fewer, taller bands)
-    static const int grp = getenv("KATIB_HIP_DWB_GROUP") ? atoi(getenv("KATIB_HIP_DWB_GROUP")) : 8;
+    // 48.2 vs 50.8 ms per darts-gpu.yaml step against 16 (half the LDS per band: fewer, taller bands),
+    // and 4 beats 8 on the round-4 kernels (B5 6.37 vs 6.44 ms, default 41.98 vs 42.20 ms,
+    // profiles/darts_dwb_group_ab_r04.log)
+    static const int grp = getenv("KATIB_HIP_DWB_GROUP") ? atoi(getenv("KATIB_HIP_DWB_GROUP")) : 4;
     if (a.C == 4 || grp == 4) return launch_dw_bwd_plane_t<K, DIL, S, 4>(b, prebn, st);
     if (a.C == 8 || grp == 8) return launch_dw_bwd_plane_t<K, DIL, S, 8>(b, prebn, st);
     return launch_dw_bwd_plane_t<K, DIL, S, 16>(b, prebn, st);
@@ -992,8 +994,8 @@ bool launch_dw_bwd_multi(DwBwdBatch b, hipStream_t st) {
   if (b.n < 1) return true;
   const DwBwdArgs& a0 = b.e[0];
   if (!(a0.C == 4 || a0.C == 8 || (a0.C % 16 == 0 && a0.C <= kMaxC)) || !aligned16(b)) return false;
-  static const int grp = getenv("KATIB_HIP_DWB_GROUP") ? atoi(getenv("KATIB_HIP_DWB_GROUP")) : 8;
-  const int C = (a0.C == 4 || grp == 4) ? 4 : 8;  // wide layers: 8-channel groups (launch_dw_bwd_t)
+  static const int grp = getenv("KATIB_HIP_DWB_GROUP") ? atoi(getenv("KATIB_HIP_DWB_GROUP")) : 4;
+  const int C = (a0.C == 4 || grp == 4) ? 4 : 8;  // channel groups as launch_dw_bwd_t
   if (a0.C % C) return false;
   int maxblk = 0;
   size_t lds = 0;
