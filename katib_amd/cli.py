@@ -132,12 +132,13 @@ def cmd_serve(a):
             token = f.read().strip()
     elif os.environ.get("KATIB_AMD_API_TOKEN"):
         token = os.environ["KATIB_AMD_API_TOKEN"]
-    exposed = [x for x in (a.address, a.grpc) if x and not is_loopback(x)]
-    if exposed and token is None and not a.insecure_listen:
+    api_addr = a.address or "0.0.0.0"  # '' binds every interface
+    if not is_loopback(api_addr) and token is None and not a.insecure_listen:
         # the API accepts Job / LocalProcess trials whose command runs as this user: never open
         # it to the network without a token
-        print("refusing to listen on %s without --token-file (or --insecure-listen)" % ", ".join(exposed),
-              file=sys.stderr)
+        print("refusing to listen on %s without --token-file (or --insecure-listen)" % api_addr, file=sys.stderr)
+        return 2
+    if a.grpc and not _grpc_bind_ok(a.grpc, a.insecure_grpc):
         return 2
     m = Manager(state_dir=a.state_dir, num_devices=a.gpus, journal=True)
     if a.config:
@@ -244,9 +245,25 @@ def cmd_edit_budget(a):
     return 0
 
 
+def _grpc_bind_ok(address: str, insecure: bool) -> bool:
+    """The gRPC services (DBManager, Suggestion, EarlyStopping) have no authentication - the HTTP
+    API's bearer token does not cover them - so they bind loopback / unix sockets unless the
+    operator explicitly opts in (``--insecure-grpc``, e.g. behind a firewall or an mTLS proxy)."""
+    from .controller.apiserver import is_loopback
+
+    if is_loopback(address) or insecure:
+        return True
+    print("refusing to serve gRPC on %s: the gRPC services are unauthenticated; bind 127.0.0.1 / a unix "
+          "socket or pass --insecure-grpc" % address, file=sys.stderr)
+    return False
+
+
 def cmd_suggestion_server(a):
     from .algorithms.registry import create_service
     from .rpc.server import make_server
+
+    if not _grpc_bind_ok(a.address, a.insecure_grpc):
+        return 2
 
     svc = create_service(a.algorithm, data_root=a.data_root)
     srv = make_server(a.address, suggestion_service=svc)
@@ -279,6 +296,8 @@ def cmd_earlystopping_server(a):
     from .earlystopping.medianstop import MedianStopService
     from .rpc.server import make_server
 
+    if not _grpc_bind_ok(a.address, a.insecure_grpc):
+        return 2
     marked = []
     svc = MedianStopService(log_source=_GrpcLogSource(a.db_manager) if a.db_manager else None,
                             set_trial_status=lambda n: (marked.append(n), print("early stopped: %s" % n, flush=True)))
@@ -294,6 +313,8 @@ def cmd_db_manager(a):
     from . import native
     from .rpc.server import make_server
 
+    if not _grpc_bind_ok(a.address, a.insecure_grpc):
+        return 2
     db = (a.db or os.environ.get("DB_NAME", "")).lower()
     if db not in ("", "native"):
         from .db.sql import new_observation_db
@@ -389,7 +410,9 @@ def build_parser():
     s.add_argument("--grpc", default="", help="also serve DBManager gRPC here, e.g. 127.0.0.1:6789")
     s.add_argument("--token-file", default="", help="bearer token required by the HTTP API (needed off loopback)")
     s.add_argument("--insecure-listen", action="store_true",
-                   help="allow a non-loopback --address / --grpc without a token (not recommended)")
+                   help="allow a non-loopback --address without a token (not recommended)")
+    s.add_argument("--insecure-grpc", action="store_true",
+                   help="allow a non-loopback --grpc address (the gRPC services have no authentication)")
     s.add_argument("--state-dir", default=None)
     s.add_argument("--gpus", type=int, default=None)
     s.add_argument("--config", default="", help="katib-config.yaml")
@@ -420,11 +443,13 @@ def build_parser():
     g.add_argument("--algorithm", required=True)
     g.add_argument("--address", default="127.0.0.1:6789")
     g.add_argument("--data-root", default="/opt/katib/data")
+    g.add_argument("--insecure-grpc", action="store_true", help="allow a non-loopback --address (no auth)")
     g.set_defaults(fn=cmd_suggestion_server)
 
     es = sub.add_parser("earlystopping-server", help="serve medianstop over gRPC (port 6788)")
     es.add_argument("--address", default="127.0.0.1:6788")
     es.add_argument("--db-manager", default="")
+    es.add_argument("--insecure-grpc", action="store_true", help="allow a non-loopback --address (no auth)")
     es.set_defaults(fn=cmd_earlystopping_server)
 
     d = sub.add_parser("db-manager", help="DBManager gRPC server on the native observation store")
@@ -432,6 +457,7 @@ def build_parser():
     d.add_argument("--journal", default="", help="append-only journal file for persistence")
     d.add_argument("--db", default="", help="native (default) | sqlite | mysql | postgres (else $DB_NAME)")
     d.add_argument("--connect-timeout", type=float, default=60.0, help="seconds to wait for the database")
+    d.add_argument("--insecure-grpc", action="store_true", help="allow a non-loopback --address (no auth)")
     d.set_defaults(fn=cmd_db_manager)
 
     sub.add_parser("metrics-collector", help="file/StdOut metrics collector (reference flags)", add_help=False)

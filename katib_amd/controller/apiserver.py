@@ -68,8 +68,12 @@ def _best_values(trial, logs):
     return best
 
 
+COOKIE = "katib_amd_token"  # UI session cookie name (see Handler._authorized)
+
+
 def is_loopback(address: str) -> bool:
-    """True for addresses only this host can reach (127.0.0.0/8, ::1, localhost, unix sockets)."""
+    """True for addresses only this host can reach (127.0.0.0/8, ::1, localhost, unix sockets).
+    An empty host, ``0.0.0.0`` and ``::`` bind every interface: exposed."""
     host = address.rsplit(":", 1)[0] if address.count(":") == 1 else address
     host = host.strip("[]")
     if address.startswith("unix:") or host in ("localhost", "::1"):
@@ -348,22 +352,39 @@ class ApiServer:
             def log_message(self, fmt, *args):  # quiet
                 pass
 
-            def _authorized(self, path) -> bool:
+            def _authorized(self, path, query) -> bool:
+                """Bearer header (SDK / CLI), or the UI's session cookie. A browser cannot send
+                the header, so opening ``/?token=<token>`` once sets an HttpOnly SameSite=Strict
+                cookie holding it (``self._set_cookie``) and later UI requests carry that."""
+                self._set_cookie = None
                 if server.token is None or path in ("/healthz", "/readyz"):
                     return True
                 import hmac
 
+                want = server.token.encode()
                 got = self.headers.get("Authorization") or ""
-                return hmac.compare_digest(got.encode(), ("Bearer " + server.token).encode())
+                if hmac.compare_digest(got.encode(), b"Bearer " + want):
+                    return True
+                for part in (self.headers.get("Cookie") or "").split(";"):
+                    k, _, v = part.strip().partition("=")
+                    if k == COOKIE and hmac.compare_digest(v.encode(), want):
+                        return True
+                q = (query.get("token") or [""])[0]
+                if q and hmac.compare_digest(q.encode(), want):
+                    self._set_cookie = "%s=%s; HttpOnly; SameSite=Strict; Path=/" % (COOKIE, server.token)
+                    return True
+                return False
 
             def _do(self, method):
                 u = urlparse(self.path)
                 n = int(self.headers.get("Content-Length") or 0)
                 body = self.rfile.read(n) if n else b""
+                query = parse_qs(u.query)
                 try:
-                    if not self._authorized(u.path):
+                    if not self._authorized(u.path, query):
                         raise _Err(401, "Unauthorized", "missing or wrong bearer token")
-                    code, ctype, data = server.handle(method, u.path, parse_qs(u.query), body)
+                    query.pop("token", None)
+                    code, ctype, data = server.handle(method, u.path, query, body)
                 except _Err as e:
                     code, ctype = e.code, "application/json"
                     data = json.dumps({"kind": "Status", "code": e.code, "reason": e.reason,
@@ -375,6 +396,8 @@ class ApiServer:
                 self.send_response(code)
                 self.send_header("Content-Type", ctype)
                 self.send_header("Content-Length", str(len(data)))
+                if getattr(self, "_set_cookie", None):
+                    self.send_header("Set-Cookie", self._set_cookie)
                 self.end_headers()
                 self.wfile.write(data)
 

@@ -758,14 +758,17 @@ class Manager:
                     continue
             gpus = run.plan.total_gpus
             # slots stack on one device only where each slot is its own process (rank plans /
-            # one-GPU replicas); a process that asks for k GPUs gets k different devices
-            distinct = any(rep.gpus > 1 for rep in run.plan.replicas)
+            # one-GPU replicas); a process that asks for k GPUs gets k different devices. Plans
+            # whose replicas all see every device of the trial (share_devices: rank plans,
+            # training-operator jobs) pick their device per rank, so they never need distinct ones.
+            distinct = not run.plan.share_devices and any(rep.gpus > 1 for rep in run.plan.replicas)
             if gpus > 0:
-                if distinct and max(rep.gpus for rep in run.plan.replicas) > self.n_devices:
+                healthy = self.n_devices - len(self.slots.quarantined())
+                if distinct and gpus > healthy:
+                    # acquire(gpus, distinct=True) could never succeed: fail instead of pending forever
                     self._finish_trial(tkey, "Failed", "Unschedulable",
                                        "0/1 nodes are available: insufficient amd.com/gpu (one process requested %d "
-                                       "GPUs, node has %d)" % (max(rep.gpus for rep in run.plan.replicas),
-                                                                self.n_devices))
+                                       "distinct GPUs, node has %d healthy)" % (gpus, healthy))
                     continue
                 if gpus > self.slots.capacity():
                     self._finish_trial(tkey, "Failed", "Unschedulable",

@@ -81,8 +81,9 @@ def render(profile: str, prefix: str, python: str = "", user: str = "katib", sta
            grpc_port: int = 6789, listen: str = "127.0.0.1") -> Dict[str, str]:
     """Write the install of ``profile`` under ``prefix``; returns {relative path: content}.
 
-    Every service binds ``listen`` (loopback by default: the API accepts trials whose command
-    runs as the service user). A non-loopback ``listen`` makes the API require a bearer token,
+    The HTTP API binds ``listen`` (loopback by default: the API accepts trials whose command
+    runs as the service user); the unauthenticated gRPC services always bind loopback. A
+    non-loopback ``listen`` makes the API require a bearer token,
     generated into ``api-token`` (mode 0600) and passed with ``--token-file``. The env file (DB
     password) and the token are written 0600 and chowned to the service user by install.sh."""
     if profile not in PROFILES:
@@ -110,7 +111,9 @@ def render(profile: str, prefix: str, python: str = "", user: str = "katib", sta
         files["api-token"] = secrets.token_hex(32) + "\n"
         secret.add("api-token")
         serve += ["--token-file", os.path.join(prefix, "api-token")]
-    bind = listen + ":%d"
+    # the gRPC services (db-manager, median-stop) carry no authentication: they stay on loopback
+    # whatever ``listen`` says; only the token-protected HTTP API follows ``listen``
+    bind = "127.0.0.1:%d"
     if gpus is not None:
         serve += ["--gpus", str(gpus)]
     units = []

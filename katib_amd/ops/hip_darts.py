@@ -74,6 +74,8 @@ _CTR: Dict[int, torch.Tensor] = {}
 def set_selffold(on: bool):
     """A/B switch for tests and experiments (call between steps, never inside a capture)."""
     global SELFFOLD
+    if on and _SYNC is not None:
+        raise RuntimeError("self-folding producers cannot run under SyncBN (see _check_sync_fold_mode)")
     SELFFOLD = bool(on)
     _K.set_selffold(SELFFOLD)
 _CTR_SIZE = 64 * 33 * 32  # 64 launch slots of (top + 32 shard) counters, 128 B apart
@@ -102,6 +104,20 @@ def _selffold(dev) -> bool:
 _SYNC = None
 
 
+def _check_sync_fold_mode():
+    """SyncBN sums the BN reductions over the ranks inside the fold (``_fold`` / ``SyncBN.fold``)
+    and ``_bn`` then divides by count * world. Without fold launches (KATIB_HIP_FOLD=0) or with
+    self-folding producers (KATIB_HIP_SELFFOLD=1) that fold never runs, and every rank would
+    normalise its LOCAL sums by the global count - mean and variance off by a factor of world,
+    silently. Refuse those combinations."""
+    if not FOLD:
+        raise RuntimeError("SyncBN needs the fold launches (KATIB_HIP_FOLD=1): the cross-rank BN sum "
+                           "happens inside them")
+    if SELFFOLD:
+        raise RuntimeError("SyncBN is incompatible with self-folding producers (KATIB_HIP_SELFFOLD=1): "
+                           "their replicas would never be summed over the ranks")
+
+
 class SyncBN:
     """Global-batch BatchNorm for the DARTS supernet under data parallelism (reference BN over
     the whole 128-image batch, ``operations.py:62,96,117,139``). Construction is collective.
@@ -112,6 +128,7 @@ class SyncBN:
     the fold is followed by one ``Comm.allreduce_sum_`` per synchronised segment (RCCL / gloo)."""
 
     def __init__(self, comm):
+        _check_sync_fold_mode()
         self.comm, self.world = comm, comm.world_size
         self.ws = None
         if comm.xgmi is not None:
@@ -143,6 +160,8 @@ class sync_scope:
 
     def __enter__(self):
         global _SYNC
+        if self.sync is not None:
+            _check_sync_fold_mode()
         self.prev, _SYNC = _SYNC, self.sync
         return self
 

@@ -119,3 +119,54 @@ def test_api_token_enforced(tmp_path):
     finally:
         api.stop()
         m.shutdown()
+
+
+def test_grpc_stays_loopback_and_empty_address_is_exposed(tmp_path, capsys):
+    """the bearer token protects only the HTTP API, so a non-loopback install keeps the
+    gRPC services on loopback, ``serve --grpc`` / the standalone gRPC servers refuse a
+    non-loopback bind without --insecure-grpc, and ``--address ''`` (every interface) counts as
+    exposed."""
+    files = render("services", str(tmp_path), python="/usr/bin/python3", listen="0.0.0.0")
+    binds = _binds({k: v for k, v in files.items() if k != "katib-amd.service"})
+    assert binds and all(b.startswith("127.0.0.1") or b.startswith("unix:") for b in binds), binds
+    rc = cli.main(["serve", "--address", "", "--port", "0", "--state-dir", str(tmp_path)])
+    assert rc == 2 and "refusing to listen" in capsys.readouterr().err
+    tok = tmp_path / "tok"
+    tok.write_text("abc\n")
+    rc = cli.main(["serve", "--address", "127.0.0.1", "--port", "0", "--state-dir", str(tmp_path),
+                   "--token-file", str(tok), "--grpc", "0.0.0.0:0"])
+    assert rc == 2 and "unauthenticated" in capsys.readouterr().err
+    for argv in (["db-manager", "--address", "0.0.0.0:0"], ["suggestion-server", "--algorithm", "random",
+                                                            "--address", "10.1.2.3:0"],
+                 ["earlystopping-server", "--address", "[::]:0"]):
+        assert cli.main(argv) == 2, argv
+        assert "unauthenticated" in capsys.readouterr().err
+
+
+def test_ui_token_cookie(tmp_path):
+    """The browser UI cannot send a bearer header: ``/?token=<token>`` sets an HttpOnly cookie that
+    authorises the later UI requests; a wrong token gets 401."""
+    import urllib.error
+    import urllib.request
+
+    from katib_amd.controller.apiserver import ApiServer
+    from katib_amd.controller.manager import Manager
+
+    m = Manager(state_dir=str(tmp_path), num_devices=0, journal=False)
+    api = ApiServer(m, "127.0.0.1", 0, token="s3cret").start()
+    try:
+        base = "http://127.0.0.1:%d" % api.port
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(base + "/katib/fetch_experiments?namespace=default")
+        assert ei.value.code == 401
+        with pytest.raises(urllib.error.HTTPError):
+            urllib.request.urlopen(base + "/?token=wrong")
+        r = urllib.request.urlopen(base + "/?token=s3cret")
+        cookie = r.headers["Set-Cookie"]
+        assert cookie.startswith("katib_amd_token=s3cret") and "HttpOnly" in cookie
+        req = urllib.request.Request(base + "/katib/fetch_experiments?namespace=default",
+                                     headers={"Cookie": cookie.split(";")[0]})
+        assert urllib.request.urlopen(req).status == 200
+    finally:
+        api.stop()
+        m.shutdown()

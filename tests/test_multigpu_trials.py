@@ -216,3 +216,76 @@ def test_single_process_multi_gpu_needs_distinct_devices(tmp_path):
         assert t.status.conditions[-1].reason.endswith("Unschedulable"), t.status.conditions[-1]
     finally:
         m.shutdown()
+
+
+def test_multi_replica_multi_gpu_job_is_scheduled(tmp_path):
+    """a PyTorchJob with Master (2 GPUs) + Worker (2 GPUs) on a 2-device node with two
+    slots per device fits (4 slots) and its replicas share the trial's devices, so it must launch
+    instead of pending forever on an all-distinct request for 4 devices."""
+    import sys
+
+    from katib_amd.api.models import V1beta1Experiment
+    from katib_amd.controller.manager import Manager
+
+    def rep(name):
+        return {"replicas": 1, "template": {"spec": {"containers": [
+            {"name": "pytorch", "command": [sys.executable, "-c", "print('loss=0.5')", "${trialParameters.x}"],
+             "resources": {"limits": {"amd.com/gpu": 2}}}]}}}
+
+    spec = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+            "spec": {"pytorchReplicaSpecs": {"Master": rep("m"), "Worker": rep("w")}}}
+    plan = make_plan(spec, "pytorch")
+    assert plan.share_devices and plan.total_gpus == 4
+    exp = {"apiVersion": "kubeflow.org/v1beta1", "kind": "Experiment",
+           "metadata": {"name": "ptj-4gpu", "namespace": "default"},
+           "spec": {"objective": {"type": "minimize", "objectiveMetricName": "loss"},
+                    "algorithm": {"algorithmName": "random"}, "parallelTrialCount": 1, "maxTrialCount": 1,
+                    "maxFailedTrialCount": 1,
+                    "parameters": [{"name": "x", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                    "trialTemplate": {"primaryContainerName": "pytorch",
+                                      "trialParameters": [{"name": "x", "reference": "x"}],
+                                      "trialSpec": spec}}}
+    m = Manager(state_dir=str(tmp_path / "state"), num_devices=2, journal=False)
+    m.config.amd.slots_per_device = 2
+    m.slots = m.N.SlotPool(2, 2)
+    m.config.amd.warm_workers = False
+    try:
+        m.create_experiment(V1beta1Experiment.from_k8s(exp))
+        done = m.run_until_complete("ptj-4gpu", timeout=60)
+        t = m.list_trials("ptj-4gpu")[0]
+        assert EC.is_succeeded(done), t.status.conditions[-1]
+        assert t.status.conditions[-1].type == "Succeeded", t.status.conditions[-1]
+    finally:
+        m.shutdown()
+
+
+def test_distinct_request_beyond_healthy_devices_is_unschedulable(tmp_path):
+    """A single process asking for more distinct GPUs than the node has healthy (quarantined
+    devices excluded) fails Unschedulable instead of pending forever."""
+    import sys
+
+    from katib_amd.api.models import V1beta1Experiment
+    from katib_amd.controller.manager import Manager
+
+    c = {"name": "c", "command": [sys.executable, "-c", "print('loss=1')", "${trialParameters.x}"],
+         "resources": {"limits": {"amd.com/gpu": 2}}, "env": [{"name": "KATIB_AMD_LAUNCH", "value": "single"}]}
+    exp = {"apiVersion": "kubeflow.org/v1beta1", "kind": "Experiment",
+           "metadata": {"name": "single-2gpu-q", "namespace": "default"},
+           "spec": {"objective": {"type": "minimize", "objectiveMetricName": "loss"},
+                    "algorithm": {"algorithmName": "random"}, "parallelTrialCount": 1, "maxTrialCount": 1,
+                    "maxFailedTrialCount": 1,
+                    "parameters": [{"name": "x", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                    "trialTemplate": {"primaryContainerName": "c", "trialParameters": [{"name": "x", "reference": "x"}],
+                                      "trialSpec": {"apiVersion": "batch/v1", "kind": "Job", "spec": {"template": {
+                                          "spec": {"containers": [c]}}}}}}}
+    m = Manager(state_dir=str(tmp_path / "state"), num_devices=2, journal=False)
+    m.config.amd.slots_per_device = 2
+    m.slots = m.N.SlotPool(2, 2)
+    m.slots.quarantine(1)
+    try:
+        m.create_experiment(V1beta1Experiment.from_k8s(exp))
+        m.run_until_complete("single-2gpu-q", timeout=30)
+        t = m.list_trials("single-2gpu-q")[0]
+        assert t.status.conditions[-1].reason.endswith("Unschedulable"), t.status.conditions[-1]
+    finally:
+        m.shutdown()

@@ -102,3 +102,37 @@ def test_darts_dp_syncbn_matches_single_process():
     assert res["geno_equal"], res
     per_rank = _run_syncbn(False)
     assert per_rank["dA"] > 10 * max(res["dA"], 1e-12), (per_rank, res)
+
+
+def test_syncbn_rejects_fold_modes_without_cross_rank_sum(monkeypatch):
+    """under SyncBN ``_bn`` divides by count * world, which is only right when the fold
+    launch summed the BN reductions over the ranks. FOLD=0 and self-folding producers skip that
+    fold, so SyncBN and sync_scope refuse them instead of normalising with local sums / world."""
+    import pytest
+
+    from katib_amd.ops import hip_darts as h
+
+    class FakeComm:
+        world_size, xgmi = 2, None
+
+        def allreduce_sum_(self, t):
+            pass
+
+    sync = h.SyncBN(FakeComm())  # default modes: accepted
+    monkeypatch.setattr(h, "FOLD", False)
+    with pytest.raises(RuntimeError, match="KATIB_HIP_FOLD"):
+        h.SyncBN(FakeComm())
+    with pytest.raises(RuntimeError, match="KATIB_HIP_FOLD"):
+        with h.sync_scope(sync):
+            pass
+    monkeypatch.setattr(h, "FOLD", True)
+    monkeypatch.setattr(h, "SELFFOLD", True)
+    with pytest.raises(RuntimeError, match="SELFFOLD"):
+        with h.sync_scope(sync):
+            pass
+    monkeypatch.setattr(h, "SELFFOLD", False)
+    with h.sync_scope(sync):
+        with pytest.raises(RuntimeError, match="SyncBN"):
+            h.set_selffold(True)
+    with h.sync_scope(None):  # per-rank BN: any fold mode
+        pass
