@@ -297,6 +297,13 @@ def main():
                        "allreduce": allreduce, "sync_bn": sync_bn,
                        "second_order": True},
             "allreduce": allreduce,
+            # one-shot xGMI all-reduce self-test verdict (None at one rank), the SyncBN fold path
+            # (xgmi-oneshot / rccl-graph / host), and the cross-rank rendezvous one step issues
+            # (gradient buckets + SyncBN folds) and whether they sit inside the captured graph
+            "xgmi_self_test": comm.xgmi_status if comm.distributed else None,
+            "syncbn_path": search._hsync.path if getattr(search, "_hsync", None) is not None else None,
+            "rendezvous_per_step": search.rendezvous_per_step if comm.distributed else 0,
+            "rendezvous_in_graph": search.rendezvous_in_graph if comm.distributed else None,
             "batchnorm": ("global batch (sync-bn)" if sync_bn else
                           ("per rank" if comm.distributed else "global batch")),
             "per_rank_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,

@@ -116,6 +116,8 @@ class DartsSearch:
                 self._hsync = self.hd.SyncBN(self.comm)  # collective
                 if not self._hsync.capturable:
                     self.capture = False  # its collectives sit inside the passes
+            elif self.capture and not self.comm.graph_capturable([]):  # collective (RCCL capture probe)
+                self.capture = False  # torch-op SyncBN all-reduces inside the passes, on the host
         R = self.hd.REP if self.hd is not None else 1
         self.gW_rep = torch.zeros(R, nW, device=dev)
         self.gWv_rep = torch.zeros(R, nW, device=dev)
@@ -160,7 +162,10 @@ class DartsSearch:
         self._hsync_side = None
         if self.hess_concurrent and self.sync_bn:
             if self._hsync is not None and self._hsync.capturable:
-                self._hsync_side = self.hd.SyncBN(self.comm)  # collective, same order on every rank
+                # collective, same order on every rank; on the RCCL path the side branch gets a
+                # communicator of its own (two concurrently running branches must not share one)
+                side = self.comm if self._hsync.ws is not None else self.comm.subgroup()
+                self._hsync_side = self.hd.SyncBN(side)
             self.hess_concurrent = self._hsync_side is not None and self._hsync_side.capturable
         if self.hess_concurrent:
             self.Wp = torch.empty_like(self.W)
@@ -179,6 +184,8 @@ class DartsSearch:
                        if self.K is not None else None)
         self._one = None
         self.graphs = None
+        self.rendezvous_per_step = None  # cross-rank rendezvous per step (set by the first step)
+        self.rendezvous_in_graph = None
         self.static = None
         self._eval_graphs = {}  # (x shape, y shape, dtypes) -> (graph, static x, static y, [loss, top1, top5])
 
@@ -376,6 +383,19 @@ class DartsSearch:
                 for t in colls:
                     self.comm.allreduce_mean_(t)
 
+    def _rendezvous(self) -> int:
+        """Cross-rank rendezvous issued so far: gradient all-reduces and SyncBN folds, on every
+        communicator / one-shot workspace of this search."""
+        n = self.comm.calls
+        for sy in (self._hsync, self._hsync_side):
+            if sy is None:
+                continue
+            if sy.ws is not None:
+                n += sy.folds  # one-shot fold + cross-rank sum: not a Comm call
+            elif sy.comm is not self.comm:
+                n += sy.comm.calls
+        return n
+
     def _build_graphs(self):
         segs = self._segments()
         # merge segments with no host-side collective in between: all of them at world size 1
@@ -402,6 +422,7 @@ class DartsSearch:
                 self._restore_state()
         torch.cuda.current_stream().wait_stream(s)
         graphs = []
+        n0 = self._rendezvous()
         for fns, colls in groups:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g), self._scope():
@@ -409,6 +430,10 @@ class DartsSearch:
                     fn()
             graphs.append((g, colls))
         self.graphs = graphs
+        # inside the graphs (captured once, replayed every step) + the host-side ones per replay
+        self.rendezvous_per_step = self._rendezvous() - n0 + (
+            sum(len(c) for _, c in graphs) if self.comm.distributed else 0)
+        self.rendezvous_in_graph = not any(c for _, c in graphs)
 
     def _state_tensors(self):
         return [self.W, self.A, self.mom, self.adam_m, self.adam_v, self.adam_t, self.bn.mean, self.bn.var,
@@ -454,7 +479,10 @@ class DartsSearch:
                 for t in colls:
                     self.comm.allreduce_mean_(t)
         else:
+            n0 = self._rendezvous()
             self._run_eager()
+            self.rendezvous_per_step = self._rendezvous() - n0
+            self.rendezvous_in_graph = False
         return self.loss_out
 
     # ------------------------------------------------------------------ eval / genotype

@@ -125,7 +125,9 @@ class SyncBN:
     With the one-shot xGMI path available the fold of every BN reduction becomes ONE launch that
     also sums the folded values over the ranks (``XgmiWorkspace.fold_sync``, graph-capturable, its
     own small workspace so its epochs never interleave with the gradient all-reduces'); otherwise
-    the fold is followed by one ``Comm.allreduce_sum_`` per synchronised segment (RCCL / gloo)."""
+    the fold is followed by ONE grouped RCCL all-reduce of the synchronised segments
+    (``Comm.allreduce_sum_many_``), which stays inside the captured step when the communicator
+    passed ``Comm.probe_rccl_capture`` (else: host-side RCCL / gloo, step not captured)."""
 
     def __init__(self, comm):
         _check_sync_fold_mode()
@@ -136,20 +138,26 @@ class SyncBN:
 
             ar = xgmi.create(comm, capacity=1 << 16, blocks=16)
             self.ws = ar.ws if ar is not None else None
+        # RCCL inside the graph when the one-shot path is off or failed its self-test (collective)
+        self.rccl_graph = self.ws is None and comm.probe_rccl_capture()
+        self.folds = 0  # cross-rank rendezvous issued (one per fold call)
 
     @property
     def capturable(self) -> bool:
-        return self.ws is not None
+        return self.ws is not None or self.rccl_graph
+
+    @property
+    def path(self) -> str:
+        return "xgmi-oneshot" if self.ws is not None else ("rccl-graph" if self.rccl_graph else "host")
 
     def fold(self, segs):
         """segs: (f64 replicas, n, rstride[, sync]); sync defaults to True (d alpha segments pass False)."""
+        self.folds += 1
         if self.ws is not None:
             self.ws.fold_sync(list(segs))
             return
         _K.fold_f64([tuple(sg[:3]) for sg in segs])
-        for sg in segs:
-            if len(sg) < 4 or sg[3]:
-                self.comm.allreduce_sum_(sg[0][:sg[1]])
+        self.comm.allreduce_sum_many_([sg[0][:sg[1]] for sg in segs if len(sg) < 4 or sg[3]])
 
 
 class sync_scope:

@@ -19,11 +19,15 @@ import torch.distributed as dist
 
 class Comm:
     def __init__(self, rank: int = 0, world_size: int = 1, local_rank: int = 0, backend: Optional[str] = None,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, group=None):
         self.rank, self.world_size, self.local_rank = rank, world_size, local_rank
         self.backend = backend
         self.device = device or torch.device("cpu")
+        self.group = group  # None: the default process group
         self.xgmi = None  # one-shot xGMI all-reduce (parallel/xgmi.py), see enable_xgmi()
+        self._rccl_capture = None  # verdict of probe_rccl_capture() (collective, run once)
+        self.calls = 0  # collectives issued (eager calls + captured ones at capture time)
+        self.xgmi_status = None  # one-shot xGMI self-test verdict (enable_xgmi)
 
     @staticmethod
     def from_env(device_type: Optional[str] = None, backend: Optional[str] = None) -> "Comm":
@@ -80,14 +84,95 @@ class Comm:
             from . import xgmi
 
             self.xgmi = xgmi.create(self)
+            if self.xgmi is not None:
+                self.xgmi_status = "passed"
+            elif os.environ.get("KATIB_AMD_XGMI", "1") == "0":
+                self.xgmi_status = "disabled"
+            elif int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world_size))) != self.world_size \
+                    or self.world_size > 8:
+                self.xgmi_status = "not applicable (ranks span nodes or > 8)"
+            else:
+                self.xgmi_status = "failed"  # mapping or self-test failed on some rank: RCCL fallback
         return self.xgmi is not None
 
+    def subgroup(self) -> "Comm":
+        """Collective: the same ranks on a communicator of their own (a new process group of this
+        backend). Two graph branches that run concurrently must not share a communicator: RCCL
+        serialises a communicator's kernels, and two branches interleaving their collectives
+        differently on different ranks deadlock."""
+        if self.world_size <= 1:
+            return Comm(self.rank, 1, self.local_rank, self.backend, self.device)
+        g = dist.new_group(backend=self.backend)
+        c = Comm(self.rank, self.world_size, self.local_rank, self.backend, self.device, group=g)
+        t = torch.zeros(1, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, group=g)  # set the communicator up now, never inside a graph capture
+        return c
+
+    def probe_rccl_capture(self) -> bool:
+        """Collective (every rank must call it at the same point): can RCCL all-reduces on this
+        communicator be captured inside a HIP graph (``torch.cuda.graph``) and replayed?
+
+        Capturing records the collective without running it, so the ranks agree on "captured"
+        before any replay (a rank whose capture raised would otherwise leave its peers waiting in
+        a replayed all-reduce), then replay twice, check the sums and agree again. Off with
+        ``KATIB_AMD_RCCL_CAPTURE=0``; only the ``nccl`` backend (RCCL) qualifies - gloo runs on
+        the host."""
+        if self._rccl_capture is not None:
+            return self._rccl_capture
+        ok = (self.world_size > 1 or dist.is_initialized()) and self.backend == "nccl" and \
+            self.device.type == "cuda" and os.environ.get("KATIB_AMD_RCCL_CAPTURE", "1") != "0"
+        if not ok or self.backend != "nccl":
+            self._rccl_capture = False
+            return False
+        g = None
+        x = torch.zeros(64, device=self.device, dtype=torch.float64)
+        try:
+            dist.all_reduce(x, group=self.group)  # communicator set up outside the capture
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                dist.all_reduce(x, group=self.group)
+        except Exception:  # noqa: BLE001 - any failure keeps the collectives on the host
+            ok, g = False, None
+        ok = self._agree(ok)
+        if ok:
+            try:
+                for _ in range(2):
+                    x.fill_(float(self.rank + 1))
+                    g.replay()
+                torch.cuda.synchronize(self.device)
+                ok = bool((x == self.world_size * (self.world_size + 1) / 2.0).all())
+            except Exception:  # noqa: BLE001
+                ok = False
+            ok = self._agree(ok)
+        self._rccl_capture = ok
+        return ok
+
+    def _agree(self, ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(t.item()))
+
+    @property
+    def rccl_capturable(self) -> bool:
+        """The verdict of :meth:`probe_rccl_capture` (False until it ran)."""
+        return bool(self._rccl_capture)
+
     def graph_capturable(self, tensors) -> bool:
-        """True when all-reducing ``tensors`` can be captured inside a HIP graph."""
-        return self.world_size == 1 or (self.xgmi is not None and all(self.xgmi.fits(t) for t in tensors))
+        """True when all-reducing ``tensors`` can be captured inside a HIP graph: world size 1, the
+        one-shot xGMI kernel (every tensor fits its workspace), or RCCL collectives that passed
+        :meth:`probe_rccl_capture`. Collective when the probe has not run yet."""
+        if self.world_size == 1:
+            return True
+        if self.xgmi is not None and all(self.xgmi.fits(t) for t in tensors):
+            return True
+        return self.probe_rccl_capture()
 
     def _coll(self, fn, t: torch.Tensor, *a, **kw) -> torch.Tensor:
         """Run a torch.distributed collective; gloo gets a host copy of device tensors."""
+        self.calls += 1
+        if self.group is not None:
+            kw["group"] = self.group
         if self.backend == "gloo" and t.is_cuda:
             h = t.cpu()
             fn(h, *a, **kw)
@@ -99,9 +184,10 @@ class Comm:
     def allreduce_mean_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world_size > 1:
             if self.xgmi is not None and self.xgmi.fits(t):
+                self.calls += 1
                 self.xgmi.allreduce_(t, average=True)
             elif self.backend == "nccl":
-                dist.all_reduce(t, op=dist.ReduceOp.AVG)
+                self._coll(dist.all_reduce, t, op=dist.ReduceOp.AVG)
             else:
                 self._coll(dist.all_reduce, t)
                 t.div_(self.world_size)
@@ -110,10 +196,29 @@ class Comm:
     def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world_size > 1:
             if self.xgmi is not None and self.xgmi.fits(t):
+                self.calls += 1
                 self.xgmi.allreduce_(t)
             else:
                 self._coll(dist.all_reduce, t)
         return t
+
+    def allreduce_sum_many_(self, ts) -> None:
+        """Sum each tensor of ``ts`` over the ranks, in place. On RCCL the all-reduces are one
+        grouped call (``ncclGroupStart/End``: one kernel for all of them, capturable like a
+        single all-reduce) - the per-fold BN segments of SyncBN are a few hundred bytes each."""
+        ts = list(ts)
+        if self.world_size <= 1 or not ts:
+            return
+        if self.backend == "nccl" and len(ts) > 1:
+            from torch.distributed.distributed_c10d import _coalescing_manager
+
+            self.calls += 1
+            with _coalescing_manager(group=self.group, device=self.device):
+                for t in ts:
+                    dist.all_reduce(t, group=self.group)
+            return
+        for t in ts:
+            self.allreduce_sum_(t)
 
     def allreduce_max(self, x: float) -> float:
         if self.world_size <= 1:
@@ -130,9 +235,9 @@ class Comm:
     def barrier(self):
         if self.world_size > 1:
             if self.backend == "nccl":
-                dist.barrier(device_ids=[self.device.index])
+                dist.barrier(group=self.group, device_ids=[self.device.index])
             else:
-                dist.barrier()
+                dist.barrier(group=self.group)
 
     def destroy(self):
         if self.world_size > 1 and dist.is_initialized():

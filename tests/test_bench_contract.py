@@ -86,3 +86,18 @@ def test_bench_refuses_world_size_mismatch():
 def test_bench_per_rank_bn_label():
     r = _run(2, "--sync-bn", "0")
     assert r["batchnorm"] == "per rank" and r["config"]["sync_bn"] is False
+
+
+def test_bench_eight_ranks_syncbn_rehearsal():
+    """the driver's N=8 case, rehearsed on the CPU - plain `python bench.py
+    --gpus 8` (self-launched, gloo), strong scaling at per-rank batch 16 with SyncBN, one JSON
+    line carrying the rendezvous keys. On MI355X the same code runs over RCCL / the one-shot
+    xGMI kernel; here every rendezvous is a host-side gloo call (not in a graph)."""
+    r = _run(8, torchrun=False)
+    assert r["n_gpus"] == 8 and r["ranks_seen"] == 8 and r["config"]["parallelism"] == "dp8"
+    assert r["config"]["per_gpu_batch"] == 16 and r["config"]["global_batch"] == 128
+    assert r["batchnorm"] == "global batch (sync-bn)" and r["allreduce"] == "gloo"
+    assert r["xgmi_self_test"] is None or r["xgmi_self_test"] != "passed"  # CPU: no one-shot path
+    # 4 gradient buckets per step + the torch-op SyncBN all-reduces of every BN layer's statistics
+    assert r["rendezvous_per_step"] > 4 and r["rendezvous_in_graph"] is False
+    assert r["final_loss"] == r["final_loss"]

@@ -118,6 +118,9 @@ def test_syncbn_rejects_fold_modes_without_cross_rank_sum(monkeypatch):
         def allreduce_sum_(self, t):
             pass
 
+        def probe_rccl_capture(self):
+            return False
+
     sync = h.SyncBN(FakeComm())  # default modes: accepted
     monkeypatch.setattr(h, "FOLD", False)
     with pytest.raises(RuntimeError, match="KATIB_HIP_FOLD"):
