@@ -99,6 +99,7 @@ def run_file(args):
     from katib_amd.controller.config import detect_gpus
     from katib_amd.controller.manager import Manager
 
+    os.environ.setdefault("KATIB_AMD_TRIAL_PHASES", "1")  # trials print their phase marks (trial_phases)
     e = load_experiment(args.experiment)
     n_gpus = args.gpus or detect_gpus()
     par = e.spec.parallel_trial_count or 3
@@ -124,6 +125,7 @@ def run_file(args):
             if mt.name == e.spec.objective.objective_metric_name:
                 best_acc = float(mt.max)
     per_trial = []
+    phases = trial_phases(m, e.metadata.name)
     for t in m.list_trials(e.metadata.name):
         a, b = t.status.start_time, t.status.completion_time
         if a and b:
@@ -140,9 +142,49 @@ def run_file(args):
         "wall_s": round(wall, 2), "trials_completed": completed, "trials_succeeded": st.trials_succeeded,
         "succeeded": EC.is_succeeded(done), "best_objective": best_acc,
         "median_trial_s": sorted(per_trial)[len(per_trial) // 2] if per_trial else None,
+        "median_trial_wall_s": phases.get("total"),
+        "trial_phases_s": phases.get("phases"),
+        "launcher": phases.get("launcher"),
         "config": {"experiment": e.metadata.name, "algorithm": e.spec.algorithm.algorithm_name,
                    "parallel": par, "max_trials": e.spec.max_trial_count, "slots_per_gpu": slots,
                    "trial_kind": e.spec.trial_template.trial_spec.get("kind")}}))
+
+
+PHASES = ["process", "module", "torch", "hip_init", "data", "model", "captured", "first_metric", "trained"]
+
+
+def trial_phases(m, exp_name):
+    """Median cold-trial phase durations (s): launch (scheduler) -> process created -> module
+    import starts -> torch imported -> HIP up -> data on device -> model built -> graph captured ->
+    first epoch metric -> training done -> reaped (scheduler saw the exit). Trials print
+    ``katib-phase`` lines when KATIB_AMD_TRIAL_PHASES=1 (workloads/common.py ``phase``)."""
+    import statistics
+
+    rows = []
+    launchers = set()
+    for (ns, name), run in list(m.runs.items()):
+        if not run.trial_dir or not run.started or not run.finished:
+            continue
+        launchers.add(getattr(run, "launcher", "exec"))
+        marks = {}
+        try:
+            with open(os.path.join(run.trial_dir, "metrics.log")) as f:
+                for ln in f:
+                    if ln.startswith("katib-phase "):
+                        _, k, v = ln.split()
+                        marks[k] = float(v)
+        except OSError:
+            continue
+        if not all(k in marks for k in PHASES):
+            continue
+        seq = [("launch", run.started)] + [(k, marks[k]) for k in PHASES] + [("reaped", run.finished)]
+        rows.append({b[0]: b[1] - a[1] for a, b in zip(seq, seq[1:])} | {"total": run.finished - run.started})
+    if not rows:
+        return {}
+    keys = [k for k, _ in zip(PHASES + ["reaped"], range(99))]
+    return {"n": len(rows), "total": round(statistics.median(r["total"] for r in rows), 3),
+            "launcher": ",".join(sorted(launchers)),
+            "phases": {k: round(statistics.median(r[k] for r in rows), 3) for k in keys}}
 
 
 if __name__ == "__main__":

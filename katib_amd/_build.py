@@ -176,6 +176,18 @@ def build_hip_zbf16(force: bool = False, verbose: bool = False) -> str:
                      build_dir=os.path.join(PKG_DIR, "csrc", "hip", "build_zbf16"))
 
 
+def stamps_target() -> str:
+    return os.path.join(PKG_DIR, "_hipkern_stamps" + EXT_SUFFIX)
+
+
+def build_hip_stamps(force: bool = False, verbose: bool = False) -> str:
+    """Diagnostic variant (``-DKATIB_HIP_STAMPS``): the DARTS plane / pool kernels record per-workgroup
+    phase timestamps of one armed launch (``stamps_arm``; ``scripts/darts_phase_stamps.py``). Never
+    loaded by default; ``KATIB_AMD_HIPKERN=<this path>`` selects it."""
+    return build_hip(force=force, verbose=verbose, defines=["KATIB_HIP_STAMPS"], out=stamps_target(),
+                     build_dir=os.path.join(PKG_DIR, "csrc", "hip", "build_stamps"))
+
+
 if __name__ == "__main__":
     print(build_native(verbose=True))
     print(build_hip(verbose=True))

@@ -813,6 +813,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_bwd_multi", &pool_bwd_multi, "stride-1 and stride-2 pool backward in one launch");
   m.def("edge_bwd", &edge_bwd, "whole input gradient of a node's edges (convs, pools, identity) in one launch");
   m.def("set_max_blocks", &set_max_blocks);
+  m.def("stamps_arm", [](int kind, int call, torch::Tensor buf) {
+    TORCH_CHECK(!buf.defined() || kind == 0 || (buf.is_cuda() && buf.scalar_type() == torch::kInt64 &&
+                                               buf.is_contiguous() && buf.numel() >= 65536 * 8),
+                "stamps_arm: int64 CUDA buffer of >= 65536 * 8 entries");
+    stamps_arm(kind, call, kind == 0 ? nullptr : reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>()));
+  }, "diagnostic build: phase-stamp the call-th launch of kind (StampKind) into buf[wg * 8 + phase]");
+  m.def("stamps_compiled", &stamps_compiled);
   m.def("fold_rows", &fold_rows);
   m.def("fold_f64", &fold_f64);
   m.def("set_fold_counters", &set_fold_counters, "register the current device's self-fold counter ring (int32, zeroed)");

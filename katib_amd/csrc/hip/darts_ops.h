@@ -249,5 +249,9 @@ int max_blocks();
 void launch_fold_rows(const FoldArgs& a, hipStream_t st);
 void launch_fold_f64(const FoldF64Args& a, hipStream_t st);
 void set_max_blocks(int n);
+// diagnostic build (-DKATIB_HIP_STAMPS): stamp every workgroup's phases of the `call`-th launch of
+// `kind` (StampKind, darts_ops_dev.h) into buf[wg * 8 + phase]; kind 0 disarms
+void stamps_arm(int kind, int call, unsigned long long* buf);
+bool stamps_compiled();
 
 }  // namespace katib_hip

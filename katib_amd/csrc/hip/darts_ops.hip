@@ -58,6 +58,28 @@ int vec_mask() {
   return m;
 }
 
+// phase-stamp arming (diagnostic build): the `call`-th launch of `kind` after stamps_arm()
+static int g_stamp_kind = 0, g_stamp_call = -1, g_stamp_seen = 0;
+static unsigned long long* g_stamp_buf = nullptr;
+void stamps_arm(int kind, int call, unsigned long long* buf) {
+  g_stamp_kind = kind;
+  g_stamp_call = call;
+  g_stamp_seen = 0;
+  g_stamp_buf = buf;
+}
+bool stamp_take(int kind) {
+  if (kind != g_stamp_kind || g_stamp_buf == nullptr) return false;
+  return g_stamp_seen++ == g_stamp_call;
+}
+unsigned long long* stamp_buffer() { return g_stamp_buf; }
+bool stamps_compiled() {
+#ifdef KATIB_HIP_STAMPS
+  return true;
+#else
+  return false;
+#endif
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // combine_fwd: out = sum_k w[k] * BN_k(z_k) + wid * x  (elementwise), running stats in block 0

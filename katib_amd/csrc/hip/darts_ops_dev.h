@@ -14,6 +14,62 @@
 namespace katib_hip {
 
 int max_blocks();
+
+// Diagnostic build only (-DKATIB_HIP_STAMPS, _build.build_hip_stamps): phase timestamps of every
+// workgroup of ONE armed launch (s_memrealtime, 100 MHz, device-wide clock), written by lane 0 of
+// the workgroup to stamps[wg * 8 + phase] (a vector store). The per-TU device pointer is set by
+// the host launcher right before the armed launch and cleared after it; the production build
+// compiles every KSTAMP to nothing.
+#ifdef KATIB_HIP_STAMPS
+static __device__ unsigned long long* g_stamps = nullptr;
+#define KSTAMP(k)                                                                          \
+  do {                                                                                     \
+    unsigned long long* _sp = g_stamps;                                                    \
+    if (_sp != nullptr && threadIdx.x == 0) {                                              \
+      const unsigned _wg = blockIdx.y * gridDim.x + blockIdx.x;                            \
+      if (_wg < 65536u) _sp[(size_t)_wg * 8 + (k)] = __builtin_amdgcn_s_memrealtime();     \
+    }                                                                                      \
+  } while (0)
+bool stamp_take(int kind);  // host: is this launch of `kind` the armed one (darts_ops.hip)
+unsigned long long* stamp_buffer();
+#define KSTAMP_ARM(kind, st)                                                               \
+  const bool _stamp_armed = stamp_take(kind);                                              \
+  if (_stamp_armed) {                                                                      \
+    static unsigned long long* _on;                                                        \
+    _on = stamp_buffer();                                                                  \
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_stamps), &_on, sizeof(_on), 0, hipMemcpyHostToDevice, st); \
+  }
+#define KSTAMP_DISARM(st)                                                                  \
+  if (_stamp_armed) {                                                                      \
+    static unsigned long long* _off = nullptr;                                             \
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_stamps), &_off, sizeof(_off), 0, hipMemcpyHostToDevice, st); \
+  }
+#else
+#define KSTAMP(k)
+#define KSTAMP_ARM(kind, st)
+#define KSTAMP_DISARM(st)
+#endif
+enum StampKind { kStampDwBwd = 1, kStampDwPw = 2, kStampPoolBwd = 3, kStampPoolFwd = 4, kStampCombineFwd = 5,
+                 kStampCombineBwd = 6, kStampPwBwd = 7 };
+// Compiler fence at the top of a per-channel loop body that reads LDS-resident weights: keeps
+// those reads inside the iteration. Without it hipcc hoists every weight of every channel out of
+// the pixel loop into registers (C * K^2 live values: 256 VGPRs + AGPRs, one wave per SIMD).
+#define KEEP_WEIGHT_READS_LOCAL() asm volatile("" ::: "memory")
+// Dynamic-LDS head of the plane kernels (floats, a multiple of 4): the group's depthwise weights
+// (up to 5x5 taps) and pointwise weights (dwpw) / depthwise weight-gradient sums (dw_bwd). In the
+// dynamic region, one allocation serves every variant body of a mixed-variant kernel; as static
+// __shared__ arrays each of the 10-32 inlined variants held its own copy, and the extra static
+// LDS cost a workgroup per CU.
+__host__ __device__ constexpr int plane_head_floats(int C) { return (C * 25 + C * C + 3) & ~3; }
+__host__ __device__ constexpr int dwb_head_floats(int C) { return (2 * C * 25 + 3) & ~3; }
+// Row pitch (floats) of the LDS planes the plane kernels stage (dwpw_plane, dw_bwd_plane): a
+// multiple of 4 floats, so the 4-pixel paths read every tap row as whole 16-byte ds_read_b128
+// quads from an aligned base (a lane's 4 outputs at stride 4 floats hit 8 of 32 banks as
+// 4-byte reads: 4-way conflicts), and an odd number of quads, so the lanes of one b128 lane
+// group that sit on consecutive rows start on different 16-byte bank slots.
+__host__ __device__ constexpr int lds_pitch(int w) {
+  return (((w + 3) & ~3) >> 2) & 1 ? ((w + 3) & ~3) : ((w + 3) & ~3) + 4;
+}
 // 4-pixels-per-thread output paths of the plane kernels (darts_ops.hip, KATIB_HIP_VEC_MASK)
 int vec_mask();
 

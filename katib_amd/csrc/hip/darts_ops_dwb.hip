@@ -169,6 +169,7 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
   unsigned char* sArg = (unsigned char*)(smem + 2 * HWo);     // [HWo] argmax tap
   // the plane's BN coefficients: four threads each sum one pair over the replicas
   __shared__ float sCo[8];
+  KSTAMP(0);
   if (threadIdx.x < 8) sCo[threadIdx.x] = (threadIdx.x & 1) ? 1.f : 0.f;
   __syncthreads();
   if (threadIdx.x == 0 && a.ga.z) bn_coeffs(a.ga.bn, c, sCo[0], sCo[1]);
@@ -177,6 +178,7 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
   if (a.ga.z) gs_means_coop(a.ga, c, 1, sCo + 2, sCo + 3);
   if (a.gm.z) gs_means_coop(a.gm, c, 1, sCo + 6, sCo + 7);
   __syncthreads();
+  KSTAMP(1);
   const float ma = sCo[0], ia = sCo[1], a1 = a.ga.z ? sCo[2] : 0.f, a2 = a.ga.z ? sCo[3] : 0.f;
   const float mm = sCo[4], im = sCo[5], m1 = a.gm.z ? sCo[6] : 0.f, m2 = a.gm.z ? sCo[7] : 0.f;
   const float wa = a.ga.w ? a.ga.w[a.ga.widx] : 0.f;
@@ -213,6 +215,7 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
       }
     }
     __syncthreads();
+    KSTAMP(2);
     const size_t pb = (size_t)nc * H * W;
     for (int q4 = threadIdx.x * 4; q4 < H * W; q4 += 1024) {
       f4 g = {0.f, 0.f, 0.f, 0.f};
@@ -238,6 +241,7 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
       f4* dst = reinterpret_cast<f4*>(a.gx + pb + q4);
       *dst = a.overwrite ? g : *dst + g;
     }
+    KSTAMP(3);
     return;
   }
   for (int o = threadIdx.x; o < HWo; o += 256) {
@@ -319,21 +323,32 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
   const int BRi = H / nb, iy0 = band * BRi, nrow = BRi;
   const int oyA = (iy0 - PAD) >> SH;                 // floor division (S in {1, 2})
   const int oyB = (iy0 + nrow - 1 + PAD) >> SH;
-  const int ODR = oyB - oyA + 1, ODW = Wo + 2 * PO, NP = nrow * W;
+  const int ODR = oyB - oyA + 1, ODW = lds_pitch(Wo + 2 * PO), NP = nrow * W;  // row pitch: lds_pitch
   const bool accum = !PREBN && !a.overwrite;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sDD = smem;                    // [C][ODR][ODW]
+  float* sWt = smem;                    // [C][KK] depthwise weights (dwb_head_floats)
+  float* sGW = smem + C * 25;           // [C][KK] block-local depthwise weight gradients
+  float* sDD = smem + dwb_head_floats(C);  // [C][ODR][ODW]
   float* sIn = sDD + C * ODR * ODW;     // [C][nrow][W] act(in)
   float* sOld = sIn + C * NP;           // [C][nrow][W] current gradient (accumulate mode)
-  __shared__ float sMean[C], sInv[C], sRed[2 * C], sGW[C * KK];
+  __shared__ float sMean[C], sInv[C], sRed[2 * C];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  KSTAMP(0);
+  // the group's depthwise weights in LDS, loaded with the prologue: read from global memory
+  // inside the tap loops, every weight was its own load + s_waitcnt vmcnt(0) (the compiler may
+  // not hoist them above the gradient stores, which could alias) - 9-25 serial round trips per
+  // channel in the middle of the compute phase
+  for (int i = tid; i < C * KK; i += 256) {
+    sGW[i] = 0.f;
+    sWt[i] = a.dw[c0 * KK + i];
+  }
   if (tid < C) {
     if (PREBN) bn_coeffs(a.inbn, c0 + tid, sMean[tid], sInv[tid]);
     sRed[tid] = 0.f;
     sRed[C + tid] = 0.f;
   }
-  for (int i = tid; i < C * KK; i += 256) sGW[i] = 0.f;
   __syncthreads();
+  KSTAMP(1);
   // staging with 16-byte loads (the band's rows are contiguous per channel; W, Wo % 4 == 0):
   // many wide loads in flight per wave, which the one-row-per-wave scalar loop lacked
   const float* ddn = a.dd + ((size_t)n * a.C + c0) * Ho * Wo;
@@ -392,6 +407,7 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
     }
   }
   __syncthreads();
+  KSTAMP(2);
   // input gradients of the band's own pixels
   float st1[C], st2[C];
 #pragma unroll
@@ -401,31 +417,44 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
     // stride 1: 4 consecutive input pixels of one row per thread (W % 4 == 0, as the staging
     // assumes): the taps' column offsets are shared, and the gradient leaves as one 16-byte store
     // per channel instead of four 4-byte ones
+    // The staged dd row the 4 pixels meet through every column tap is dd columns ix .. ix + 3 + 2 PAD
+    // (PO = PAD at stride 1): NQ aligned 16-byte quads from ix (ODW = lds_pitch, a multiple of 4),
+    // read as ds_read_b128 per tap row instead of 4 K ds_read_b32 at a 4-float lane stride (8 of
+    // 32 banks: 4-way conflicts)
     typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int NQ = (4 + 2 * PAD + 3) / 4;
     for (int p = 4 * tid; p < ((dbg & 1) ? 0 : NP); p += 1024) {
       const int r = p / W, ix = p - r * W, iy = iy0 + r;
-      int srow[K], scol[K];
+      int srow[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        srow[k] = (iy + PAD - k * DIL - oyA) * ODW;
-        scol[k] = ix + PAD - k * DIL + PO;
-      }
+      for (int k = 0; k < K; ++k) srow[k] = (iy + PAD - k * DIL - oyA) * ODW + ix;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
+        KEEP_WEIGHT_READS_LOCAL();
+        const float* wk = sWt + c * KK;  // LDS broadcast reads
         const float* dd = sDD + c * ODR * ODW;
         f4 ga = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ky = 0; ky < K; ++ky)
+        for (int ky = 0; ky < K; ++ky) {
+          float v[4 * NQ];  // v[m] = dd column ix + m
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const float4 t = *reinterpret_cast<const float4*>(dd + srow[ky] + 4 * q);
+            v[4 * q] = t.x;
+            v[4 * q + 1] = t.y;
+            v[4 * q + 2] = t.z;
+            v[4 * q + 3] = t.w;
+          }
 #pragma unroll
           for (int kx = 0; kx < K; ++kx) {
             const float w = wk[ky * K + kx];
-            const float* q = dd + srow[ky] + scol[kx];
-            ga.x += w * q[0];
-            ga.y += w * q[1];
-            ga.z += w * q[2];
-            ga.w += w * q[3];
+            const int o = 2 * PAD - kx * DIL;  // pixel ix + t meets dd column ix + t + o
+            ga.x += w * v[o];
+            ga.y += w * v[o + 1];
+            ga.z += w * v[o + 2];
+            ga.w += w * v[o + 3];
           }
+        }
         const int li = (c * nrow + r) * W + ix;
         const f4 act = *reinterpret_cast<const f4*>(sIn + li);
         const f4 g = {act.x > 0.f ? ga.x : 0.f, act.y > 0.f ? ga.y : 0.f, act.z > 0.f ? ga.z : 0.f,
@@ -461,7 +490,8 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
       }
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
+        KEEP_WEIGHT_READS_LOCAL();
+        const float* wk = sWt + c * KK;  // LDS broadcast reads
         const float* dd = sDD + c * ODR * ODW;
         float ga = 0.f;
 #pragma unroll
@@ -501,7 +531,8 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
+      KEEP_WEIGHT_READS_LOCAL();
+        const float* wk = sWt + c * KK;  // LDS broadcast reads
       const float* dd = sDD + c * ODR * ODW;
       float ga = 0.f;
 #pragma unroll
@@ -534,6 +565,7 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
     const float v = wave_reduce_scatter<2 * C>(st);
     if ((lane & (32 / C - 1)) == 0) atomicAdd(sRed + wave_scatter_index<2 * C>(lane), v);
   }
+  KSTAMP(3);
   // depthwise weight gradients over the band: thread per (channel, tap, pixel part)
   if (a.gW && !(dbg & 2) && S == 1) {
     // stride 1: job = (channel, ky, own row). A 4-pixel quad of the input row (one 16-byte LDS
@@ -549,9 +581,18 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
       for (int kx = 0; kx < K; ++kx) acc[kx] = 0.f;
       for (int ix = 0; ix < W; ix += 4) {
         const float4 v = *reinterpret_cast<const float4*>(inr + ix);
-        float dseg[4 + 2 * PAD];  // dseg[m] = dd[ix - PAD + m]
+        // dseg[m] = dd[ix - PAD + m]: dd column ix - PAD + PO + m = ix + m (PO = PAD at stride 1),
+        // whole aligned quads from ix (ds_read_b128; ODW = lds_pitch)
+        constexpr int NQ = (4 + 2 * PAD + 3) / 4;
+        float dseg[4 * NQ];
 #pragma unroll
-        for (int m = 0; m < 4 + 2 * PAD; ++m) dseg[m] = ddr[ix - PAD + m];
+        for (int q = 0; q < NQ; ++q) {
+          const float4 t = *reinterpret_cast<const float4*>(ddr - PO + ix + 4 * q);
+          dseg[4 * q] = t.x;
+          dseg[4 * q + 1] = t.y;
+          dseg[4 * q + 2] = t.z;
+          dseg[4 * q + 3] = t.w;
+        }
 #pragma unroll
         for (int kx = 0; kx < K; ++kx) {
           const int o = 2 * PAD - kx * DIL;  // in[ix + q] meets dd[ix + q + PAD - kx*DIL]
@@ -580,11 +621,13 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
       atomicAdd(sGW + job, acc);
     }
   }
+  KSTAMP(4);
   __syncthreads();
   if (PREBN && a.red && tid < 2 * C)  // red replica layout [sum g: a.C | sum g*y: a.C]
     atomicAdd(a.red + rep_slot() * 2 * a.C + (tid < C ? c0 + tid : a.C + c0 + tid - C), (double)sRed[tid]);
   if (a.gW)
     for (int i = tid; i < C * KK; i += 256) atomicAdd(a.gW + (size_t)rep_slot() * a.gstride + c0 * KK + i, sGW[i]);
+  KSTAMP(5);
 }
 
 template <int K, int DIL, int S, bool PREBN, int C>
@@ -922,8 +965,10 @@ void launch_pool_bwd_multi(const PoolBwdBatch& b, hipStream_t st) {
          al(a.gx, 16) && (!a.ga.z || !a.gm.z || a.ga.g == a.gm.g);
     for (int j = 0; j < a.nextra; ++j) v4 = v4 && al(a.extra[j], 16);
   }
+  KSTAMP_ARM(kStampPoolBwd, st)
   if (v4) hipLaunchKernelGGL(pool_bwd_multi_kernel<true>, dim3(maxblk, b.n), dim3(256), lds, st, b);
   else hipLaunchKernelGGL(pool_bwd_multi_kernel<false>, dim3(maxblk, b.n), dim3(256), lds, st, b);
+  KSTAMP_DISARM(st)
 }
 
 // LDS floats of one dw_bwd_plane band (nb bands per image)
@@ -931,7 +976,8 @@ static size_t dw_plane_floats(const DwBwdArgs& a, int K, int DIL, int S, int nb,
   const int PAD = (K - 1) / 2 * DIL, PO = (PAD + S - 1) / S, sh = S == 2 ? 1 : 0, BRi = a.H / nb;
   auto fdiv = [sh](int v) { return v >= 0 ? v >> sh : -((-v + (1 << sh) - 1) >> sh); };
   const int ODR = fdiv(BRi - 1 + PAD) - fdiv(-PAD) + 2;  // +1: odd bands start at odd rows
-  return (size_t)C * ODR * (a.Wo + 2 * PO) + (size_t)C * BRi * a.W * (accum ? 2 : 1);
+  return (size_t)dwb_head_floats(C) + (size_t)C * ODR * lds_pitch(a.Wo + 2 * PO) +
+         (size_t)C * BRi * a.W * (accum ? 2 : 1);
 }
 
 template <int K, int DIL, int S, int C>
@@ -1019,8 +1065,10 @@ bool launch_dw_bwd_multi(DwBwdBatch b, hipStream_t st) {
     maxblk = std::max(maxblk, a.nblk);
     lds = std::max(lds, sizeof(float) * dw_plane_floats(a, K, DIL, S, nb, false, C));
   }
+  KSTAMP_ARM(kStampDwBwd, st)
   if (C == 4) hipLaunchKernelGGL(dw_bwd_plane_multi_kernel<4>, dim3(maxblk, b.n), dim3(256), lds, st, b);
   else hipLaunchKernelGGL(dw_bwd_plane_multi_kernel<8>, dim3(maxblk, b.n), dim3(256), lds, st, b);
+  KSTAMP_DISARM(st)
   return true;
 }
 

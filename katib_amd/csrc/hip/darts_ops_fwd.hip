@@ -10,7 +10,7 @@ template <int K, int DIL, int S, int C>
 static void launch_dwpw_plane_t(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
   const DwPwFwdArgs& a = b.e[0];
   const int nb = a.chunk, BR = (a.Ho + nb - 1) / nb;
-  const size_t lds = sizeof(float) * C * ((BR - 1) * S + (K - 1) * DIL + 1) * (a.W + 2 * a.pad);
+  const size_t lds = sizeof(float) * (plane_head_floats(C) + C * ((BR - 1) * S + (K - 1) * DIL + 1) * lds_pitch(a.W + 2 * a.pad));
   dim3 grid(a.N * nb, b.n);
   // 16-byte staging when every row is whole float4s and every input is 16-byte aligned
   bool vec = a.W % 4 == 0;
@@ -59,7 +59,7 @@ static bool try_dwpw_split_g(const DwPwFwdBatch& b, bool prebn, hipStream_t st, 
   int nb = std::max(1, std::min(a.Ho / 4, 2048 / std::max(a.N * b.n * G, 1)));
   auto band_bytes = [&](int v) {
     const int BR = (a.Ho + v - 1) / v;
-    return (size_t)CG * ((BR - 1) * S + (K - 1) * DIL + 1) * (a.W + 2 * a.pad) * sizeof(float);
+    return ((size_t)plane_head_floats(CG) + (size_t)CG * ((BR - 1) * S + (K - 1) * DIL + 1) * lds_pitch(a.W + 2 * a.pad)) * sizeof(float);
   };
   while (band_bytes(nb) > 65536 && nb < a.Ho) ++nb;
   DwPwFwdBatch db = b;
@@ -137,7 +137,7 @@ static bool dwpw_multi_prep(DwPwMultiBatch& b, bool& fused, int& maxblk, size_t&
     int nb = std::max(1, std::min(a.Ho / 4, 2048 / std::max(N * b.n * G, 1)));
     auto band_bytes = [&](int v) {
       const int BR = (a.Ho + v - 1) / v;
-      return (size_t)CG * ((BR - 1) * S + (K - 1) * DIL + 1) * (a.W + 2 * a.pad) * sizeof(float);
+      return ((size_t)plane_head_floats(CG) + (size_t)CG * ((BR - 1) * S + (K - 1) * DIL + 1) * lds_pitch(a.W + 2 * a.pad)) * sizeof(float);
     };
     while (band_bytes(nb) > 65536 && nb < a.Ho) ++nb;
     a.chunk = nb;
@@ -160,6 +160,7 @@ bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st) {
   if (!dwpw_multi_prep(b, fused, maxblk, lds)) return false;
   const dim3 grid(maxblk, b.n);
   if (fused) {
+    // (phase stamps: armed in the launching translation unit, darts_ops_fwd_m{4,8,16}.hip)
     if (C == 4) launch_dwpw_plane_multi_t<4>(true, grid, lds, st, b);
     else if (C == 8) launch_dwpw_plane_multi_t<8>(true, grid, lds, st, b);
     else launch_dwpw_plane_multi_t<16>(true, grid, lds, st, b);

@@ -151,18 +151,28 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
   const int G = PW ? 1 : a.C / C, c0 = PW ? 0 : (bx % G) * C, nbx = PW ? bx : bx / G;
   const int n = nbx / nb, band = nbx - n * nb;
   const int oy0 = band * BR, oy1 = min(Ho, oy0 + BR);
-  const int HP = (BR - 1) * S + (K - 1) * DIL + 1, WP = W + 2 * pad, PL = HP * WP;
+  const int HP = (BR - 1) * S + (K - 1) * DIL + 1, WP = lds_pitch(W + 2 * pad), PL = HP * WP;
   const int iyb = oy0 * S - pad;  // input row of staged row 0
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sIn = smem;  // [C][HP][WP]
+  float* sWt = smem;                            // [C][KK] depthwise weights (plane_head_floats)
+  float* sPw = smem + C * 25;                   // [C][C] pointwise weights
+  float* sIn = smem + plane_head_floats(C);     // [C][HP][WP]
   __shared__ float sMean[C], sInv[C], sStat[2 * C];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  KSTAMP(0);
+  // depthwise and pointwise weights in LDS, loaded with the prologue: read from global memory in
+  // the compute loops, each weight was a separate load + s_waitcnt vmcnt(0) (not hoistable above
+  // the d / z stores, which could alias) - a serial chain of C (K^2 + C) round trips per thread
+  for (int i = tid; i < C * KK; i += 256) sWt[i] = a.dw[c0 * KK + i];
+  if (PW)
+    for (int i = tid; i < C * C; i += 256) sPw[i] = a.pw[i];
   if (PREBN) bn_coeffs_coop(a.inbn, c0, C, sMean, sInv);  // the input BN may arrive unfolded (rep > 1)
   if (tid < C) {
     sStat[tid] = 0.f;
     sStat[C + tid] = 0.f;
   }
   __syncthreads();
+  KSTAMP(1);
   const size_t xin = ((size_t)n * a.C + c0) * H * W;
   if (VEC) {
     // 16-byte loads over the band's contiguous in-range rows, scattered into the padded plane;
@@ -214,6 +224,7 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
     }
   }
   __syncthreads();
+  KSTAMP(2);
   float st1[C], st2[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) st1[c] = st2[c] = 0.f;
@@ -223,35 +234,51 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
   const bool vout = VEC && Wo % 4 == 0 && a.vout;
   if (vout) {
     // 4 consecutive output pixels (one row: Wo % 4 == 0) per thread: d and z leave as one 16-byte
-    // (bf16: 8-byte) store per channel instead of four 4-byte ones
+    // (bf16: 8-byte) store per channel instead of four 4-byte ones. Each tap row the 4 outputs
+    // reach (SPAN staged columns from ox0 * S, a multiple of 4) is read as NQ aligned 16-byte
+    // quads (WP = lds_pitch: a multiple of 4 floats, wide enough for the last quad): 2-4
+    // ds_read_b128 per row instead of 4 K ds_read_b32 whose lanes, 4 S floats apart, sat on 8 (S = 1)
+    // or 4 (S = 2) of the 32 banks
+    constexpr int SPAN = 3 * S + (K - 1) * DIL + 1, NQ = (SPAN + 3) / 4;
     for (int p = oy0 * Wo + 4 * tid; p < oy1 * Wo; p += 1024) {
       const int oy = p / Wo, ox0 = p - oy * Wo;
       zf4 d[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const float* src = sIn + c * PL + ((oy - oy0) * S) * WP + ox0 * S;
-        const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
+        const float* src = sIn + c * PL + ((oy - oy0) * S) * WP + ox0 * S;  // 16-byte aligned
+        KEEP_WEIGHT_READS_LOCAL();
+        const float* wk = sWt + c * KK;  // LDS broadcast reads
         zf4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ky = 0; ky < K; ++ky)
+        for (int ky = 0; ky < K; ++ky) {
+          float v[4 * NQ];
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const float4 t = *reinterpret_cast<const float4*>(src + ky * DIL * WP + 4 * q);
+            v[4 * q] = t.x;
+            v[4 * q + 1] = t.y;
+            v[4 * q + 2] = t.z;
+            v[4 * q + 3] = t.w;
+          }
 #pragma unroll
           for (int kx = 0; kx < K; ++kx) {
             const float w = wk[ky * K + kx];
-            const float* q = src + ky * DIL * WP + kx * DIL;
-            acc.x += w * q[0];
-            acc.y += w * q[S];
-            acc.z += w * q[2 * S];
-            acc.w += w * q[3 * S];
+            acc.x += w * v[kx * DIL];
+            acc.y += w * v[kx * DIL + S];
+            acc.z += w * v[kx * DIL + 2 * S];
+            acc.w += w * v[kx * DIL + 3 * S];
           }
+        }
         d[c] = acc;
         zst4(dn + (size_t)c * HWo + p, acc);
       }
       if (!PW) continue;
 #pragma unroll
       for (int co = 0; co < C; ++co) {
+        KEEP_WEIGHT_READS_LOCAL();
         zf4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ci = 0; ci < C; ++ci) z += a.pw[co * C + ci] * d[ci];
+        for (int ci = 0; ci < C; ++ci) z += sPw[co * C + ci] * d[ci];
         zst4(zn + (size_t)co * HWo + p, z);
         st1[co] += (z.x + z.y) + (z.z + z.w);
         st2[co] += (z.x * z.x + z.y * z.y) + (z.z * z.z + z.w * z.w);
@@ -264,7 +291,8 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const float* src = sIn + c * PL + ((oy - oy0) * S) * WP + ox * S;
-      const float* wk = a.dw + (c0 + c) * KK;  // uniform -> scalar loads
+      KEEP_WEIGHT_READS_LOCAL();
+        const float* wk = sWt + c * KK;  // LDS broadcast reads
       float acc = 0.f;
 #pragma unroll
       for (int ky = 0; ky < K; ++ky)
@@ -276,14 +304,16 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
     if (!PW) continue;
 #pragma unroll
     for (int co = 0; co < C; ++co) {
+      KEEP_WEIGHT_READS_LOCAL();
       float z = 0.f;
 #pragma unroll
-      for (int ci = 0; ci < C; ++ci) z += a.pw[co * C + ci] * d[ci];
+      for (int ci = 0; ci < C; ++ci) z += sPw[co * C + ci] * d[ci];
       zput(zn + (size_t)co * HWo + p, z);
       st1[co] += z;
       st2[co] += z * z;
     }
   }
+  KSTAMP(3);
   if (!PW || !a.stats) return;
   {
     float st[2 * C];  // [sum | sum of squares], reduce-scattered over the wave
@@ -294,6 +324,7 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
   }
   __syncthreads();
   if (tid < 2 * C) atomicAdd(a.stats + (bx % kRep) * 2 * C + tid, (double)sStat[tid]);
+  KSTAMP(4);
 }
 template <int K, int DIL, int S, bool PREBN, int C, bool VEC, bool PW = true>
 __global__ void __launch_bounds__(256) dwpw_plane_kernel(DwPwFwdBatch bt) {

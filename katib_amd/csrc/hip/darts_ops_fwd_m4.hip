@@ -7,7 +7,9 @@ namespace katib_hip {
 template <>
 void launch_dwpw_plane_multi_t<4>(bool pw, dim3 grid, size_t lds, hipStream_t st, const DwPwMultiBatch& b) {
   (void)pw;
+  KSTAMP_ARM(kStampDwPw, st)
   hipLaunchKernelGGL((dwpw_plane_multi_kernel<4, true>), grid, dim3(256), lds, st, b);
+  KSTAMP_DISARM(st)
 }
 
 template <>

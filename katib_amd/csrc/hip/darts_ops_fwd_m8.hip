@@ -10,7 +10,9 @@ void launch_dwpw_plane_multi_t<8>(bool pw, dim3 grid, size_t lds, hipStream_t st
     hipLaunchKernelGGL((dwpw_plane_multi_kernel<8, false>), grid, dim3(256), lds, st, b);
     return;
   }
+  KSTAMP_ARM(kStampDwPw, st)
   hipLaunchKernelGGL((dwpw_plane_multi_kernel<8, true>), grid, dim3(256), lds, st, b);
+  KSTAMP_DISARM(st)
 }
 
 template <>

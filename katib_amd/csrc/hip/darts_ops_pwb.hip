@@ -282,10 +282,15 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
     } else {
       const int oy = pp / Wo, ox = pp - oy * Wo, iy = oy * a.S + a.off, ix = ox * a.S + a.off;
       inb = iy < a.H && ix < a.W;
-      xi0 = (size_t)iy * a.W + ix;  // pixel inside the channel plane (plane_off below)
+      xi0 = inb ? (size_t)iy * a.W + ix : 0;  // pixel inside the channel plane (plane_off below)
+      // every channel loaded unconditionally (out-of-band pixels read pixel 0 and are masked):
+      // a load under `inb ?` made hipcc branch around each load and wait vmcnt(0) per channel,
+      // CI serial round trips per pixel
+      float raw[CI];
 #pragma unroll
-      for (int c = 0; c < CI; ++c)
-        av[c] = inb ? fmaxf(a.x[plane_off(n, c, a.N, CI, a.xnodes, (size_t)a.H * a.W) + xi0], 0.f) : 0.f;
+      for (int c = 0; c < CI; ++c) raw[c] = a.x[plane_off(n, c, a.N, CI, a.xnodes, (size_t)a.H * a.W) + xi0];
+#pragma unroll
+      for (int c = 0; c < CI; ++c) av[c] = inb ? fmaxf(raw[c], 0.f) : 0.f;
     }
     if (want_w) {
 #pragma unroll

@@ -191,6 +191,16 @@ PYBIND11_MODULE(_native, m) {
           py::arg("trial"), py::arg("argv"), py::arg("env"), py::arg("cwd"), py::arg("log_path"), py::arg("collector"),
           py::arg("deadline") = 0.0)
       .def(
+          "adopt",
+          [](TrialRuntime& r, const std::string& trial, int pid, int fd, const std::string& log_path,
+             const py::dict& cfg, double deadline) {
+            CollectorConfig c = make_cfg(cfg);
+            py::gil_scoped_release rel;
+            return r.adopt(trial, static_cast<pid_t>(pid), fd, log_path, c, deadline);
+          },
+          py::arg("trial"), py::arg("pid"), py::arg("fd"), py::arg("log_path"), py::arg("collector"),
+          py::arg("deadline") = 0.0)
+      .def(
           "spawn_worker",
           [](TrialRuntime& r, const std::vector<std::string>& argv, const std::vector<std::string>& env,
              const std::string& cwd, const std::string& log_path) {

@@ -273,6 +273,23 @@ pid_t TrialRuntime::spawn(const std::string& trial, const std::vector<std::strin
     }
     return -1;
   }
+  track(trial, pid, p[0], log_path, cfg, deadline_seconds);
+  return pid;
+}
+
+bool TrialRuntime::adopt(const std::string& trial, pid_t pid, int fd, const std::string& log_path,
+                         const CollectorConfig& cfg, double deadline_seconds) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (procs_.count(trial) || pid <= 0 || fd < 0) return false;
+  fcntl(fd, F_SETFD, fcntl(fd, F_GETFD) | FD_CLOEXEC);
+  track(trial, pid, fd, log_path, cfg, deadline_seconds);
+  return true;
+}
+
+// register a running trial process (mu_ held): its stdout pipe, collector and deadline
+void TrialRuntime::track(const std::string& trial, pid_t pid, int fd, const std::string& log_path,
+                         const CollectorConfig& cfg, double deadline_seconds) {
+  int p[1] = {fd};
   fcntl(p[0], F_SETFL, fcntl(p[0], F_GETFL) | O_NONBLOCK);
   auto proc = std::make_unique<Proc>();
   proc->trial = trial;
@@ -291,7 +308,6 @@ pid_t TrialRuntime::spawn(const std::string& trial, const std::vector<std::strin
   pid_trial_[pid] = trial;
   add_fd(p[0]);
   procs_[trial] = std::move(proc);
-  return pid;
 }
 
 int TrialRuntime::spawn_worker(const std::vector<std::string>& argv, const std::vector<std::string>& env,

@@ -101,6 +101,11 @@ class TrialRuntime {
   pid_t spawn(const std::string& trial, const std::vector<std::string>& argv, const std::vector<std::string>& env,
               const std::string& cwd, const std::string& log_path, const CollectorConfig& cfg,
               double deadline_seconds);
+  // Supervise a process started elsewhere (the fork server, controller/zygote.py) exactly like a
+  // spawned one: `pid` must be this process's child (re-parented: child subreaper) and its own
+  // process-group leader; `fd` is the read end of its stdout/stderr pipe (taken over, closed at exit).
+  bool adopt(const std::string& trial, pid_t pid, int fd, const std::string& log_path, const CollectorConfig& cfg,
+             double deadline_seconds);
   // Warm worker: a long-lived process speaking the \x1e line protocol.
   int spawn_worker(const std::vector<std::string>& argv, const std::vector<std::string>& env, const std::string& cwd,
                    const std::string& log_path);
@@ -122,6 +127,8 @@ class TrialRuntime {
   int num_running() const;
 
  private:
+  void track(const std::string& trial, pid_t pid, int fd, const std::string& log_path, const CollectorConfig& cfg,
+             double deadline_seconds);
   struct Proc;
   struct Worker;
   void add_fd(int fd);

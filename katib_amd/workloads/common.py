@@ -28,6 +28,26 @@ def device() -> torch.device:
     return torch.device("cpu")
 
 
+def process_start_time() -> float:
+    """Wall-clock time this process was created (fork), from /proc (10 ms resolution)."""
+    try:
+        with open("/proc/self/stat") as f:
+            start_ticks = int(f.read().rsplit(")", 1)[1].split()[19])
+        with open("/proc/stat") as f:
+            btime = next(int(ln.split()[1]) for ln in f if ln.startswith("btime"))
+        return btime + start_ticks / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, StopIteration, IndexError):
+        return float("nan")
+
+
+def phase(name: str, t: Optional[float] = None):
+    """Cold-trial phase breakdown (``KATIB_AMD_TRIAL_PHASES=1``): print ``katib-phase <name>
+    <wall time>`` (no ``=``, so the metrics collector ignores it); bench_trials.py pairs the lines
+    with the scheduler's launch and completion times."""
+    if os.environ.get("KATIB_AMD_TRIAL_PHASES") == "1":
+        print("katib-phase %s %.6f" % (name, time.time() if t is None else t), flush=True)
+
+
 def report(**metrics):
     print(" ".join("%s=%s" % (k, _fmt(v)) for k, v in metrics.items()), flush=True)
 

@@ -25,13 +25,19 @@ collector format).
 
 from __future__ import annotations
 
-import argparse
-import math
+import time as _time
 
-import torch
-import torch.nn.functional as F
+_T_MODULE = _time.time()  # cold-trial phases: the module starts importing (interpreter + katib_amd up)
 
-from .common import CapturedStep, Timer, device, report, teacher_vectors
+import argparse  # noqa: E402
+import math  # noqa: E402
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from .common import CapturedStep, Timer, device, phase, process_start_time, report, teacher_vectors  # noqa: E402
+
+_T_TORCH = _time.time()
 
 
 def parse_args(argv):
@@ -166,10 +172,18 @@ class HipMLP:
 
 
 def main(argv=None):
+    phase("process", process_start_time())
+    phase("module", _T_MODULE)
+    phase("torch", _T_TORCH)
     args = parse_args(argv if argv is not None else [])
     dev = device()
+    if dev.type == "cuda":
+        torch.zeros(1, device=dev).add_(1)
+        torch.cuda.synchronize()
+    phase("hip_init")
     torch.manual_seed(args.seed)
     x, y = teacher_vectors(args.num_train + args.num_valid, seed=1234, dev=dev)
+    phase("data")
     tx, ty = x[:args.num_train], y[:args.num_train]
     vx, vy = x[args.num_train:], y[args.num_train:]
     custom = args.num_layers > 0 or args.optimizer != "sgd"
@@ -216,6 +230,7 @@ def main(argv=None):
                     if torch.is_tensor(v):
                         v.zero_()
     gen = torch.Generator(device=dev).manual_seed(args.seed)
+    phase("model")
     timer = Timer()
     acc = 0.0
     for epoch in range(args.epochs):
@@ -225,6 +240,8 @@ def main(argv=None):
         for s in range(steps):
             idx.copy_(perm[s])
             step()
+            if epoch == 0 and s == step.warmup:
+                phase("captured")  # warm-up steps + graph capture + first replay issued
         with torch.no_grad(), torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=amp):
             pred = model(vx).argmax(1)
             acc = float((pred == vy).float().mean())
@@ -233,7 +250,10 @@ def main(argv=None):
             loss = float("nan")
         report(epoch=epoch, loss=loss, **{"Validation-accuracy": acc,
                                          "Train-accuracy": float(correct_buf) / max(steps * bs, 1)})
+        if epoch == 0:
+            phase("first_metric")
     report(**{"train_seconds": timer.elapsed()})
+    phase("trained")
     return acc
 
 
