@@ -50,6 +50,9 @@ class AmdConfig:
     # a Job / LocalProcess trial with amd.com/gpu: N > 1 runs as N rank processes ("ranks", one
     # process per GPU with the torchrun env) or as one process seeing all N GPUs ("single")
     multi_gpu_launch: str = "ranks"
+    # cold Python trial processes (`python3 -m module ...` Job commands) forked from a fork server
+    # that has already imported torch (controller/zygote.py); KATIB_AMD_ZYGOTE=0 turns it off
+    zygote: bool = True
 
 
 @dataclass

@@ -84,6 +84,7 @@ class TrialRun:
     deleted: bool = False
     scraper: Optional[object] = None  # PrometheusMetric collector (metricscollector/prometheus.py)
     prom_final: str = ""  # KATIB_PROMETHEUS_FINAL snapshot path
+    launcher: str = ""  # "exec" (fork + exec) or "zygote" (forked from the fork server)
 
 
 @dataclass
@@ -133,6 +134,8 @@ class Manager:
         self._lock = threading.RLock()
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
+        self._zygote = None  # fork server for cold Python trials (controller/zygote.py), started lazily
+        self._zygote_failed = False
         self._t0 = time.time()
         self._completed = 0
         self.fault_injector: Optional[Callable[[str, Key], bool]] = None
@@ -348,6 +351,9 @@ class Manager:
     def shutdown(self):
         self.stop()
         self.runtime.shutdown()
+        if self._zygote is not None:
+            self._zygote.close()
+            self._zygote = None
         if self._journal:
             self.store.close_journal()
 
@@ -913,12 +919,53 @@ class Manager:
             if rep.entrypoint or rep.function:
                 argv = [sys.executable, "-m", "katib_amd.controller.runentry", json.dumps(
                     {"entrypoint": rep.entrypoint, "args": argv, "function": rep.function})]
-            pid = self.runtime.spawn(proc_name, argv, ["%s=%s" % kv for kv in env.items()], cwd, lp, cfg,
-                                     float(plan.deadline))
+            pid = self._zygote_spawn(proc_name, argv, env, cwd, lp, cfg, float(plan.deadline))
+            run.launcher = "zygote" if pid > 0 else "exec"
+            if pid < 0:
+                pid = self.runtime.spawn(proc_name, argv, ["%s=%s" % kv for kv in env.items()], cwd, lp, cfg,
+                                         float(plan.deadline))
             if pid < 0:
                 raise RuntimeError("failed to start %s (see %s)" % (argv[0], lp))
         if run.phase == "Launching" and run.worker is None:
             self._mark_running(tkey)
+
+    def _zygote_spawn(self, proc_name, argv, env, cwd, log_path, cfg, deadline) -> int:
+        """Start a cold Python trial from the fork server (controller/zygote.py) and hand it to the
+        native runtime (``TrialRuntime.adopt``); -1: not eligible or the server is unavailable,
+        the caller then fork+execs as before. The trial sees the same environment as an exec'd
+        one: this process's environment with the trial's entries on top."""
+        from .zygote import Zygote
+
+        if self._zygote_failed or not self.config.amd.zygote or os.environ.get("KATIB_AMD_ZYGOTE", "1") == "0" \
+                or not Zygote.eligible(argv):
+            return -1
+        if self._zygote is None or not self._zygote.alive():
+            try:
+                self._zygote = Zygote(self.state_dir)
+            except Exception as e:  # noqa: BLE001 - the exec path always works
+                log.warning("fork server unavailable (%s): trials are exec'd", e)
+                self._zygote_failed = True
+                return -1
+        full = dict(os.environ)
+        full.update(env)
+        r, w = os.pipe()
+        try:
+            pid = self._zygote.spawn(argv, full, cwd, w)
+        except Exception as e:  # noqa: BLE001
+            log.warning("fork server spawn failed (%s): exec instead", e)
+            os.close(r)
+            os.close(w)
+            return -1
+        os.close(w)
+        if not self.runtime.adopt(proc_name, pid, r, log_path, cfg, deadline):
+            os.close(r)
+            try:
+                os.killpg(pid, 9)
+                os.waitpid(pid, 0)
+            except OSError:
+                pass
+            return -1
+        return pid
 
     def _mark_running(self, tkey):
         run = self.runs[tkey]

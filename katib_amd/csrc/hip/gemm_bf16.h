@@ -10,5 +10,12 @@ bool supported(int M, int N, int K);  // M, N multiples of 128, K of 64
 hipError_t launch_nt(const void* A, const void* W, const void* bias, void* C, void* G, int M, int N, int K,
                      hipStream_t st);
 
+// Layout-native GEMM: C = op(A) op(B), op(A)[M][K] from A stored [M][K] (a_mn false) or [K][M]
+// (a_mn true), op(B)[K][N] from B stored [N][K] (b_mn false) or [K][N] (b_mn true); lda / ldb are
+// the stored row strides (elements). out_f32: C is an fp32 slab [splitk][M][N] (one slab per K
+// slice), else bf16 [M][N] (+ bias[N], splitk 1). M, N multiples of 128, K of 64 * splitk.
+hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
+                     bool out_f32, int splitk, int M, int N, int K, hipStream_t st);
+
 }  // namespace gemm
 }  // namespace katib_hip

@@ -166,7 +166,350 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const uint16_t* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Layout-native variants for the backward GEMMs (no transposed copies):
+//   dgrad  dX[M][N] = dY[M][K] . W[K][N]      A K-contiguous, B MN-contiguous   ("NN")
+//   wgrad  dW[M][N] = dY^T X: A = dY [K][M], B = X [K][N]   both MN-contiguous   ("TN")
+// An MN-contiguous operand K-tile (64 k rows x 128 mn, 256-byte rows) is staged by the same
+// lane-linear LDS-DMA as the K-contiguous one, and its MFMA fragments (8 consecutive k of one mn
+// column per lane) are read with the hardware transpose ds_read_b64_tr_b16: per 16-lane group a
+// 4-row x 16-column block arrives column-major, two reads per fragment. Bank conflicts: the eight
+// rows a 32-lane half reads (q = 0..3 of k groups 8g and 8g + 8) each cover two 16-byte slots of a
+// 256-byte row; the slot XOR 2 * ((r & 3) | ((r >> 3) & 1) << 2) gives them eight distinct even
+// slot pairs (all 64 banks once), applied on the DMA source address and undone on the read.
+// Split-K (gridDim.y slices, fp32 output slabs [slice][M][N]) gives the long-K wgrad shapes
+// (K = tokens) enough workgroups; a row-sum kernel folds the slabs.
+// ------------------------------------------------------------------------------------------------
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4* lds_s16x4;
+
+__device__ __forceinline__ constexpr int mn_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+// one MN-contiguous operand K-tile (64 k rows x 128 mn bf16) -> LDS: 4 DMA instructions per thread
+__device__ __forceinline__ void stage_mn(const uint16_t* __restrict__ src, int ld, int mn0, int k0, char* lds,
+                                         int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = i * 4 + wave;           // 4-row (1 KB) block of this wave instruction
+    const int row = blk * 4 + (lane >> 4);  // k row: 16 lanes per 256-byte row
+    const int chunk = (lane & 15) ^ mn_swz(row);
+    const uint16_t* g = src + (size_t)(k0 + row) * ld + mn0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds(g, (lds_ptr)(lds + blk * 1024), 16, 0, 0);
+  }
+}
+
+// MFMA operand fragment of mn columns [mn_base, mn_base + 16), k = kk * 32 + 8 (lane >> 4) + j
+__device__ __forceinline__ bf16x8 frag_mn(const char* lds, int mn_base, int kk, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const int col = mn_base + 4 * (li & 3), chunk = col >> 3, half = (col >> 2) & 1;
+  const int r0 = kk * 32 + 8 * g + (li >> 2), r1 = r0 + 4;
+  const char* p0 = lds + r0 * 256 + ((chunk ^ mn_swz(r0)) << 4) + half * 8;
+  const char* p1 = lds + r1 * 256 + ((chunk ^ mn_swz(r1)) << 4) + half * 8;
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4)(p0));
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4)(p1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// C (+)= op(A) op(B) over k slice blockIdx.y; OUT_F32: fp32 slab [slice][M][N], else bf16 (+ bias)
+template <bool A_MN, bool B_MN, bool OUT_F32>
+__global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict__ A, int lda,
+                                                      const uint16_t* __restrict__ B, int ldb,
+                                                      const uint16_t* __restrict__ bias, void* __restrict__ Cv,
+                                                      int M, int N, int kslice) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * TILE_BYTES];  // [stage][A|B][16 KB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+  const int NB = N / BN, nwg = NB * (M / BM), b = blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, xcd = b % 8, loc = b / 8;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  const int m0 = (t / NB) * BM, n0 = (t % NB) * BN;
+  const int kbeg = blockIdx.y * kslice;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kslice / BK;
+  auto stage_tile = [&](int kt) {
+    char* d = lds + (kt & 1) * 2 * TILE_BYTES;
+    const int k0 = kbeg + kt * BK;
+    if constexpr (A_MN) stage_mn(A, lda, m0, k0, d, wave, lane);
+    else stage(A, lda, m0, k0, d, wave, lane);
+    if constexpr (B_MN) stage_mn(B, ldb, n0, k0, d + TILE_BYTES, wave, lane);
+    else stage(B, ldb, n0, k0, d + TILE_BYTES, wave, lane);
+  };
+  auto compute = [&](int kt) {
+    const char* la = lds + (kt & 1) * 2 * TILE_BYTES;
+    const char* lb = la + TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+      bf16x8 a[4], w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = A_MN ? frag_mn(la, wr * 64 + i * 16, kk, lane) : frag(la, wr * 64 + i * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = B_MN ? frag_mn(lb, wc * 64 + j * 16, kk, lane) : frag(lb, wc * 64 + j * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  stage_tile(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) stage_tile(kt + 1);  // the other buffer: its readers passed the last barrier
+    compute(kt);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if constexpr (OUT_F32) {
+    // fp32 slab rows of this slice: each wave stages its 64 x 64 tile in LDS (256-byte rows) and
+    // writes 16-byte row segments
+    float* C = static_cast<float*>(Cv) + (size_t)blockIdx.y * M * N;
+    float* tile = reinterpret_cast<float*>(lds + wave * 16384);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tile[(i * 16 + (lane >> 4) * 4 + e) * 64 + j * 16 + (lane & 15)] = acc[i][j][e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = it * 4 + (lane >> 4), ch = lane & 15;
+      *reinterpret_cast<float4*>(C + (size_t)(m0 + wr * 64 + row) * N + n0 + wc * 64 + ch * 4) =
+          *reinterpret_cast<const float4*>(tile + row * 64 + ch * 4);
+    }
+  } else {
+    uint16_t* C = static_cast<uint16_t*>(Cv);
+    char* tile_u = lds + wave * 8192;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = j * 16 + (lane & 15);
+      const float bv = bias ? bf2f(bias[n0 + wc * 64 + col]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          *reinterpret_cast<uint16_t*>(tile_u + (i * 16 + (lane >> 4) * 4 + e) * 128 + col * 2) = f2bf(acc[i][j][e] + bv);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 8 + (lane >> 3), ch = lane & 7;
+      *reinterpret_cast<uint4*>(C + (size_t)(m0 + wr * 64 + row) * N + n0 + wc * 64 + ch * 8) =
+          *reinterpret_cast<const uint4*>(tile_u + row * 128 + ch * 16);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// 256 x 128 tile, 8 waves (4 along M x 2 along N, 64 x 64 each), three LDS stages (144 KB, one
+// workgroup per CU): the DMA of K-tile t + 2 is issued right after the barrier that opens tile t
+// and stays in flight across the next barrier - each wave waits only for its OWN 6 loads of the
+// tile about to be read (counted vmcnt, never 0 in the loop) before a raw s_barrier (no
+// __syncthreads: its fence would drain the DMA). Two waves per SIMD keep the matrix pipe fed while
+// the other pair waits on LDS. Operand tiles are 1 KB DMA blocks of 16 KB sub-images (K-contiguous
+// [128 rows][64 k] or MN-contiguous [64 k][128 mn], the same swizzled images as above).
+// ------------------------------------------------------------------------------------------------
+constexpr int BM2 = 256, BN2 = 128, SUB = 16384, STAGE2 = 3 * SUB;  // per stage: A 2 sub-images + B 1
+
+// DMA block `blk` (0..15) of a 16 KB sub-image whose first mn row / column is mn0
+template <bool MN>
+__device__ __forceinline__ void stage_blk(const uint16_t* __restrict__ src, int ld, int mn0, int k0, char* img,
+                                          int blk, int lane) {
+  if constexpr (MN) {
+    const int row = blk * 4 + (lane >> 4);
+    const int chunk = (lane & 15) ^ mn_swz(row);
+    __builtin_amdgcn_global_load_lds(src + (size_t)(k0 + row) * ld + mn0 + chunk * 8, (lds_ptr)(img + blk * 1024),
+                                     16, 0, 0);
+  } else {
+    const int row = blk * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ (row & 7);
+    __builtin_amdgcn_global_load_lds(src + (size_t)(mn0 + row) * ld + k0 + chunk * 8, (lds_ptr)(img + blk * 1024),
+                                     16, 0, 0);
+  }
+}
+
+template <bool A_MN, bool B_MN, bool OUT_F32>
+__global__ void __launch_bounds__(512) gemm_lt2_kernel(const uint16_t* __restrict__ A, int lda,
+                                                       const uint16_t* __restrict__ B, int ldb,
+                                                       const uint16_t* __restrict__ bias, void* __restrict__ Cv,
+                                                       int M, int N, int kslice) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [3 stages][A0 | A1 | B] 16 KB each
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+  const int NB = N / BN2, nwg = NB * (M / BM2), b = blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, xcd = b % 8, loc = b / 8;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  const int m0 = (t / NB) * BM2, n0 = (t % NB) * BN2;
+  const int kbeg = blockIdx.y * kslice;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kslice / BK;
+  // 48 DMA blocks per stage, 6 per wave: A sub-image (wave >> 2) blocks (wave & 3) * 4 .. + 3, B blocks
+  // (wave * 2, wave * 2 + 1)
+  auto stage_tile = [&](int kt) {
+    char* d = lds + (kt % 3) * STAGE2;
+    const int k0 = kbeg + kt * BK, ai = wave >> 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      stage_blk<A_MN>(A, lda, m0 + ai * 128, k0, d + ai * SUB, (wave & 3) * 4 + i, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) stage_blk<B_MN>(B, ldb, n0, k0, d + 2 * SUB, wave * 2 + i, lane);
+  };
+  auto compute = [&](int kt) {
+    const char* la = lds + (kt % 3) * STAGE2 + (wr >> 1) * SUB;  // this wave's 128-row A sub-image
+    const char* lb = lds + (kt % 3) * STAGE2 + 2 * SUB;
+    const int ar = (wr & 1) * 64;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+      bf16x8 a[4], w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = A_MN ? frag_mn(la, ar + i * 16, kk, lane) : frag(la, ar + i * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = B_MN ? frag_mn(lb, wc * 64 + j * 16, kk, lane) : frag(lb, wc * 64 + j * 16 + (lane & 15), chunk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+  stage_tile(0);
+  if (nk > 1) stage_tile(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's 6 loads of tile kt have landed (tile kt + 1's 6 may stay in flight), every wave
+    // is past compute(kt - 1), whose buffer the next stage_tile refills
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) stage_tile(kt + 2);
+    compute(kt);
+  }
+  __builtin_amdgcn_s_barrier();  // every wave's reads done before the epilogue reuses the LDS
+
+  const int orow = m0 + wr * 64, ocol = n0 + wc * 64;
+  if constexpr (OUT_F32) {
+    float* C = static_cast<float*>(Cv) + (size_t)blockIdx.y * M * N;
+    float* tile = reinterpret_cast<float*>(lds + wave * 16384);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tile[(i * 16 + (lane >> 4) * 4 + e) * 64 + j * 16 + (lane & 15)] = acc[i][j][e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = it * 4 + (lane >> 4), ch = lane & 15;
+      *reinterpret_cast<float4*>(C + (size_t)(orow + row) * N + ocol + ch * 4) =
+          *reinterpret_cast<const float4*>(tile + row * 64 + ch * 4);
+    }
+  } else {
+    uint16_t* C = static_cast<uint16_t*>(Cv);
+    char* tile_u = lds + wave * 8192;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = j * 16 + (lane & 15);
+      const float bv = bias ? bf2f(bias[ocol + col]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          *reinterpret_cast<uint16_t*>(tile_u + (i * 16 + (lane >> 4) * 4 + e) * 128 + col * 2) = f2bf(acc[i][j][e] + bv);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 8 + (lane >> 3), ch = lane & 7;
+      *reinterpret_cast<uint4*>(C + (size_t)(orow + row) * N + ocol + ch * 8) =
+          *reinterpret_cast<const uint4*>(tile_u + row * 128 + ch * 16);
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
+                     bool out_f32, int splitk, int M, int N, int K, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || splitk < 1 || K % (splitk * BK) ||
+      (!out_f32 && splitk != 1))
+    return hipErrorInvalidValue;
+  const uint16_t* a = static_cast<const uint16_t*>(A);
+  const uint16_t* b = static_cast<const uint16_t*>(B);
+  const uint16_t* bb = static_cast<const uint16_t*>(bias);
+  const int ks = K / splitk;
+  // tile: KATIB_HIP_GEMM_TILE=256 (256 x 128, 3 stages, 8 waves) / 128 (128 x 128, 2 stages)
+  static const int tile = getenv("KATIB_HIP_GEMM_TILE") ? atoi(getenv("KATIB_HIP_GEMM_TILE")) : 256;
+  if (tile == 256 && M % BM2 == 0) {
+    static bool attr = false;
+    if (!attr) {  // > 64 KB of dynamic LDS must be opted into per kernel
+      const void* ks_[] = {(const void*)gemm_lt2_kernel<false, false, false>, (const void*)gemm_lt2_kernel<false, true, false>,
+                           (const void*)gemm_lt2_kernel<true, false, false>, (const void*)gemm_lt2_kernel<true, true, false>,
+                           (const void*)gemm_lt2_kernel<false, false, true>, (const void*)gemm_lt2_kernel<false, true, true>,
+                           (const void*)gemm_lt2_kernel<true, false, true>, (const void*)gemm_lt2_kernel<true, true, true>};
+      for (const void* f : ks_) hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * STAGE2);
+      attr = true;
+    }
+    const dim3 grid2((M / BM2) * (N / BN2), splitk);
+#define LT2_LAUNCH(AM, BMN, F32) \
+  hipLaunchKernelGGL((gemm_lt2_kernel<AM, BMN, F32>), grid2, dim3(512), 3 * STAGE2, st, a, lda, b, ldb, bb, C, M, N, ks)
+    if (out_f32) {
+      if (a_mn && b_mn) LT2_LAUNCH(true, true, true);
+      else if (a_mn) LT2_LAUNCH(true, false, true);
+      else if (b_mn) LT2_LAUNCH(false, true, true);
+      else LT2_LAUNCH(false, false, true);
+    } else {
+      if (a_mn && b_mn) LT2_LAUNCH(true, true, false);
+      else if (a_mn) LT2_LAUNCH(true, false, false);
+      else if (b_mn) LT2_LAUNCH(false, true, false);
+      else LT2_LAUNCH(false, false, false);
+    }
+#undef LT2_LAUNCH
+    return hipGetLastError();
+  }
+  const dim3 grid((M / BM) * (N / BN), splitk);
+#define LT_LAUNCH(AM, BMN, F32) \
+  hipLaunchKernelGGL((gemm_lt_kernel<AM, BMN, F32>), grid, dim3(256), 0, st, a, lda, b, ldb, bb, C, M, N, ks)
+  if (out_f32) {
+    if (a_mn && b_mn) LT_LAUNCH(true, true, true);
+    else if (a_mn) LT_LAUNCH(true, false, true);
+    else if (b_mn) LT_LAUNCH(false, true, true);
+    else LT_LAUNCH(false, false, true);
+  } else {
+    if (a_mn && b_mn) LT_LAUNCH(true, true, false);
+    else if (a_mn) LT_LAUNCH(true, false, false);
+    else if (b_mn) LT_LAUNCH(false, true, false);
+    else LT_LAUNCH(false, false, false);
+  }
+#undef LT_LAUNCH
+  return hipGetLastError();
+}
 
 bool supported(int M, int N, int K) { return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0; }
 

@@ -233,9 +233,43 @@ void gemm_nt(const Tensor& A, const Tensor& W, const c10::optional<Tensor>& bias
      "gemm_nt");
 }
 
+// C = op(A) op(B) on the layout-native MFMA kernel (gemm_bf16.hip gemm_lt_kernel): a_mn: A stored
+// [K][M] (else [M][K]); b_mn: B stored [K][N] (else [N][K]). C: bf16 [M][N] (splitk 1, optional
+// bias) or fp32 [splitk][M][N] slabs (one per K slice, summed by the caller).
+void gemm_lt(const Tensor& A, bool a_mn, const Tensor& B, bool b_mn, const c10::optional<Tensor>& bias,
+             const Tensor& C, int64_t splitk) {
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "gemm_lt: 2-D operands");
+  const int64_t M = a_mn ? A.size(1) : A.size(0), K = a_mn ? A.size(0) : A.size(1);
+  const int64_t N = b_mn ? B.size(1) : B.size(0), KB = b_mn ? B.size(0) : B.size(1);
+  TORCH_CHECK(KB == K, "gemm_lt: inner dimensions differ");
+  TORCH_CHECK(M % 128 == 0 && N % 128 == 0 && splitk >= 1 && K % (64 * splitk) == 0,
+              "gemm_lt: M, N % 128 and K % (64 splitk) required");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm_lt: dims");
+  chk(A, at::kBFloat16, M * K, "A");
+  chk(B, at::kBFloat16, N * K, "B");
+  const bool f32 = C.scalar_type() == at::kFloat;
+  if (f32) chk(C, at::kFloat, splitk * M * N, "C");
+  else {
+    TORCH_CHECK(splitk == 1, "gemm_lt: a bf16 output needs splitk 1");
+    chk(C, at::kBFloat16, M * N, "C");
+  }
+  const void* bp_ = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(!f32, "gemm_lt: bias only with a bf16 output");
+    chk(*bias, at::kBFloat16, N, "bias");
+    bp_ = bias->data_ptr();
+  }
+  ok(katib_hip::gemm::launch_lt(A.data_ptr(), (int)A.size(1), a_mn, B.data_ptr(), (int)B.size(1), b_mn, bp_,
+                                C.data_ptr(), f32, (int)splitk, (int)M, (int)N, (int)K, stream()),
+     "gemm_lt");
+}
+
 }  // namespace
 
 void register_transformer(py::module& m) {
+  m.def("gemm_lt", &gemm_lt, "bf16 C = op(A) op(B), layout-native operands (NN / TN / NT), split-K fp32 slabs",
+        py::arg("A"), py::arg("a_mn"), py::arg("B"), py::arg("b_mn"), py::arg("bias"), py::arg("C"),
+        py::arg("splitk") = 1);
   m.def("gemm_nt", &gemm_nt, "bf16 C = A W^T (+ bias) (+ GELU) on MFMA (gemm_bf16.hip)");
   m.def("gemm_nt_supported", [](int64_t M, int64_t N, int64_t K) {
     return M < (1 << 30) && N < (1 << 30) && K < (1 << 30) && katib_hip::gemm::supported((int)M, (int)N, (int)K);

@@ -220,21 +220,21 @@ class GPT2Flat:
             # MLP: dr is the gradient of fc2's output
             ops.wgrad(dr, gl, g[pre + "fc2.weight"])
             ops.colsum(dr, g[pre + "fc2.bias"])
-            du = ops.gelu_bwd(u, torch.mm(dr, self.w[pre + "fc2.weight"]))
+            du = ops.gelu_bwd(u, ops.dgrad(dr, self.w[pre + "fc2.weight"]))
             ops.wgrad(du, h2, g[pre + "fc.weight"])
             ops.colsum(du, g[pre + "fc.bias"])
-            dh2 = torch.mm(du, self.w[pre + "fc.weight"])
+            dh2 = ops.dgrad(du, self.w[pre + "fc.weight"])
             del du
             ops.ln_bwd(dh2, sb, mu2, rs2, self.w[pre + "ln2.weight"], G, dr, g[pre + "ln2.weight"],
                        g[pre + "ln2.bias"])
             # attention: dr is now the gradient of proj's output
             ops.wgrad(dr, o, g[pre + "proj.weight"])
             ops.colsum(dr, g[pre + "proj.bias"])
-            do = torch.mm(dr, self.w[pre + "proj.weight"])
+            do = ops.dgrad(dr, self.w[pre + "proj.weight"])
             dqkv = ops.attn_bwd(qkv, o, do, lse, B, T, H, d // H)
             ops.wgrad(dqkv, h1, g[pre + "qkv.weight"])
             ops.colsum(dqkv, g[pre + "qkv.bias"])
-            dh1 = torch.mm(dqkv, self.w[pre + "qkv.weight"])
+            dh1 = ops.dgrad(dqkv, self.w[pre + "qkv.weight"])
             del dqkv
             ops.ln_bwd(dh1, sa, mu1, rs1, self.w[pre + "ln1.weight"], G, dr if i > 0 else None,
                        g[pre + "ln1.weight"], g[pre + "ln1.bias"])

@@ -134,6 +134,9 @@ class TorchOps:
     def colsum(self, x, out):
         torch.sum(x, 0, out=out)
 
+    def dgrad(self, dy, w):
+        return torch.mm(dy, w)
+
     def wgrad(self, dy, x, out):
         torch.mm(dy.t(), x, out=out)
 
@@ -249,13 +252,53 @@ class HipOps:
         """Bias gradient: bf16 column sums of [M, N] (two-stage, fp32 partials)."""
         self.k.colsum(x, out)
 
+    # Backward GEMMs on the layout-native kernel (gemm_lt: dgrad NN, wgrad TN, no transposed
+    # copies; profiles/gemm_fwd_bwd_table_r05.log, MI355X, median of 5 interleaved rounds):
+    # every projection wgrad beats hipBLASLt 1.07-2.06x with the split-K below; the LM head wgrad
+    # (0.86x) and the dgrads at 16k tokens (0.58-0.86x: hipBLASLt's larger tiles reach ~1 PF/s
+    # where the 128^2 two-stage tile holds ~750 TF/s) stay on hipBLASLt, the d x d dgrad at 8k
+    # tokens wins 1.19x. KATIB_HIP_GEMM_BWD=0: hipBLASLt for all, =all: gemm_lt wherever supported.
+    WGRAD_SPLIT = {(768, 768): 8, (2304, 768): 4, (3072, 768): 8, (768, 3072): 8}  # (out, in) -> split-K
+    DGRAD_WINS = {(768, 768)}  # (out, in) classes of W where the NN kernel won (at <= 8k tokens)
+
+    def _bwd_mode(self):
+        return os.environ.get("KATIB_HIP_GEMM_BWD", "auto")
+
+    def _lt_ok(self, *ts):
+        return all(t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous() for t in ts)
+
+    def dgrad(self, dy, w):
+        """``dy @ w`` ([M, K] from dy [M, N], w [N, K]): the NN GEMM where it wins, else hipBLASLt."""
+        M, N = dy.shape
+        K = w.shape[1]
+        mode = self._bwd_mode()
+        use = mode == "all" or (mode == "auto" and (N, K) in self.DGRAD_WINS and M <= 8192)
+        if use and mode != "0" and self._lt_ok(dy, w) and M % 128 == 0 and K % 128 == 0 and N % 64 == 0:
+            out = torch.empty((M, K), device=dy.device, dtype=torch.bfloat16)
+            self.k.gemm_lt(dy, False, w, True, None, out)
+            return out
+        return torch.mm(dy, w)
+
     def wgrad(self, dy, x, out):
         """``out = dy^T x`` ([N, K] from [M, N], [M, K]). The reduction over M = B*T tokens is
         long and the output small (768 x 768 = 36 tiles of 128^2 for the attention
-        projection), so split it S ways into a batched GEMM with fp32 output and add the
-        slabs with one kernel: >= 512 output tiles fill the 256 CUs."""
+        projection), so it is split S ways: the layout-native TN kernel (gemm_lt) writes one fp32
+        slab per K slice and one row-sum launch adds them into the bf16 gradient."""
         M, N = dy.shape
         K = x.shape[1]
+        mode = self._bwd_mode()
+        S = self.WGRAD_SPLIT.get((N, K)) if mode == "auto" else (8 if mode == "all" else None)
+        if S is not None and self._lt_ok(dy, x) and out.is_contiguous() and N % 128 == 0 and K % 128 == 0:
+            while S > 1 and M % (64 * S):
+                S //= 2
+            if M % 64 == 0:
+                if S == 1:
+                    self.k.gemm_lt(dy, True, x, True, None, out)
+                    return
+                part = torch.empty((S, N, K), device=dy.device, dtype=torch.float32)
+                self.k.gemm_lt(dy, True, x, True, None, part, S)
+                self.k.reduce_rows(part.view(S, N * K), out.view(-1))
+                return
         tiles = -(-N // 128) * -(-K // 128)
         S = 1
         while tiles * S < 512 and M % (2 * S) == 0 and M // (2 * S) >= 1024:

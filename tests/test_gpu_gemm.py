@@ -57,3 +57,45 @@ def test_gpt2_forward_hip_gemm_matches_torch_ops():
         m = GPT2Flat(cfg, dev, ops, seed=0)
         outs.append(m.forward(idx).float())
     torch.testing.assert_close(outs[1], outs[0], rtol=5e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("a_mn,b_mn", [(False, True), (True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("M,N,K,splitk", [(128, 128, 64, 1), (256, 768, 2304, 1), (768, 768, 4096, 4),
+                                          (384, 256, 1024, 2), (3072, 768, 2048, 8)])
+def test_gemm_lt_layouts_match_fp32(a_mn, b_mn, M, N, K, splitk):
+    """Layout-native GEMM (gemm_lt_kernel): NN (dgrad), TN (wgrad), NT and TT operand layouts, the
+    MN-contiguous operands read through ds_read_b64_tr_b16 with the swizzled LDS image; bf16 output
+    (splitk 1) or fp32 split-K slabs summed here. Asymmetric data so a transposed fragment fails."""
+    k = _k()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(M * 3 + N * 5 + K + 7 * splitk)
+    opA = torch.randn(M, K, device=dev, generator=g) + (torch.arange(M, device=dev)[:, None] % 7) * 0.1
+    opB = (torch.randn(K, N, device=dev, generator=g) + (torch.arange(N, device=dev)[None, :] % 5) * 0.05) * 0.05
+    opA, opB = opA.to(torch.bfloat16), opB.to(torch.bfloat16)
+    A = opA.t().contiguous() if a_mn else opA  # stored [K][M] or [M][K]
+    B = opB.contiguous() if b_mn else opB.t().contiguous()  # stored [K][N] or [N][K]
+    ref = opA.float() @ opB.float()
+    tol = dict(rtol=2e-2, atol=2e-2 * float(ref.abs().max()) ** 0.5)
+    if splitk == 1:
+        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        k.gemm_lt(A, a_mn, B, b_mn, None, C)
+        torch.testing.assert_close(C.float(), ref, **tol)
+    C32 = torch.empty(splitk, M, N, device=dev, dtype=torch.float32)
+    k.gemm_lt(A, a_mn, B, b_mn, None, C32, splitk)
+    torch.testing.assert_close(C32.sum(0), ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))
+
+
+def test_gemm_lt_bias_and_errors():
+    k = _k()
+    dev = torch.device("cuda", 0)
+    A = torch.randn(256, 512, device=dev).to(torch.bfloat16)
+    B = torch.randn(512, 384, device=dev).to(torch.bfloat16)
+    b = torch.randn(384, device=dev).to(torch.bfloat16)
+    C = torch.empty(256, 384, device=dev, dtype=torch.bfloat16)
+    k.gemm_lt(A, False, B, True, b, C)
+    ref = A.float() @ B.float() + b.float()
+    torch.testing.assert_close(C.float(), ref, rtol=2e-2, atol=0.2)
+    with pytest.raises(RuntimeError):
+        k.gemm_lt(A, False, B[:, :100].contiguous(), True, None, C)  # N % 128
+    with pytest.raises(RuntimeError):
+        k.gemm_lt(A, False, B, True, None, C, 2)  # bf16 output with split-K
