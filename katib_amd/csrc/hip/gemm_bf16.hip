@@ -244,21 +244,26 @@ __global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict
   auto compute = [&](int kt) {
     const char* la = lds + (kt & 1) * 2 * TILE_BYTES;
     const char* lb = la + TILE_BYTES;
+    // both k sub-steps' fragments issued up front: the second half's LDS reads are in flight
+    // while the first half's MFMAs run (the wait before them is counted, not a drain)
+    bf16x8 a[2][4], w[2][4];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + (lane >> 4);
-      bf16x8 a[4], w[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        a[i] = A_MN ? frag_mn(la, wr * 64 + i * 16, kk, lane) : frag(la, wr * 64 + i * 16 + (lane & 15), chunk);
+        a[kk][i] = A_MN ? frag_mn(la, wr * 64 + i * 16, kk, lane) : frag(la, wr * 64 + i * 16 + (lane & 15), chunk);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        w[j] = B_MN ? frag_mn(lb, wc * 64 + j * 16, kk, lane) : frag(lb, wc * 64 + j * 16 + (lane & 15), chunk);
+        w[kk][j] = B_MN ? frag_mn(lb, wc * 64 + j * 16, kk, lane) : frag(lb, wc * 64 + j * 16 + (lane & 15), chunk);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], w[kk][j], acc[i][j], 0, 0, 0);
   };
   stage_tile(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -378,23 +383,26 @@ __global__ void __launch_bounds__(512) gemm_lt2_kernel(const uint16_t* __restric
     const char* la = lds + (kt % 3) * STAGE2 + (wr >> 1) * SUB;  // this wave's 128-row A sub-image
     const char* lb = lds + (kt % 3) * STAGE2 + 2 * SUB;
     const int ar = (wr & 1) * 64;
+    bf16x8 a[2][4], w[2][4];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + (lane >> 4);
-      bf16x8 a[4], w[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        a[i] = A_MN ? frag_mn(la, ar + i * 16, kk, lane) : frag(la, ar + i * 16 + (lane & 15), chunk);
+        a[kk][i] = A_MN ? frag_mn(la, ar + i * 16, kk, lane) : frag(la, ar + i * 16 + (lane & 15), chunk);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        w[j] = B_MN ? frag_mn(lb, wc * 64 + j * 16, kk, lane) : frag(lb, wc * 64 + j * 16 + (lane & 15), chunk);
-      __builtin_amdgcn_s_setprio(1);
+        w[kk][j] = B_MN ? frag_mn(lb, wc * 64 + j * 16, kk, lane) : frag(lb, wc * 64 + j * 16 + (lane & 15), chunk);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], w[kk][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   };
   stage_tile(0);
   if (nk > 1) stage_tile(1);
@@ -464,8 +472,10 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
   const uint16_t* b = static_cast<const uint16_t*>(B);
   const uint16_t* bb = static_cast<const uint16_t*>(bias);
   const int ks = K / splitk;
-  // tile: KATIB_HIP_GEMM_TILE=256 (256 x 128, 3 stages, 8 waves) / 128 (128 x 128, 2 stages)
-  static const int tile = getenv("KATIB_HIP_GEMM_TILE") ? atoi(getenv("KATIB_HIP_GEMM_TILE")) : 256;
+  // tile: 128 (128 x 128, 2 stages, 2 workgroups per CU; default) or KATIB_HIP_GEMM_TILE=256
+  // (256 x 128, 3 stages, 8 waves, 1 per CU): measured 15-25 % slower on every GPT-2 backward shape
+  // (profiles/gemm_fwd_bwd_table_r05.log), kept selectable
+  static const int tile = getenv("KATIB_HIP_GEMM_TILE") ? atoi(getenv("KATIB_HIP_GEMM_TILE")) : 128;
   if (tile == 256 && M % BM2 == 0) {
     static bool attr = false;
     if (!attr) {  // > 64 KB of dynamic LDS must be opted into per kernel

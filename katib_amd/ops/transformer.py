@@ -253,12 +253,13 @@ class HipOps:
         self.k.colsum(x, out)
 
     # Backward GEMMs on the layout-native kernel (gemm_lt: dgrad NN, wgrad TN, no transposed
-    # copies; profiles/gemm_fwd_bwd_table_r05.log, MI355X, median of 5 interleaved rounds):
-    # every projection wgrad beats hipBLASLt 1.07-2.06x with the split-K below; the LM head wgrad
-    # (0.86x) and the dgrads at 16k tokens (0.58-0.86x: hipBLASLt's larger tiles reach ~1 PF/s
-    # where the 128^2 two-stage tile holds ~750 TF/s) stay on hipBLASLt, the d x d dgrad at 8k
-    # tokens wins 1.19x. KATIB_HIP_GEMM_BWD=0: hipBLASLt for all, =all: gemm_lt wherever supported.
-    WGRAD_SPLIT = {(768, 768): 8, (2304, 768): 4, (3072, 768): 8, (768, 3072): 8}  # (out, in) -> split-K
+    # copies; profiles/gemm_fwd_bwd_table_r05.log, MI355X, median of 5 interleaved rounds, 16k
+    # tokens = the PBT member's batch). Against the best hipBLASLt form (split-K batched fp32 +
+    # row sum for wgrad, the strided mm for dgrad) the 128^2 two-stage tile (~600-800 TF/s) wins
+    # only the qkv wgrad (1.07x); hipBLASLt's 192x256 / 256x256 tiles reach ~1 PF/s on the rest.
+    # The d x d dgrad wins at 8k tokens (1.19x). KATIB_HIP_GEMM_BWD=0: hipBLASLt for all, =all:
+    # gemm_lt wherever supported (tests).
+    WGRAD_SPLIT = {(2304, 768): 4}  # (out, in) -> split-K
     DGRAD_WINS = {(768, 768)}  # (out, in) classes of W where the NN kernel won (at <= 8k tokens)
 
     def _bwd_mode(self):

@@ -9,8 +9,8 @@ L=gpurun_out/r05e.log
 : > $L
 echo "=== pytest $(date +%T)" >> $L
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_gemm.py >> $L 2>&1 || exit 1
-echo "=== bench 8192 $(date +%T)" >> $L
-timeout -k 10 400 python benchmarks/bench_gemm.py --backward-only --tokens 8192 >> $L 2>&1 || exit 1
-echo "=== bench 16384 $(date +%T)" >> $L
-timeout -k 10 400 python benchmarks/bench_gemm.py --backward --tokens 16384 >> $L 2>&1 || exit 1
+echo "=== tile128 16384 $(date +%T)" >> $L
+timeout -k 10 400 env KATIB_HIP_GEMM_TILE=128 python benchmarks/bench_gemm.py --backward-only --tokens 16384 >> $L 2>&1 || exit 1
+echo "=== tile256 16384 $(date +%T)" >> $L
+timeout -k 10 400 env KATIB_HIP_GEMM_TILE=256 python benchmarks/bench_gemm.py --backward-only --tokens 16384 >> $L 2>&1 || exit 1
 echo done >> $L
