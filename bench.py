@@ -59,7 +59,7 @@ def main():
     ap.add_argument("--config", default="b5", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=128, help="global batch (strong) / per-GPU batch (weak)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
-    ap.add_argument("--trials", type=int, default=3, help="trials per GPU of the trials/hour experiment (0: skip)")
+    ap.add_argument("--trials", type=int, default=12, help="trials per GPU of the trials/hour experiment (0: skip)")
     ap.add_argument("--trial-slots", type=int, default=1,
                     help="concurrent trials per GPU in the trials/hour experiment (warm workers per GPU)")
     ap.add_argument("--comparator-steps", type=int, default=5,
@@ -366,8 +366,10 @@ def b1_trials_per_hour(gpus: int):
         return None
     return {"value": res["value"], "unit": "trials/h", "vs_b1": res["vs_baseline"], "wall_s": res["wall_s"],
             "trials_completed": res["trials_completed"], "median_trial_s": res["median_trial_s"],
+            "launcher": res.get("launcher"), "trial_phases_s": res.get("trial_phases_s"),
             "best_validation_accuracy": res["best_objective"], "n_gpus": gpus,
-            "config": "B1 shape: random, 12 trials, parallel 3, cold batch/v1 Job processes, MLP lr / "
+            "config": "B1 shape: random, 12 trials, parallel 3, cold batch/v1 Job processes (forked from the "
+                      "trial fork server unless KATIB_AMD_ZYGOTE=0), MLP lr / "
                       "num-layers / optimizer, batch 64, 3 epochs", "b1_trials_per_hour": 36.3}
 
 

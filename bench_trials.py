@@ -150,12 +150,12 @@ def run_file(args):
                    "trial_kind": e.spec.trial_template.trial_spec.get("kind")}}))
 
 
-PHASES = ["process", "module", "torch", "hip_init", "data", "model", "captured", "first_metric", "trained"]
+PHASES = ["module", "torch", "hip_init", "data", "model", "captured", "first_metric", "trained"]
 
 
 def trial_phases(m, exp_name):
-    """Median cold-trial phase durations (s): launch (scheduler) -> process created -> module
-    import starts -> torch imported -> HIP up -> data on device -> model built -> graph captured ->
+    """Median cold-trial phase durations (s): launch (scheduler) -> the trial module starts
+    importing -> torch imported -> HIP up -> data on device -> model built -> graph captured ->
     first epoch metric -> training done -> reaped (scheduler saw the exit). Trials print
     ``katib-phase`` lines when KATIB_AMD_TRIAL_PHASES=1 (workloads/common.py ``phase``)."""
     import statistics

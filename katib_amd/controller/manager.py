@@ -134,8 +134,9 @@ class Manager:
         self._lock = threading.RLock()
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
-        self._zygote = None  # fork server for cold Python trials (controller/zygote.py), started lazily
+        self._zygote = None  # fork server for cold Python trials (controller/zygote.py)
         self._zygote_failed = False
+        self._zygote_thread: Optional[threading.Thread] = None
         self._t0 = time.time()
         self._completed = 0
         self.fault_injector: Optional[Callable[[str, Key], bool]] = None
@@ -351,6 +352,8 @@ class Manager:
     def shutdown(self):
         self.stop()
         self.runtime.shutdown()
+        if self._zygote_thread is not None:
+            self._zygote_thread.join(timeout=180)
         if self._zygote is not None:
             self._zygote.close()
             self._zygote = None
@@ -929,6 +932,25 @@ class Manager:
         if run.phase == "Launching" and run.worker is None:
             self._mark_running(tkey)
 
+    def start_zygote(self, wait: bool = True) -> bool:
+        """Start the trial fork server now (a daemon does this at start-up; otherwise it starts with
+        the first eligible trial and the trials launched before it is up are exec'd)."""
+        from .zygote import Zygote
+
+        if self._zygote is None and not self._zygote_failed and self._zygote_thread is None:
+            def start():
+                try:
+                    self._zygote = Zygote(self.state_dir)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("fork server unavailable (%s): trials are exec'd", e)
+                    self._zygote_failed = True
+
+            self._zygote_thread = threading.Thread(target=start, name="katib-zygote", daemon=True)
+            self._zygote_thread.start()
+        if wait and self._zygote_thread is not None:
+            self._zygote_thread.join(timeout=180)
+        return self._zygote is not None
+
     def _zygote_spawn(self, proc_name, argv, env, cwd, log_path, cfg, deadline) -> int:
         """Start a cold Python trial from the fork server (controller/zygote.py) and hand it to the
         native runtime (``TrialRuntime.adopt``); -1: not eligible or the server is unavailable,
@@ -940,12 +962,20 @@ class Manager:
                 or not Zygote.eligible(argv):
             return -1
         if self._zygote is None or not self._zygote.alive():
-            try:
-                self._zygote = Zygote(self.state_dir)
-            except Exception as e:  # noqa: BLE001 - the exec path always works
-                log.warning("fork server unavailable (%s): trials are exec'd", e)
-                self._zygote_failed = True
-                return -1
+            # start the server in the background (import torch + torch.optim: ~3 s) and exec the
+            # trials launched meanwhile instead of making them wait for it
+            self._zygote = None
+            if self._zygote_thread is None or not self._zygote_thread.is_alive():
+                def start():
+                    try:
+                        self._zygote = Zygote(self.state_dir)
+                    except Exception as e:  # noqa: BLE001 - the exec path always works
+                        log.warning("fork server unavailable (%s): trials are exec'd", e)
+                        self._zygote_failed = True
+
+                self._zygote_thread = threading.Thread(target=start, name="katib-zygote", daemon=True)
+                self._zygote_thread.start()
+            return -1
         full = dict(os.environ)
         full.update(env)
         r, w = os.pipe()

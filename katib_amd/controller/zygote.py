@@ -111,6 +111,12 @@ def _run_child(req: Dict, out_fd: int, keep_parent: int) -> None:
             code = 1
     finally:
         try:
+            import atexit
+
+            atexit._run_exitfuncs()  # what interpreter exit would run (trial code's own handlers)
+        except Exception:  # noqa: BLE001
+            pass
+        try:
             sys.stdout.flush()
             sys.stderr.flush()
         except Exception:  # noqa: BLE001
@@ -138,7 +144,6 @@ def _handle(conn: socket.socket, listener: socket.socket) -> None:
     sys.stdout.flush()
     sys.stderr.flush()
     r, w = os.pipe()
-    me = os.getpid()
     pid1 = os.fork()
     if pid1 == 0:  # intermediate: fork the trial and exit, so the trial is re-parented to the subreaper
         try:
@@ -153,7 +158,6 @@ def _handle(conn: socket.socket, listener: socket.socket) -> None:
             os.write(w, struct.pack("i", pid2))
         finally:
             os._exit(0)
-    del me
     os.close(w)
     os.close(out_fd)
     os.waitpid(pid1, 0)
@@ -176,6 +180,17 @@ def serve(path: str, preload: List[str]) -> int:
             loaded.append(mod)
         except Exception as e:  # noqa: BLE001 - a missing preload only costs the child its import
             print("zygote: preload %s failed: %s" % (mod, e), file=sys.stderr, flush=True)
+    if "torch" in sys.modules:
+        # torch.optim's first optimizer construction imports torch._dynamo (~1.3 s of pure Python,
+        # measured on MI355X: scripts/trial_model_phase_probe.py): do it here, once, on a CPU
+        # tensor - no kernel runs and no thread pool starts
+        try:
+            import torch
+
+            torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=0.1)
+            loaded.append("torch.optim(+_dynamo)")
+        except Exception as e:  # noqa: BLE001
+            print("zygote: optimizer warm-up failed: %s" % e, file=sys.stderr, flush=True)
     if "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized():
         print("zygote: refusing to serve - the GPU was initialised during preload", file=sys.stderr, flush=True)
         return 3
@@ -191,11 +206,20 @@ def serve(path: str, preload: List[str]) -> int:
     print(json.dumps({"ready": True, "pid": os.getpid(), "preloaded": loaded, "threads": threads,
                       "preload_s": round(time.time() - t0, 3)}), flush=True)
     signal.signal(signal.SIGTERM, lambda *_: (listener.close(), os._exit(0)))
+    # the scheduler may start this server from a helper thread, so the parent-death signal (tied to
+    # the creating THREAD) cannot be used: poll the parent instead and exit once re-parented
+    parent = os.getppid()
+    listener.settimeout(1.0)
     while True:
         try:
             conn, _ = listener.accept()
+        except socket.timeout:
+            if os.getppid() != parent:
+                return 0
+            continue
         except OSError:
             return 0
+        conn.settimeout(None)
         with conn:
             try:
                 _handle(conn, listener)
@@ -224,7 +248,7 @@ class Zygote:
         env["PYTHONPATH"] = os.pathsep.join(p for p in (root, env.get("PYTHONPATH", "")) if p)
         self.proc = subprocess.Popen([sys.executable, "-m", "katib_amd.controller.zygote", "--socket", self.path,
                                       "--preload", preload], stdout=subprocess.PIPE, stdin=subprocess.DEVNULL,
-                                     env=env, text=True, preexec_fn=lambda: _prctl(PR_SET_PDEATHSIG, signal.SIGKILL))
+                                     env=env, text=True)
         line = ""
         t0 = time.time()
         while time.time() - t0 < timeout:

@@ -67,6 +67,7 @@ def test_manager_runs_job_trials_through_zygote(tmp_path):
     e = load_experiment(os.path.join(root, "examples", "hp-tuning", "random-quadratic.yaml"))
     e.spec.max_trial_count, e.spec.parallel_trial_count = 4, 2
     m = Manager(state_dir=str(tmp_path / "s"), num_devices=0, journal=False)
+    assert m.start_zygote(wait=True)
     try:
         m.create_experiment(e)
         done = m.run_until_complete(e.metadata.name, timeout=120)
@@ -95,6 +96,7 @@ def test_zygote_trial_deadline_kill(tmp_path):
                                           "activeDeadlineSeconds": 2,
                                           "template": {"spec": {"containers": [c]}}}}}}}
     m = Manager(state_dir=str(tmp_path / "s"), num_devices=0, journal=False)
+    assert m.start_zygote(wait=True)
     try:
         t0 = time.time()
         m.create_experiment(V1beta1Experiment.from_k8s(exp))
@@ -103,5 +105,26 @@ def test_zygote_trial_deadline_kill(tmp_path):
         t = m.list_trials("zy-deadline")[0]
         assert t.status.conditions[-1].type == "Failed", t.status.conditions[-1]
         assert {r.launcher for r in m.runs.values()} == {"zygote"}
+    finally:
+        m.shutdown()
+
+
+def test_trials_before_the_server_is_up_are_execd(tmp_path):
+    """The fork server starts with the first eligible trial; trials launched while it imports torch
+    are fork+exec'd instead of waiting for it, later ones are forked from it."""
+    from katib_amd.api.conditions import ExperimentConditions as EC
+    from katib_amd.api.yaml_io import load_experiment
+    from katib_amd.controller.manager import Manager
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = load_experiment(os.path.join(root, "examples", "hp-tuning", "random-quadratic.yaml"))
+    e.spec.max_trial_count, e.spec.parallel_trial_count, e.spec.max_failed_trial_count = 2, 1, 1
+    m = Manager(state_dir=str(tmp_path / "s"), num_devices=0, journal=False)
+    try:
+        m.create_experiment(e)
+        done = m.run_until_complete(e.metadata.name, timeout=120)
+        assert EC.is_succeeded(done)
+        first = min(m.runs.values(), key=lambda r: r.started)
+        assert first.launcher == "exec"
     finally:
         m.shutdown()
