@@ -144,6 +144,18 @@ def parse_args(argv):
     return p.parse_args(argv)
 
 
+def _tensors(obj):
+    """Every tensor of a (nested) checkpoint state."""
+    if torch.is_tensor(obj):
+        yield obj
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            yield from _tensors(v)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            yield from _tensors(v)
+
+
 def _ckpt_dir(args):
     return args.checkpoint_dir or os.environ.get("KATIB_TRIAL_CHECKPOINT_DIR", "")
 
@@ -195,8 +207,9 @@ def main(argv=None):
     if st is not None:
         moments = _load_state(model, opt, st, flat)
         start_step = int(st["step"])
+        nbytes = sum(t.numel() * t.element_size() for t in _tensors(st))
         report(checkpoint_source=source, checkpoint_load_seconds=time.time() - t_load,
-               checkpoint_optimizer_state=int(moments))
+               checkpoint_optimizer_state=int(moments), checkpoint_bytes=nbytes)
     B = args.batch_size
     offs = torch.zeros(B, dtype=torch.long, device=dev)
     ar = torch.arange(T + 1, device=dev)
