@@ -201,6 +201,10 @@ class DartsSearch:
             grads.append(g)
         return leaves, grads
 
+    @staticmethod
+    def _fixed(leaves):
+        return [a.detach() for a in leaves]
+
     def _arch(self, leaves):
         return leaves[0], (leaves[1] if len(leaves) > 1 else [])
 
@@ -223,7 +227,9 @@ class DartsSearch:
         """FWD1/BWD1 -> gW (not yet reduced)."""
         if self.K is None:  # the fused optimizer kernels leave gW zeroed after reading it
             self.gW.zero_()
-        loss, _ = self._loss(tx, ty, self.Pw.views, *self._arch(self.Aw), self.bn)
+        # weight-only pass: detached alphas, so the network Function neither computes nor writes
+        # d(alpha) (backward(inputs=...) does not reach a custom Function's needs_input_grad)
+        loss, _ = self._loss(tx, ty, self.Pw.views, *self._arch(self._fixed(self.Aw)), self.bn)
         self._backward(loss, self.Pw.list)
         self._fold(self.gW_rep)
 
@@ -319,7 +325,7 @@ class DartsSearch:
         if self.K is None:
             self.gW.zero_()  # (the fused virtual step left it zeroed)
             self.gA.zero_()  # (the fused Adam launch already zeroed it)
-        loss, logits = self._loss(tx, ty, self.Pw.views, *self._arch(self.Aw), self.bn)
+        loss, logits = self._loss(tx, ty, self.Pw.views, *self._arch(self._fixed(self.Aw)), self.bn)
         self._backward(loss, self.Pw.list)
         self._fold(self.gW_rep)
         if self.hd is not None:

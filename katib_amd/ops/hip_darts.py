@@ -258,6 +258,11 @@ def arena_end():
 def zeros64(n: int, device) -> torch.Tensor:
     a = _ARENA
     if a.active:
+        if a.pending_zero and a.buf is not None:
+            # the deferred zeroing was meant for the step's network_loss launch, but a slice is
+            # handed out first (a per-cell fallback step): zero the arena now, never hand out stale sums
+            a.buf.zero_()
+            a.pending_zero = False
         step = (n + 31) // 32 * 32  # 256-byte aligned slices
         a.used += step
         if a.buf is not None and a.off + step <= a.buf.numel() and a.buf.device == device:
