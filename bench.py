@@ -68,6 +68,9 @@ def main():
     ap.add_argument("--b1", type=int, default=1,
                     help="also run the B1-shaped experiment (examples/hp-tuning/b1-random-mnist-mlp.yaml: random "
                          "search, 12 cold batch/v1 Job trials, 3 in parallel) -> b1_trials_per_hour")
+    ap.add_argument("--experiment", type=int, default=1,
+                    help="also run examples/nas/darts-cifar10.yaml through the scheduler, Experiment create -> "
+                         "Succeeded (the span the reference's 282 s measures) -> b5_experiment_wall_s")
     ap.add_argument("--capture", type=int, default=1)
     ap.add_argument("--ops", default=os.environ.get("KATIB_AMD_DARTS_OPS", "hip"))
     ap.add_argument("--valid-batches", type=int, default=10)
@@ -104,11 +107,13 @@ def main():
 
     # trials/hour (BASELINE config 2) first, from rank 0, before this process touches the GPU:
     # the scheduler's warm workers then own every GPU while the experiment runs
-    tph = b1 = None
+    tph = b1 = b5x = None
     if args.trials > 0 and int(os.environ.get("RANK", "0")) == 0:
         tph = trials_per_hour(args.gpus, args.trials, args.trial_slots)
     if args.b1 and int(os.environ.get("RANK", "0")) == 0:
         b1 = b1_trials_per_hour(args.gpus)
+    if args.experiment and int(os.environ.get("RANK", "0")) == 0 and args.config == "b5":
+        b5x = b5_experiment()
 
     import torch
 
@@ -320,6 +325,9 @@ def main():
             "speedup_vs_module_eager": round(comp["module_eager"] / ms_step, 2) if comp["module_eager"] else None,
             "trials_per_hour": tph,
             "b1_trials_per_hour": b1,
+            # the reference's B5 span end to end on 1 GPU: the DARTS Experiment through the scheduler
+            "b5_experiment_wall_s": b5x.get("wall_s") if b5x else None,
+            "b5_experiment": b5x,
         }
         print(json.dumps(out), flush=True)
     comm.destroy()
@@ -345,6 +353,26 @@ def self_launch(n: int) -> int:
         return r.returncode or 1
     print(lines[0], flush=True)
     return 0
+
+
+def b5_experiment():
+    """examples/nas/darts-cifar10.yaml (the B5 config) through the in-process scheduler, Experiment
+    create -> Succeeded, in a child process before this one touches the GPU (scripts/experiments_r05.py)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    cmd = [sys.executable, os.path.join(here, "scripts", "experiments_r05.py"), "--only", "darts-b5", "--slots", "1"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not line:
+            print("B5 experiment failed: %s" % (r.stderr[-2000:],), file=sys.stderr)
+            return None
+        res = json.loads(line[-1])
+    except (subprocess.TimeoutExpired, ValueError) as e:
+        print("B5 experiment failed: %s" % e, file=sys.stderr)
+        return None
+    return {"wall_s": res["wall_s"], "condition": res["condition"], "baseline_b5_s": B5_SECONDS,
+            "vs_b5": round(res["wall_s"] / B5_SECONDS, 4), "trial_s": res.get("median_trial_s"),
+            "span": "Experiment create -> Succeeded (reference nas-with-darts.ipynb:487,727-740)"}
 
 
 def b1_trials_per_hour(gpus: int):

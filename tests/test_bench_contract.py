@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-BENCH_ARGS = ["--steps", "2", "--warmup", "1", "--trials", "0", "--b1", "0", "--comparator-steps", "0", "--full-search", "0",
+BENCH_ARGS = ["--steps", "2", "--warmup", "1", "--trials", "0", "--b1", "0", "--experiment", "0", "--comparator-steps", "0", "--full-search", "0",
               "--valid-batches", "2"]
 
 
