@@ -16,7 +16,7 @@ void plan(int P, int C, int* R, int* rows, int* cvb);
 // rmean != nullptr, ss = [scale; shift] (2C), y = relu?(x * scale + shift + res?).
 hipError_t fwd_train(const bf16* x, const bf16* res, bf16* y, const float* gamma, const float* beta, float* rmean,
                      float* rvar, float* mean, float* invstd, float* ss, float* part, int P, int C, float eps,
-                     float momentum, int relu, hipStream_t st);
+                     float momentum, int relu, hipStream_t st, long long* counter = nullptr);
 // Inference forward with the running statistics.
 hipError_t fwd_eval(const bf16* x, const bf16* res, bf16* y, const float* gamma, const float* beta,
                     const float* rmean, const float* rvar, float* ss, int P, int C, float eps, int relu,

@@ -135,9 +135,12 @@ __global__ __launch_bounds__(256) void fwd_finalize_k(const float* __restrict__ 
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float eps, float momentum, float* __restrict__ rmean,
                                                       float* __restrict__ rvar, float* __restrict__ mean,
-                                                      float* __restrict__ invstd, float* __restrict__ ss) {
+                                                      float* __restrict__ invstd, float* __restrict__ ss,
+                                                      long long* __restrict__ counter) {
   __shared__ float red[2][4][64];
   float s, q;
+  // nn.BatchNorm2d's num_batches_tracked += 1, folded in here instead of its own framework launch
+  if (counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
   sum_parts(part, R, C, s, q, red);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if (threadIdx.x >= 64 || c >= C) return;
@@ -259,14 +262,14 @@ void plan(int P, int C, int* R, int* rows, int* cvb) {
 
 hipError_t fwd_train(const bf16* x, const bf16* res, bf16* y, const float* gamma, const float* beta, float* rmean,
                      float* rvar, float* mean, float* invstd, float* ss, float* part, int P, int C, float eps,
-                     float momentum, int relu, hipStream_t st) {
+                     float momentum, int relu, hipStream_t st, long long* counter) {
   int R, rows, cvb;
   plan(P, C, &R, &rows, &cvb);
   const u16* xx = reinterpret_cast<const u16*>(x);
   hipLaunchKernelGGL(stats_k<0>, dim3((C / 8 + cvb - 1) / cvb, R), dim3(256), 0, st, xx, nullptr, nullptr, nullptr,
                      nullptr, P, C, rows, cvb, part);
   hipLaunchKernelGGL(fwd_finalize_k, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, P, gamma, beta, eps,
-                     momentum, rmean, rvar, mean, invstd, ss);
+                     momentum, rmean, rvar, mean, invstd, ss, counter);
   const int64_t n8 = (int64_t)P * C / 8;
   hipLaunchKernelGGL(apply_k, dim3(ew_grid(n8)), dim3(256), 0, st, xx, reinterpret_cast<const u16*>(res),
                      reinterpret_cast<u16*>(y), ss, n8, C, relu);

@@ -35,7 +35,8 @@ void ok(hipError_t e, const char* w) { TORCH_CHECK(e == hipSuccess, w, ": ", hip
 
 void bn_fwd_train(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& y, const Tensor& gamma,
                   const Tensor& beta, const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
-                  const Tensor& mean, const Tensor& invstd, double eps, double momentum, bool relu) {
+                  const Tensor& mean, const Tensor& invstd, double eps, double momentum, bool relu,
+                  const c10::optional<Tensor>& num_batches) {
   int64_t P, C;
   dims(x, P, C);
   chk_act(x, P, C, "x");
@@ -58,7 +59,8 @@ void bn_fwd_train(const Tensor& x, const c10::optional<Tensor>& res, const Tenso
                    rmean.has_value() ? rmean->data_ptr<float>() : nullptr,
                    rvar.has_value() ? rvar->data_ptr<float>() : nullptr, mean.data_ptr<float>(),
                    invstd.data_ptr<float>(), ss.data_ptr<float>(), part.data_ptr<float>(), (int)P, (int)C, (float)eps,
-                   (float)momentum, relu ? 1 : 0, stream()),
+                   (float)momentum, relu ? 1 : 0, stream(),
+                   num_batches.has_value() ? reinterpret_cast<long long*>(num_batches->data_ptr<int64_t>()) : nullptr),
      "bn_fwd_train");
 }
 
@@ -119,7 +121,10 @@ void channel_sum(const Tensor& x, const Tensor& out) {
 
 void register_batchnorm(py::module& m) {
   m.def("channel_sum", &channel_sum, "per-channel sum of a [P, C] bf16 activation (bias gradients), graph-safe");
-  m.def("bn_fwd_train", &bn_fwd_train, "NHWC bf16 batch norm (+residual, +ReLU), training statistics");
+  m.def("bn_fwd_train", &bn_fwd_train, "NHWC bf16 batch norm (+residual, +ReLU), training statistics",
+        py::arg("x"), py::arg("res"), py::arg("y"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"),
+        py::arg("rvar"), py::arg("mean"), py::arg("invstd"), py::arg("eps"), py::arg("momentum"), py::arg("relu"),
+        py::arg("num_batches") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval, "NHWC bf16 batch norm (+residual, +ReLU) with running statistics");
   m.def("bn_bwd", &bn_bwd, "NHWC bf16 batch norm backward (ReLU mask from the output, residual gradient)");
 }

@@ -47,7 +47,7 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
 
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, rmean, rvar, training, momentum, eps, relu):
+    def forward(ctx, x, res, weight, bias, rmean, rvar, training, momentum, eps, relu, counter=None):
         k = kernels()
         N, C, H, W = x.shape
         xr = _rows(x)
@@ -58,7 +58,7 @@ class _BNFn(torch.autograd.Function):
         if training:
             mean = torch.empty(C, device=x.device, dtype=torch.float32)
             invstd = torch.empty_like(mean)
-            k.bn_fwd_train(xr, rr, y.view(-1, C), w, b, rmean, rvar, mean, invstd, eps, momentum, relu)
+            k.bn_fwd_train(xr, rr, y.view(-1, C), w, b, rmean, rvar, mean, invstd, eps, momentum, relu, counter)
             ctx.save_for_backward(xr, y if relu else None, w, mean, invstd)
         else:
             k.bn_fwd_eval(xr, rr, y.view(-1, C), w, b, rmean, rvar, eps, relu)
@@ -80,7 +80,7 @@ class _BNFn(torch.autograd.Function):
         k.bn_bwd(gr, None if y is None else y.view(-1, C), xr, w, mean, invstd, dx.view(-1, C),
                  None if dres is None else dres.view(-1, C), dgamma, dbeta)
         return (dx.permute(0, 3, 1, 2), None if dres is None else dres.permute(0, 3, 1, 2), dgamma, dbeta,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -89,11 +89,10 @@ class BatchNorm2d(nn.BatchNorm2d):
     def forward(self, x, residual=None, relu: bool = False):
         if x.is_cuda and self.num_features % 8 == 0 and self.affine and self.track_running_stats:
             training = self.training
-            if training:
-                self.num_batches_tracked.add_(1)
             mom = self.momentum if self.momentum is not None else 0.1
+            # num_batches_tracked is bumped by the finalize kernel (one launch fewer per layer)
             return _BNFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, training,
-                               mom, self.eps, relu)
+                               mom, self.eps, relu, self.num_batches_tracked if training else None)
         y = super().forward(x)
         if residual is not None:
             y = y + residual
