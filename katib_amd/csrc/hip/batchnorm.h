@@ -23,9 +23,10 @@ hipError_t fwd_eval(const bf16* x, const bf16* res, bf16* y, const float* gamma,
                     hipStream_t st);
 // Backward. y (the forward output) masks dy when the forward applied ReLU (nullptr: no ReLU);
 // dres (may be nullptr) receives the masked gradient that flows to the residual input.
+// accumulate: dgamma / dbeta += instead of = (persistent gradient buffers).
 hipError_t bwd(const bf16* dy, const bf16* y, const bf16* x, const float* gamma, const float* mean,
                const float* invstd, bf16* dx, bf16* dres, float* dgamma, float* dbeta, float* coef, float* part, int P,
-               int C, hipStream_t st);
+               int C, hipStream_t st, int accumulate = 0);
 
 // Per-channel sum of a [P, C] bf16 activation into out[C] fp32 (bias gradients): the statistics
 // pass into part (R * 2 * C floats) + one finalize launch; deterministic, no atomics and no

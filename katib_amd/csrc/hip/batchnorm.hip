@@ -202,14 +202,16 @@ __global__ __launch_bounds__(256) void apply_k(const u16* __restrict__ x, const 
 __global__ __launch_bounds__(256) void bwd_finalize_k(const float* __restrict__ part, int R, int C, int P,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                                      float* __restrict__ dbeta, float* __restrict__ coef) {
+                                                      float* __restrict__ dbeta, float* __restrict__ coef,
+                                                      int accumulate) {
   __shared__ float red[2][4][64];
   float sg, sgx;
   sum_parts(part, R, C, sg, sgx, red);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if (threadIdx.x >= 64 || c >= C) return;
-  dgamma[c] = sgx;
-  dbeta[c] = sg;
+  // accumulate: add into persistent gradient buffers (zeroed by the fused optimizer after use)
+  dgamma[c] = accumulate ? dgamma[c] + sgx : sgx;
+  dbeta[c] = accumulate ? dbeta[c] + sg : sg;
   coef[c] = gamma[c] * invstd[c];
   coef[C + c] = sg / P;
   coef[2 * C + c] = sgx / P;
@@ -297,7 +299,7 @@ hipError_t fwd_eval(const bf16* x, const bf16* res, bf16* y, const float* gamma,
 
 hipError_t bwd(const bf16* dy, const bf16* y, const bf16* x, const float* gamma, const float* mean,
                const float* invstd, bf16* dx, bf16* dres, float* dgamma, float* dbeta, float* coef, float* part, int P,
-               int C, hipStream_t st) {
+               int C, hipStream_t st, int accumulate) {
   int R, rows, cvb;
   plan(P, C, &R, &rows, &cvb);
   const u16* d = reinterpret_cast<const u16*>(dy);
@@ -306,7 +308,7 @@ hipError_t bwd(const bf16* dy, const bf16* y, const bf16* x, const float* gamma,
   hipLaunchKernelGGL(stats_k<1>, dim3((C / 8 + cvb - 1) / cvb, R), dim3(256), 0, st, xx, d, yy, mean, invstd, P, C,
                      rows, cvb, part);
   hipLaunchKernelGGL(bwd_finalize_k, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, P, gamma, invstd, dgamma,
-                     dbeta, coef);
+                     dbeta, coef, accumulate);
   const int64_t n8 = (int64_t)P * C / 8;
   hipLaunchKernelGGL(bwd_apply_k, dim3(ew_grid(n8)), dim3(256), 0, st, d, yy, xx, mean, invstd, coef,
                      reinterpret_cast<u16*>(dx), reinterpret_cast<u16*>(dres), n8, C);

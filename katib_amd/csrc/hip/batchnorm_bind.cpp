@@ -83,7 +83,7 @@ void bn_fwd_eval(const Tensor& x, const c10::optional<Tensor>& res, const Tensor
 
 void bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, const Tensor& x, const Tensor& gamma,
             const Tensor& mean, const Tensor& invstd, const Tensor& dx, const c10::optional<Tensor>& dres,
-            const Tensor& dgamma, const Tensor& dbeta) {
+            const Tensor& dgamma, const Tensor& dbeta, bool accumulate) {
   int64_t P, C;
   dims(x, P, C);
   chk_act(dy, P, C, "dy");
@@ -102,7 +102,7 @@ void bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, const Tensor& x, c
   auto coef = at::empty({3 * C}, x.options().dtype(at::kFloat));
   ok(B_::bwd(bp(dy), obp(y), bp(x), gamma.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), bp(dx),
              dres.has_value() ? bp(*dres) : nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-             coef.data_ptr<float>(), part.data_ptr<float>(), (int)P, (int)C, stream()),
+             coef.data_ptr<float>(), part.data_ptr<float>(), (int)P, (int)C, stream(), accumulate ? 1 : 0),
      "bn_bwd");
 }
 
@@ -126,5 +126,7 @@ void register_batchnorm(py::module& m) {
         py::arg("rvar"), py::arg("mean"), py::arg("invstd"), py::arg("eps"), py::arg("momentum"), py::arg("relu"),
         py::arg("num_batches") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval, "NHWC bf16 batch norm (+residual, +ReLU) with running statistics");
-  m.def("bn_bwd", &bn_bwd, "NHWC bf16 batch norm backward (ReLU mask from the output, residual gradient)");
+  m.def("bn_bwd", &bn_bwd, "NHWC bf16 batch norm backward (ReLU mask from the output, residual gradient)",
+        py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("invstd"), py::arg("dx"),
+        py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("accumulate") = false);
 }

@@ -61,15 +61,23 @@ void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& y, const std::vect
   TORCH_CHECK(e == hipSuccess, "conv_fwd launch: ", hipGetErrorString(e));
 }
 
-void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, const std::vector<int64_t>& geom) {
+void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, const std::vector<int64_t>& geom,
+                const c10::optional<Tensor>& add_d, const c10::optional<Tensor>& add_y) {
   const ConvGeom g = make_geom(geom);
   TORCH_CHECK(g.K % 8 == 0, "conv_dgrad: K must be a multiple of 8");
   check_bf16(dy, (int64_t)g.N * g.OH * g.OW * g.K, "dy");
   check_bf16(wt, (int64_t)g.C * g.R * g.S * g.K, "wt");
   check_bf16(dx, (int64_t)g.N * g.H * g.W * g.C, "dx");
+  TORCH_CHECK(add_d.has_value() || !add_y.has_value(), "conv_dgrad: add_y masks add_d");
+  if (add_d.has_value()) check_bf16(*add_d, (int64_t)g.N * g.H * g.W * g.C, "add_d");
+  if (add_y.has_value()) check_bf16(*add_y, (int64_t)g.N * g.H * g.W * g.C, "add_y");
+  auto cp = [](const c10::optional<Tensor>& t) {
+    return t.has_value() ? reinterpret_cast<const __hip_bfloat16*>(t->data_ptr()) : nullptr;
+  };
   auto e = katib_hip::conv::launch_dgrad(g, reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr()),
                                          reinterpret_cast<const __hip_bfloat16*>(wt.data_ptr()),
-                                         reinterpret_cast<__hip_bfloat16*>(dx.data_ptr()), stream());
+                                         reinterpret_cast<__hip_bfloat16*>(dx.data_ptr()), stream(), cp(add_d),
+                                         cp(add_y));
   TORCH_CHECK(e == hipSuccess, "conv_dgrad launch: ", hipGetErrorString(e));
 }
 
@@ -91,6 +99,8 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, const Tensor& dw32, const std
 
 void register_conv(py::module& m) {
   m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16, MFMA)");
-  m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv input gradient");
+  m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv input gradient (+ optional ReLU-masked residual gradient)",
+        py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("geom"), py::arg("add_d") = py::none(),
+        py::arg("add_y") = py::none());
   m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient (fp32 atomics, caller zeroes dw32)");
 }

@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 
+#include <cstdlib>
+
 #include "conv_igemm.h"
 
 namespace katib_hip {
@@ -47,7 +49,9 @@ __device__ inline int xcd_remap(int bid, int nwg) {
 template <int MODE, int BM, int BN>
 __global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16* __restrict__ src,
                                                          const bf16* __restrict__ wmat, bf16* __restrict__ y,
-                                                         float* __restrict__ y32, int M, int N, int Kd) {
+                                                         float* __restrict__ y32, int M, int N, int Kd,
+                                                         const bf16* __restrict__ add_d,
+                                                         const bf16* __restrict__ add_y) {
   constexpr int WM = BM / 2, WN = BN / 2, RM = WM / 16, RN = WN / 16;
   constexpr int LD = kBK + kPad;
   constexpr int AR = BM / 32, BR = BN / 32;  // rows per thread per stage
@@ -179,10 +183,17 @@ __global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16*
       for (int j = 0; j < 4; ++j) {
         const int row = m0 + wr * WM + a * 16 + 4 * (lane >> 4) + j;
         if (row >= M) continue;
-        if (y32)
-          y32[(int64_t)row * N + col] = acc[a][b][j];
-        else
-          y[(int64_t)row * N + col] = __float2bfloat16(acc[a][b][j]);
+        const int64_t o = (int64_t)row * N + col;
+        if (y32) {
+          y32[o] = acc[a][b][j];
+        } else {
+          float v = acc[a][b][j];
+          if (MODE == 1 && add_d != nullptr) {  // residual-branch gradient (ReLU-masked by add_y)
+            const float ad = __bfloat162float(add_d[o]);
+            v += (add_y == nullptr || __bfloat162float(add_y[o]) > 0.f) ? ad : 0.f;
+          }
+          y[o] = __float2bfloat16(v);
+        }
       }
     }
 }
@@ -321,22 +332,23 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(ConvGeom g, const bf16*
 
 template <int MODE, int BM, int BN>
 hipError_t launch_igemm(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, float* y32, int M, int N, int Kd,
-                        hipStream_t st) {
+                        hipStream_t st, const bf16* add_d, const bf16* add_y) {
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN>), dim3(grid), dim3(kThreads), 0, st, g, src, wm, y, y32, M, N, Kd);
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN>), dim3(grid), dim3(kThreads), 0, st, g, src, wm, y, y32, M, N, Kd,
+                     add_d, add_y);
   return hipGetLastError();
 }
 
 template <int MODE>
 hipError_t dispatch(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, float* y32, int M, int N, int Kd,
-                    hipStream_t st) {
+                    hipStream_t st, const bf16* add_d = nullptr, const bf16* add_y = nullptr) {
   const bool wide = N > 64;
   const int tiles128 = ((M + 127) / 128) * ((N + (wide ? 127 : 63)) / (wide ? 128 : 64));
   const bool tall = tiles128 >= 512;  // else halve BM to fill the 256 CUs
-  if (wide) return tall ? launch_igemm<MODE, 128, 128>(g, src, wm, y, y32, M, N, Kd, st)
-                        : launch_igemm<MODE, 64, 128>(g, src, wm, y, y32, M, N, Kd, st);
-  return tall ? launch_igemm<MODE, 128, 64>(g, src, wm, y, y32, M, N, Kd, st)
-              : launch_igemm<MODE, 64, 64>(g, src, wm, y, y32, M, N, Kd, st);
+  if (wide) return tall ? launch_igemm<MODE, 128, 128>(g, src, wm, y, y32, M, N, Kd, st, add_d, add_y)
+                        : launch_igemm<MODE, 64, 128>(g, src, wm, y, y32, M, N, Kd, st, add_d, add_y);
+  return tall ? launch_igemm<MODE, 128, 64>(g, src, wm, y, y32, M, N, Kd, st, add_d, add_y)
+              : launch_igemm<MODE, 64, 64>(g, src, wm, y, y32, M, N, Kd, st, add_d, add_y);
 }
 
 }  // namespace
@@ -345,8 +357,9 @@ hipError_t launch_fwd(const ConvGeom& g, const bf16* x, const bf16* w, bf16* y, 
   return dispatch<0>(g, x, w, y, out_f32, g.N * g.OH * g.OW, g.K, g.R * g.S * g.C, st);
 }
 
-hipError_t launch_dgrad(const ConvGeom& g, const bf16* dy, const bf16* wt, bf16* dx, hipStream_t st) {
-  return dispatch<1>(g, dy, wt, dx, nullptr, g.N * g.H * g.W, g.C, g.R * g.S * g.K, st);
+hipError_t launch_dgrad(const ConvGeom& g, const bf16* dy, const bf16* wt, bf16* dx, hipStream_t st, const bf16* add_d,
+                        const bf16* add_y) {
+  return dispatch<1>(g, dy, wt, dx, nullptr, g.N * g.H * g.W, g.C, g.R * g.S * g.K, st, add_d, add_y);
 }
 
 hipError_t launch_wgrad(const ConvGeom& g, const bf16* x, const bf16* dy, float* dw32, hipStream_t st) {
@@ -354,8 +367,22 @@ hipError_t launch_wgrad(const ConvGeom& g, const bf16* x, const bf16* dy, float*
   const bool wideM = g.K > 64, wideN = Kd > 64;
   const int tiles = ((g.K + (wideM ? 127 : 63)) / (wideM ? 128 : 64)) * ((Kd + (wideN ? 127 : 63)) / (wideN ? 128 : 64));
   constexpr int BP = 64;
-  int splits = (2048 + tiles - 1) / tiles;
-  const int max_splits = (P + 4 * BP - 1) / (4 * BP);  // >= 4 stages per block
+  // Split-K over pixels: every split adds its 128 x 128 fp32 tile into dw32 with atomics, so the
+  // split count trades fill (workgroups) against atomic traffic (tiles x splits x 64 KB).
+  // KATIB_CONV_WGRAD_WG / _MIN_STAGES override the target workgroups / stages per workgroup.
+  // Round-5 sweep on the ResNet-18 shapes (profiles/conv_graph_table_r05.log): 2048 WGs / >= 4
+  // stages (the old policy) 1.64 ms for the nine layers' fwd+bwd, 512 / >= 16: 1.42 ms - the
+  // 128 x 128 tiles of l2-l4 spent most of their time in atomics (l3 wgrad 110 -> 61 us).
+  static const int target_wg = [] {
+    const char* e = getenv("KATIB_CONV_WGRAD_WG");
+    return e ? atoi(e) : 512;
+  }();
+  static const int min_stages = [] {
+    const char* e = getenv("KATIB_CONV_WGRAD_MIN_STAGES");
+    return e ? atoi(e) : 16;
+  }();
+  int splits = (target_wg + tiles - 1) / tiles;
+  const int max_splits = (P + min_stages * BP - 1) / (min_stages * BP);  // >= min_stages stages per block
   splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
   if (splits < 1) splits = 1;
   int chunk = (P + splits - 1) / splits;

@@ -795,6 +795,7 @@ void register_enas(py::module& m);  // enas_bind.cpp
 void register_dwconv(py::module& m);  // dwconv_bind.cpp
 void register_darts_optim(py::module& m);  // darts_optim_bind.cpp
 void register_darts_head(py::module& m);  // darts_head_bind.cpp
+void register_resnet(py::module& m);  // resnet_bind.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, transformer, xGMI all-reduce)";
@@ -838,4 +839,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_stem(m);
   register_darts_optim(m);
   register_darts_head(m);
+  register_resnet(m);
 }

@@ -55,6 +55,10 @@ def parse_args(argv):
     p.add_argument("--max-steps", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
     p.add_argument("--conv", default="hip", choices=["hip", "torch"], help="convolution backend on GPU")
     p.add_argument("--bn", default="hip", choices=["hip", "torch"], help="batch-norm backend on GPU")
+    p.add_argument("--step", default="fused", choices=["fused", "module"],
+                   help="GPU train step: 'fused' = ops/resnet_step.py (every launch a katib_hip kernel: no "
+                        "autograd tape, one multi-tensor SGD launch); 'module' = the nn.Module + autograd + "
+                        "torch.optim path (also used with --conv/--bn torch and on CPU)")
     return p.parse_args(argv)
 
 
@@ -129,6 +133,12 @@ def main(argv=None):
         loss_buf.add_(loss.detach().float())
         return loss_buf
 
+    if cuda and args.step == "fused" and args.conv == "hip" and args.bn == "hip":
+        from ..ops.resnet_step import FusedResNetStep
+
+        model.train()
+        fused = FusedResNetStep(model, tx, ty, idx, loss_buf, args.lr, args.momentum, args.weight_decay, nesterov=True)
+        train_step = fused.step  # noqa: F811 - same contract: static idx in, loss_buf out
     step = CapturedStep(train_step, enabled=bool(args.capture))
     gen = torch.Generator(device=dev).manual_seed(args.seed)
     timer = Timer()
