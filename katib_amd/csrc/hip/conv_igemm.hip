@@ -16,6 +16,11 @@
 // image with 16-B padded rows (conflict-free ds_read_b128 fragment reads) and the
 // 4 waves (2 x 2) run 2 MFMA k-steps per 64-deep stage. Block -> tile order is XCD
 // aware: the tiles that share an im2col row block sit on one XCD (one L2).
+// Strided dgrad (MODE 2): with stride s only the taps r = (ih + ph) mod s (+ s, ...) reach an
+// input row, so 3/4 of a 3x3 / stride-2 reduction would multiply zeros. The input pixels are
+// split into s_h x s_w phase classes (blockIdx.y); each class is its own implicit GEMM over just
+// its taps (1x1, 1x2, 2x1 or 2x2 of the 3x3 filter), reading the [C][R][S][K] filter rows at
+// those taps only.
 // wgrad: the reduction runs over pixels, which are strided in both operands, so the
 // LDS images stay in natural [pixel][channel] layout and the MFMA fragments are read
 // with the gfx950 transposing ds_read_b64_tr_b16.
@@ -64,6 +69,25 @@ __global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16*
   const int m0 = (wg / tilesN) * BM, n0 = (wg % tilesN) * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
   const int kc = tid & 7, trow = tid >> 3;
+  // MODE 2: this workgroup's phase class (py, px), its pixel grid Hc x Wc and its taps
+  int py = 0, px = 0, Hc = 1, Wc = 1, r0 = 0, s0 = 0, Ss = 1;
+  if (MODE == 2) {
+    py = blockIdx.y / g.sw;
+    px = blockIdx.y - py * g.sw;
+    Hc = (g.H - py + g.sh - 1) / g.sh;
+    Wc = (g.W - px + g.sw - 1) / g.sw;
+    M = g.N * Hc * Wc;
+    r0 = (py + g.ph) % g.sh;
+    s0 = (px + g.pw) % g.sw;
+    const int Rr = r0 < g.R ? (g.R - r0 + g.sh - 1) / g.sh : 0;
+    Ss = s0 < g.S ? (g.S - s0 + g.sw - 1) / g.sw : 0;
+    Kd = Rr * Ss * g.K;  // this class's reduction; the filter rows keep their full R*S*K stride
+    if (m0 >= M) return;  // uniform per workgroup: the grid is sized for the largest class
+  }
+  auto class_pix = [&](int m) {  // MODE 2 class row -> input pixel
+    const int hw = Hc * Wc, n = m / hw, rem = m - n * hw, i2 = rem / Wc, j2 = rem - i2 * Wc;
+    return (n * g.H + i2 * g.sh + py) * g.W + j2 * g.sw + px;
+  };
 
   // per-thread gathered rows: image base pixel and the (h, w) origin of the window
   int a_base[AR], a_h[AR], a_w[AR];
@@ -78,20 +102,26 @@ __global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16*
       a_base[i] = n * g.H * g.W;
       a_h[i] = oh * g.sh - g.ph;
       a_w[i] = ow * g.sw - g.pw;
-    } else {
+    } else if (MODE == 1) {
       const int hw = g.H * g.W, n = mm / hw, rem = mm - n * hw, ih = rem / g.W, iw = rem - ih * g.W;
       a_base[i] = n * g.OH * g.OW;
       a_h[i] = ih + g.ph;
       a_w[i] = iw + g.pw;
+    } else {
+      const int hw = Hc * Wc, n = mm / hw, rem = mm - n * hw, i2 = rem / Wc, j2 = rem - i2 * Wc;
+      a_base[i] = n * g.OH * g.OW;
+      a_h[i] = i2 * g.sh + py + g.ph;
+      a_w[i] = j2 * g.sw + px + g.pw;
     }
   }
+  const int64_t wrow = MODE == 2 ? (int64_t)g.R * g.S * g.K : Kd;  // filter row stride
   const bf16* b_row[BR];
   bool b_ok[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
     const int n = n0 + trow + 32 * i;
     b_ok[i] = n < N;
-    b_row[i] = wmat + (int64_t)(b_ok[i] ? n : 0) * Kd;
+    b_row[i] = wmat + (int64_t)(b_ok[i] ? n : 0) * wrow;
   }
 
   u32x4 ra[AR], rb[BR];
@@ -100,12 +130,30 @@ __global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16*
     const int kk = kt * kBK + kc * 8;
     const bool kin = kk < Kd;
     const int CH = MODE == 0 ? g.C : g.K;
-    const int rs = kk / CH, ch = kk - rs * CH, r = rs / g.S, s = rs - r * g.S;
+    const int rs = kk / CH, ch = kk - rs * CH;
+    int r, s;
+    if (MODE == 2) {
+      const int rr = rs / Ss;
+      r = r0 + rr * g.sh;
+      s = s0 + (rs - rr * Ss) * g.sw;
+    } else {
+      r = rs / g.S;
+      s = rs - r * g.S;
+    }
+    const int boff = MODE == 2 ? (r * g.S + s) * g.K + ch : kk;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       u32x4 v = zero;
       if (kin && a_ok[i]) {
-        if (MODE == 0) {
+        if (MODE == 2) {
+          // the class guarantees divisibility; only the image border can cut a tap
+          const int th = a_h[i] - r, tw = a_w[i] - s;
+          if (th >= 0 && tw >= 0) {
+            const int oh = th / g.sh, ow = tw / g.sw;
+            if (oh < g.OH && ow < g.OW)
+              v = *reinterpret_cast<const u32x4*>(src + (int64_t)(a_base[i] + oh * g.OW + ow) * g.K + ch);
+          }
+        } else if (MODE == 0) {
           const int ih = a_h[i] + r * g.dh, iw = a_w[i] + s * g.dw;
           if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
             v = *reinterpret_cast<const u32x4*>(src + (int64_t)(a_base[i] + ih * g.W + iw) * g.C + ch);
@@ -127,7 +175,7 @@ __global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16*
       ra[i] = v;
     }
 #pragma unroll
-    for (int i = 0; i < BR; ++i) rb[i] = (kin && b_ok[i]) ? *reinterpret_cast<const u32x4*>(b_row[i] + kk) : zero;
+    for (int i = 0; i < BR; ++i) rb[i] = (kin && b_ok[i]) ? *reinterpret_cast<const u32x4*>(b_row[i] + boff) : zero;
   };
   auto sstore = [&](int buf) {
 #pragma unroll
@@ -183,12 +231,12 @@ __global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16*
       for (int j = 0; j < 4; ++j) {
         const int row = m0 + wr * WM + a * 16 + 4 * (lane >> 4) + j;
         if (row >= M) continue;
-        const int64_t o = (int64_t)row * N + col;
+        const int64_t o = (int64_t)(MODE == 2 ? class_pix(row) : row) * N + col;
         if (y32) {
           y32[o] = acc[a][b][j];
         } else {
           float v = acc[a][b][j];
-          if (MODE == 1 && add_d != nullptr) {  // residual-branch gradient (ReLU-masked by add_y)
+          if (MODE >= 1 && add_d != nullptr) {  // residual-branch gradient (ReLU-masked by add_y)
             const float ad = __bfloat162float(add_d[o]);
             v += (add_y == nullptr || __bfloat162float(add_y[o]) > 0.f) ? ad : 0.f;
           }
@@ -334,8 +382,9 @@ template <int MODE, int BM, int BN>
 hipError_t launch_igemm(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, float* y32, int M, int N, int Kd,
                         hipStream_t st, const bf16* add_d, const bf16* add_y) {
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN>), dim3(grid), dim3(kThreads), 0, st, g, src, wm, y, y32, M, N, Kd,
-                     add_d, add_y);
+  const int classes = MODE == 2 ? g.sh * g.sw : 1;  // M is the largest (first) class there
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN>), dim3(grid, classes), dim3(kThreads), 0, st, g, src, wm, y, y32, M,
+                     N, Kd, add_d, add_y);
   return hipGetLastError();
 }
 
@@ -359,6 +408,16 @@ hipError_t launch_fwd(const ConvGeom& g, const bf16* x, const bf16* w, bf16* y, 
 
 hipError_t launch_dgrad(const ConvGeom& g, const bf16* dy, const bf16* wt, bf16* dx, hipStream_t st, const bf16* add_d,
                         const bf16* add_y) {
+  static const bool phase_split = [] {
+    const char* e = getenv("KATIB_CONV_DGRAD_PHASES");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  // 1x1 strided (the shortcut): one class holds every tap, the unit-stride path is as fast (measured)
+  if (phase_split && (g.sh > 1 || g.sw > 1) && g.dh == 1 && g.dw == 1 && g.R * g.S > 1) {
+    const int M0 = g.N * ((g.H + g.sh - 1) / g.sh) * ((g.W + g.sw - 1) / g.sw);  // class (0, 0): the largest
+    const int rs0 = ((g.R + g.sh - 1) / g.sh) * ((g.S + g.sw - 1) / g.sw) * g.K;
+    return dispatch<2>(g, dy, wt, dx, nullptr, M0, g.C, rs0, st, add_d, add_y);
+  }
   return dispatch<1>(g, dy, wt, dx, nullptr, g.N * g.H * g.W, g.C, g.R * g.S * g.K, st, add_d, add_y);
 }
 

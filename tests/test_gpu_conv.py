@@ -97,3 +97,33 @@ def test_same_conv_asymmetric_padding(k, s, size):
     assert _rel(yh, yr) < 1e-2
     assert _rel(xh.grad, xr.grad) < 1e-2
     assert _rel(wh.grad, wr.grad) < 2e-3
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_dgrad_residual_epilogue(stride):
+    """conv_dgrad(add_d, add_y): dx + (add_y > 0 ? add_d : 0) in the GEMM epilogue (the ResNet
+    residual join), on the unit-stride and the phase-split strided paths."""
+    from katib_amd.ops import conv as hc
+
+    k = hc.kernels()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(11)
+    N, C, H, K, R = 4, 32, 16, 64, 3
+    OH = (H + 2 - R) // stride + 1
+    geom = [N, H, H, C, K, R, R, OH, OH, stride, stride, 1, 1, 1, 1]
+    w = (torch.randn(K, R, R, C, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    wt = w.permute(3, 1, 2, 0).contiguous()
+    dy = torch.randn(N, OH, OH, K, device=dev, generator=g).to(torch.bfloat16)
+    add_d = torch.randn(N, H, H, C, device=dev, generator=g).to(torch.bfloat16)
+    add_y = torch.randn(N, H, H, C, device=dev, generator=g).to(torch.bfloat16)
+    dx = torch.empty(N, H, H, C, device=dev, dtype=torch.bfloat16)
+    plain = torch.empty_like(dx)
+    k.conv_dgrad(dy, wt, plain, geom)
+    k.conv_dgrad(dy, wt, dx, geom, add_d, add_y)
+    ref_plain = torch.nn.grad.conv2d_input((N, C, H, H), w.permute(0, 3, 1, 2).float(),
+                                           dy.permute(0, 3, 1, 2).float(), stride=stride, padding=1)
+    assert _rel(plain.permute(0, 3, 1, 2), ref_plain) < 1e-2
+    ref = plain.float() + torch.where(add_y.float() > 0, add_d.float(), torch.zeros_like(add_d.float()))
+    assert _rel(dx, ref) < 1e-2
+    k.conv_dgrad(dy, wt, dx, geom, add_d)
+    assert _rel(dx, plain.float() + add_d.float()) < 1e-2
