@@ -103,6 +103,75 @@ __global__ void own_pass_kernel(float4* b0, float4* b1, int n4, int K, float a, 
   }
 }
 
+// Round 5: a hierarchical per-XCD barrier. Workgroups are dispatched to the
+// 8 XCDs round-robin (XCD = blockIdx.x & 7), so each XCD's workgroups first meet at a counter of
+// their own (one 128-byte line per XCD); the last arrival of an XCD is the only one that touches
+// the global counter, and on release the 8 XCD leaders alone poll the global generation word and
+// forward it to a per-XCD generation word the rest of their XCD polls. Fewer same-address
+// atomics (8 instead of 256 at the global counter) and 8 instead of 256 global pollers.
+struct HierBar {
+  unsigned* xcount;  // [8 x 32]: per-XCD arrival counters, 128 B apart
+  unsigned* xgen;    // [8 x 32]: per-XCD generation words
+  unsigned* count;   // global arrivals (one per XCD)
+  unsigned* gen;     // global generation
+};
+
+__device__ __forceinline__ bool spin_until_changed(unsigned* w, unsigned g, int* err) {
+  long spins = 0;
+  while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1l << 20)) {
+      atomicOr(err, 2);
+      return false;
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ void hier_sync(const HierBar& b, unsigned& mygen, int* err) {
+  __syncthreads();
+  if (threadIdx.x == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+    const unsigned nblk = gridDim.x, xcd = blockIdx.x & 7u;
+    const unsigned in_xcd = nblk / 8 + (xcd < (nblk & 7u) ? 1u : 0u);
+    const unsigned nx = nblk < 8 ? nblk : 8;
+    const unsigned g = mygen;
+    unsigned* xc = b.xcount + xcd * 32;
+    unsigned* xg = b.xgen + xcd * 32;
+    if (__hip_atomic_fetch_add(xc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == in_xcd - 1) {
+      __hip_atomic_store(xc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // XCD leader
+      if (__hip_atomic_fetch_add(b.count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nx - 1) {
+        __hip_atomic_store(b.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(b.gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        spin_until_changed(b.gen, g, err);
+      }
+      __hip_atomic_fetch_add(xg, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      spin_until_changed(xg, g, err);
+    }
+    mygen = g + 1;
+  }
+  __syncthreads();
+}
+
+__global__ void hier_barrier_kernel(int K, HierBar b, int* err) {
+  unsigned mygen = __hip_atomic_load(b.xgen + (blockIdx.x & 7u) * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < K; ++k) hier_sync(b, mygen, err);
+}
+
+__global__ void hier_pass_kernel(float4* b0, float4* b1, int n4, int K, float a, float bb, HierBar b, int* err) {
+  unsigned mygen = __hip_atomic_load(b.xgen + (blockIdx.x & 7u) * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < K; ++k) {
+    const float4* x = (k & 1) ? b1 : b0;
+    float4* y = (k & 1) ? b0 : b1;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+      float4 v = x[i];
+      y[i] = make_float4(a * v.x + bb, a * v.y + bb, a * v.z + bb, a * v.w + bb);
+    }
+    hier_sync(b, mygen, err);
+  }
+}
+
 template <class F>
 static float time_ms(F&& f, hipStream_t st, int reps) {
   for (int i = 0; i < 3; ++i) f();
@@ -147,6 +216,11 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(ctr, 0, sizeof(unsigned)));
   CHECK(hipMemset(gen, 0, sizeof(unsigned)));
   CHECK(hipMemset(err, 0, sizeof(int)));
+  HierBar hb;
+  CHECK(hipMalloc(&hb.xcount, 8 * 32 * sizeof(unsigned)));
+  CHECK(hipMalloc(&hb.xgen, 8 * 32 * sizeof(unsigned)));
+  CHECK(hipMalloc(&hb.count, 64 * sizeof(unsigned)));
+  CHECK(hipMalloc(&hb.gen, 64 * sizeof(unsigned)));
   CHECK(hipMemsetAsync(b0, 0, n * sizeof(float), st));
   CHECK(hipMemsetAsync(b1, 0, n * sizeof(float), st));
 
@@ -199,10 +273,26 @@ int main(int argc, char** argv) {
     }, st, reps);
     std::printf(", \"own_barrier_us_%dwg\": %.3f, \"own_pass_us_%dwg\": %.3f", blocks, ms_own * 1e3f / K, blocks,
                 ms_own_pass * 1e3f / K);
+    // hierarchical per-XCD barrier (all generation words start at 0 and advance together)
+    CHECK(hipMemset(hb.xcount, 0, 8 * 32 * sizeof(unsigned)));
+    CHECK(hipMemset(hb.xgen, 0, 8 * 32 * sizeof(unsigned)));
+    CHECK(hipMemset(hb.count, 0, sizeof(unsigned)));
+    CHECK(hipMemset(hb.gen, 0, sizeof(unsigned)));
+    CHECK(hipDeviceSynchronize());
+    void* hargs[] = {&Kv, &hb, &err};
+    const float ms_hier = time_ms([&] {
+      CHECK(hipLaunchCooperativeKernel((const void*)hier_barrier_kernel, dim3(blocks), dim3(256), hargs, 0, st));
+    }, st, reps);
+    void* hpargs[] = {&b0, &b1, &n4v, &Kv, &a, &bb, &hb, &err};
+    const float ms_hier_pass = time_ms([&] {
+      CHECK(hipLaunchCooperativeKernel((const void*)hier_pass_kernel, dim3(blocks), dim3(256), hpargs, 0, st));
+    }, st, reps);
+    std::printf(", \"hier_xcd_barrier_us_%dwg\": %.3f, \"hier_xcd_pass_us_%dwg\": %.3f", blocks, ms_hier * 1e3f / K,
+                blocks, ms_hier_pass * 1e3f / K);
   }
   int herr = 0;
   CHECK(hipMemcpy(&herr, err, sizeof(int), hipMemcpyDeviceToHost));
-  std::printf(", \"own_barrier_timeouts\": %d", herr);
+  std::printf(", \"own_barrier_timeouts\": %d", herr);  // bit 1: flat barrier, bit 2: hierarchical
   std::printf("}\n");
   CHECK(hipGraphExecDestroy(g_empty));
   CHECK(hipGraphExecDestroy(g_pass));
@@ -212,5 +302,9 @@ int main(int argc, char** argv) {
   CHECK(hipFree(ctr));
   CHECK(hipFree(gen));
   CHECK(hipFree(err));
+  CHECK(hipFree(hb.xcount));
+  CHECK(hipFree(hb.xgen));
+  CHECK(hipFree(hb.count));
+  CHECK(hipFree(hb.gen));
   return 0;
 }
