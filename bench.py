@@ -395,6 +395,7 @@ def b1_trials_per_hour(gpus: int):
     return {"value": res["value"], "unit": "trials/h", "vs_b1": res["vs_baseline"], "wall_s": res["wall_s"],
             "trials_completed": res["trials_completed"], "median_trial_s": res["median_trial_s"],
             "launcher": res.get("launcher"), "trial_phases_s": res.get("trial_phases_s"),
+            "fork_server_start_s": res.get("fork_server_start_s"), "daemon": res.get("daemon"),
             "best_validation_accuracy": res["best_objective"], "n_gpus": gpus,
             "config": "B1 shape: random, 12 trials, parallel 3, cold batch/v1 Job processes (forked from the "
                       "trial fork server unless KATIB_AMD_ZYGOTE=0), MLP lr / "

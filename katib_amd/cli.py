@@ -147,6 +147,8 @@ def cmd_serve(a):
         m.config = KatibConfig.load(a.config)
     restored = m.restore()
     m.start()
+    if m.config.amd.zygote:  # the cold-trial fork server warms up with the daemon, not with the first trial
+        m.start_zygote(wait=False)
     api = ApiServer(m, a.address, a.port, token=token).start()
     grpc_srv = None
     if a.grpc:

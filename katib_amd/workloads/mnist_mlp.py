@@ -57,6 +57,13 @@ def parse_args(argv):
     p.add_argument("--num-layers", type=int, default=0,
                    help="hidden layers of width --hidden (0: the 784-h-h/2-10 net of the fused HIP path)")
     p.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "ftrl"])
+    p.add_argument("--unroll", type=int, default=int(__import__("os").environ.get("KATIB_MLP_UNROLL", "1")),
+                   help="train steps per captured HIP graph replay (the batch index comes from a device-side "
+                        "step counter into the epoch's permutation, so one replay runs that many SGD steps); "
+                        "1 (default) = one replay + one index copy per step. Measured on the B1 trials (3 per "
+                        "GPU): 16 is slower (median trial 3.4-3.7 vs 2.4 s: the larger graph's capture and the "
+                        "counter / gather kernels cost more than the per-step replay launches they remove, "
+                        "profiles/b1_trial_phases_r05.txt)")
     return p.parse_args(argv)
 
 
@@ -205,9 +212,19 @@ def main(argv=None):
     idx = torch.zeros(bs, dtype=torch.long, device=dev)
     loss_buf = torch.zeros((), device=dev)
     correct_buf = torch.zeros((), device=dev)
+    # launch-bound inner loop (batch-64 MLP steps are ~30 tiny kernels): U steps per graph replay, each
+    # taking its batch indices from row `counter` of the epoch's permutation (device-side, no host copy)
+    U = max(1, args.unroll) if (dev.type == "cuda" and args.capture) else 1
+    perm_rows = torch.zeros(max(steps, 1), bs, dtype=torch.long, device=dev)
+    counter = torch.zeros(1, dtype=torch.long, device=dev)
 
     def train_step():
-        xb, yb = tx.index_select(0, idx), ty.index_select(0, idx)
+        if U > 1:
+            idx_ = perm_rows.index_select(0, counter).view(-1)
+            counter.add_(1)
+        else:
+            idx_ = idx
+        xb, yb = tx.index_select(0, idx_), ty.index_select(0, idx_)
         with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=amp):
             logits = model(xb)
             loss = F.cross_entropy(logits, yb)
@@ -218,7 +235,14 @@ def main(argv=None):
         correct_buf.add_((logits.detach().argmax(1) == yb).sum())
         return loss_buf
 
+    def train_chunk():
+        for _ in range(U):
+            out = train_step()
+        return out
+
     step = CapturedStep(train_step, enabled=bool(args.capture))
+    # one eager warm-up chunk (U real steps) creates the optimizer state and the allocator blocks
+    chunk = CapturedStep(train_chunk, enabled=bool(args.capture), warmup=1) if U > 1 else None
     # zero grads exist before capture (set_to_none=False keeps the same buffers)
     for p_ in model.parameters():
         p_.grad = torch.zeros_like(p_)
@@ -237,11 +261,21 @@ def main(argv=None):
         perm = torch.randperm(args.num_train, device=dev, generator=gen)[:steps * bs].view(steps, bs)
         loss_buf.zero_()
         correct_buf.zero_()
-        for s in range(steps):
-            idx.copy_(perm[s])
-            step()
-            if epoch == 0 and s == step.warmup:
-                phase("captured")  # warm-up steps + graph capture + first replay issued
+        if U > 1:
+            perm_rows[:steps].copy_(perm)
+            counter.zero_()
+            for c in range(steps // U):
+                chunk()
+                if epoch == 0 and c == chunk.warmup:
+                    phase("captured")  # warm-up chunks + graph capture + first replay issued
+            for _ in range(steps % U):
+                step()
+        else:
+            for s in range(steps):
+                idx.copy_(perm[s])
+                step()
+                if epoch == 0 and s == step.warmup:
+                    phase("captured")  # warm-up steps + graph capture + first replay issued
         with torch.no_grad(), torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=amp):
             pred = model(vx).argmax(1)
             acc = float((pred == vy).float().mean())
