@@ -523,40 +523,52 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const u16* __restrict__ qkv, u
           s[1][n] = MFMA(kf, qf[1][ks], s[1][n]);
         }
       }
+      // Online softmax in the log2 domain, trimmed for the VALU: the mask only on diagonal tiles (a
+      // wave-uniform branch), the scale folded into one FMA per score, v_exp_f32 directly (exp2f's
+      // denormal range reduction tripled the exp cost; probabilities below 2^-126 are 0 here anyway),
+      // and lazy rescaling: the running max moves only when a tile's max exceeds it by more than
+      // kLazy (probabilities then stay <= 2^kLazy, safe in fp32 / bf16), so after the first tiles the
+      // 32 accumulator rescales of a tile are skipped unless some lane of the wave needs them.
+      constexpr float kLazy = 8.f;
       const bool diag = kv0 + KT - 1 > q0w;
       bf16x8 pb[2][2];
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         const int q = q0w + 16 * r + li;
+        if (diag) {
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (kv0 + 16 * n + 4 * g + j > q) s[r][n][j] = -INFINITY;
+        }
         float mx = -INFINITY;
 #pragma unroll
         for (int n = 0; n < 4; ++n)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float x = s[r][n][j] * c;
-            if (diag && kv0 + 16 * n + 4 * g + j > q) x = -INFINITY;
-            s[r][n][j] = x;
-            mx = fmaxf(mx, x);
-          }
+          for (int j = 0; j < 4; ++j) mx = fmaxf(mx, s[r][n][j]);
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mn = fmaxf(mrow[r], mx);
-        const float alpha = exp2f(mrow[r] - mn);
+        const float mxc = mx * c;  // c > 0: max commutes with the scale
+        const float mn = mxc > mrow[r] + kLazy ? mxc : mrow[r];
+        const float alpha = __builtin_amdgcn_exp2f(mrow[r] - mn);
         mrow[r] = mn;
         float rs = 0.f;
 #pragma unroll
         for (int n = 0; n < 4; ++n)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float p = exp2f(s[r][n][j] - mn);
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r][n][j], c, -mn));
             s[r][n][j] = p;
             rs += p;
           }
         rs += __shfl_xor(rs, 16, 64);
         rs += __shfl_xor(rs, 32, 64);
         lrow[r] = lrow[r] * alpha + rs;
+        if (__builtin_amdgcn_read_exec() & __ballot(alpha != 1.f)) {
 #pragma unroll
-        for (int mm = 0; mm < 4; ++mm) acc[r][mm] *= alpha;
+          for (int mm = 0; mm < 4; ++mm) acc[r][mm] *= alpha;
+        }
         pb[r][0] = pack8(s[r][0], s[r][1]);
         pb[r][1] = pack8(s[r][2], s[r][3]);
       }
@@ -676,7 +688,7 @@ __global__ __launch_bounds__(256) void attn_dq_k(const u16* __restrict__ qkv, co
         for (int n = 0; n < 4; ++n)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float p = exp2f(s[r][n][j] * c - lq[r]);
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r][n][j], c, -lq[r]));  // v_exp_f32, see attn_fwd_k
             if (diag && kv0 + 16 * n + 4 * g + j > q) p = 0.f;
             s[r][n][j] = p * (dp[r][n][j] - dq_[r]);
           }
@@ -810,7 +822,7 @@ __global__ __launch_bounds__(256) void attn_dkdv_k(const u16* __restrict__ qkv, 
           const int key = k0w + 16 * cc + li;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float p = exp2f(s[cc][n][j] * c - lq[j]);
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[cc][n][j], c, -lq[j]));
             if (diag && key > q0t + 16 * n + 4 * g + j) p = 0.f;
             s[cc][n][j] = p;
             dp[cc][n][j] = p * (dp[cc][n][j] - dq[j]);
