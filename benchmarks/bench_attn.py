@@ -34,6 +34,19 @@ def timeit_graph(fn, it=10, reps=5):
     return e0.elapsed_time(e1) / (it * reps)
 
 
+def timeit_eager(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / it
+
+
 def main():
     from katib_amd.ops.transformer import HipOps
 
@@ -48,22 +61,21 @@ def main():
     res = {}
     res["hip_fwd_ms"] = timeit_graph(lambda: ops.attn_fwd(qkv, B, T, H))
     res["hip_bwd_ms"] = timeit_graph(lambda: ops.attn_bwd(qkv, o, dout, lse, B, T, H))
+    print(json.dumps({"shape": [B, T, H, d], **{k_: round(v_, 4) for k_, v_ in res.items()}}), flush=True)
     q, k, v = qkv.view(B, T, 3, H, d).permute(2, 0, 3, 1, 4)
     q, k, v = (t.contiguous().requires_grad_(True) for t in (q, k, v))
     do = dout.view(B, T, H, d).permute(0, 2, 1, 3).contiguous()
-    try:
-        res["sdpa_fwd_ms"] = timeit_graph(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True))
-        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+    # PyTorch SDPA (same node): forward captured; forward + backward timed eagerly (its autograd
+    # backward aborted inside graph capture on this stack), GPU-bound at this size
+    res["sdpa_fwd_ms"] = timeit_graph(lambda: F.scaled_dot_product_attention(q.detach(), k.detach(), v.detach(),
+                                                                             is_causal=True))
 
-        def fb():
-            yy = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-            torch.autograd.grad(yy, (q, k, v), do)
+    def fb():
+        yy = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        torch.autograd.grad(yy, (q, k, v), do)
 
-        res["sdpa_fwdbwd_ms"] = timeit_graph(fb)
-        res["sdpa_bwd_ms"] = res["sdpa_fwdbwd_ms"] - res["sdpa_fwd_ms"]
-        del y
-    except RuntimeError as e:  # no capturable SDPA backend on this stack
-        res["sdpa_error"] = str(e)[:200]
+    res["sdpa_fwdbwd_eager_ms"] = timeit_eager(fb)
+    res["sdpa_bwd_ms"] = res["sdpa_fwdbwd_eager_ms"] - res["sdpa_fwd_ms"]
     out = {"shape": [B, T, H, d]}
     for k_, val in res.items():
         if k_.endswith("_ms"):
