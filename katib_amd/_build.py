@@ -96,10 +96,14 @@ def build_selftest(sanitize: str = "address,undefined", out_dir: str = "", verbo
     return out
 
 
-# Per-translation-unit compiler flags. transformer.hip (flash attention): MFMA accumulators in VGPRs
-# instead of AGPRs - the online softmax reads every score tile, and with AGPR accumulators each tile
-# cost ~190 v_accvgpr moves (attn_fwd_k 1124 -> 911 instructions, 208 -> 160 VGPRs at gfx950).
-HIP_TU_FLAGS = {"transformer.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# Per-translation-unit compiler flags: MFMA accumulators in VGPRs instead of AGPRs where the kernels
+# read or rescale accumulators inside their loops. transformer.hip (flash attention): the online softmax
+# reads every score tile, with AGPR accumulators each tile cost ~190 v_accvgpr moves (attn_fwd_k 1124 ->
+# 911 instructions, 208 -> 160 VGPRs; 293 -> 450 TFLOP/s with the softmax changes, profiles/attention_r05.log).
+# darts_ops_fwd.hip / darts_ops_pwb.hip (DARTS pointwise MFMA): darts-gpu.yaml step 41.86 -> 40.71 ms, B5
+# neutral (profiles/darts_vgpr_form_ab_r05.log).
+_VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+HIP_TU_FLAGS = {"transformer.hip": _VGPR_FORM, "darts_ops_fwd.hip": _VGPR_FORM, "darts_ops_pwb.hip": _VGPR_FORM}
 
 
 def hip_target() -> str:
@@ -107,7 +111,7 @@ def hip_target() -> str:
 
 
 def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", defines=(), out: str = "",
-              build_dir: str = "") -> str:
+              build_dir: str = "", tu_flags=None) -> str:
     """Compile every ``csrc/hip/*.hip`` kernel file + the torch binding into one .so.
     ``defines`` / ``out`` / ``build_dir`` build a tuning variant elsewhere (e.g.
     ``defines=["KATIB_HIP_REP=8"]``), loadable with ``KATIB_AMD_HIPKERN=<path>``."""
@@ -140,7 +144,8 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", 
         objs.append(o)
         if force or _newer(o, [s] + sorted(_local_includes(s, HIP_SRC))):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            cmds.append([hipcc] + common + HIP_TU_FLAGS.get(os.path.basename(s), []) + inc + lang + ["-c", s, "-o", o])
+            extra = (HIP_TU_FLAGS if tu_flags is None else tu_flags).get(os.path.basename(s), [])
+            cmds.append([hipcc] + common + extra + inc + lang + ["-c", s, "-o", o])
     # One hipcc per translation unit, run concurrently (bounded by MAX_JOBS / CPU count).
     jobs = max(1, min(len(cmds) or 1, int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 4), 16))
     pending, running = list(cmds), []
