@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 CFG=${1:-b5}
-ARGS="--steps 2 --warmup 1 --capture 0 --valid-batches 1 --trials 0 --b1 0 --comparator-steps 0 --full-search 0"
+ARGS="--steps 2 --warmup 1 --capture 0 --valid-batches 1 --trials 0 --b1 0 --experiment 0 --comparator-steps 0 --full-search 0"
 [ "$CFG" = default ] && ARGS="$ARGS --config default"
 rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- \
