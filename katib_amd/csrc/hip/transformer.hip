@@ -21,6 +21,7 @@
 //                           MFMA as B operands with no data movement; V (and K, dO, Q in
 //                           the backward) are consumed column-wise through the gfx950
 //                           transposing LDS read ds_read_b64_tr_b16.
+#include <cstdlib>
 #include "transformer.h"
 
 #include <math.h>
@@ -127,38 +128,68 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const u16* __restrict__ dy, cons
     const u32x2 gg = *reinterpret_cast<const u32x2*>(gamma + 256 * i + 4 * lane);
     gv[i] = f32x4{lo2f(gg[0]), hi2f(gg[0]), lo2f(gg[1]), hi2f(gg[1])};
   }
-  for (int row = blockIdx.x * 4 + w; row < M; row += gridDim.x * 4) {
-    const int64_t base = (int64_t)row * D;
-    const float mu = mean[row], rs = rstd[row];
-    f32x4 xh[V], g[V];
-    float s1 = 0.f, s2 = 0.f;
+  // two rows per wave per iteration: both rows' loads issue before either row's reductions (one row
+  // per iteration left each wave with a serial load -> wave_sum -> store chain at one wave per SIMD)
+  constexpr int RR = 2;
+  const int stride = gridDim.x * 4;
+  for (int row0 = blockIdx.x * 4 + w; row0 < M; row0 += RR * stride) {
+    f32x4 xh[RR][V], g[RR][V], rd[RR][V];
+    float s1[RR], s2[RR], mu[RR], rs[RR];
+    bool ok[RR];
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int c = 256 * i + 4 * lane;
-      const f32x4 x = *reinterpret_cast<const f32x4*>(xin + base + c);
-      const u32x2 d2 = *reinterpret_cast<const u32x2*>(dy + base + c);
-      g[i] = f32x4{lo2f(d2[0]), hi2f(d2[0]), lo2f(d2[1]), hi2f(d2[1])};
+    for (int r = 0; r < RR; ++r) {
+      const int row = row0 + r * stride;
+      ok[r] = row < M;
+      const int rw = ok[r] ? row : row0;
+      const int64_t base = (int64_t)rw * D;
+      mu[r] = mean[rw];
+      rs[r] = rstd[rw];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        xh[i][k] = (x[k] - mu) * rs;
-        const float dxh = g[i][k] * gv[i][k];
-        s1 += dxh;
-        s2 += dxh * xh[i][k];
-        ag[i][k] += g[i][k] * xh[i][k];
-        ab[i][k] += g[i][k];
+      for (int i = 0; i < V; ++i) {
+        const int c = 256 * i + 4 * lane;
+        xh[r][i] = *reinterpret_cast<const f32x4*>(xin + base + c);
+        const u32x2 d2 = *reinterpret_cast<const u32x2*>(dy + base + c);
+        g[r][i] = f32x4{lo2f(d2[0]), hi2f(d2[0]), lo2f(d2[1]), hi2f(d2[1])};
+        rd[r][i] = dres ? *reinterpret_cast<const f32x4*>(dres + base + c) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    s1 = wave_sum(s1) * (1.f / D);
-    s2 = wave_sum(s2) * (1.f / D);
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int c = 256 * i + 4 * lane;
-      f32x4 o;
+    for (int r = 0; r < RR; ++r) {
+      s1[r] = 0.f;
+      s2[r] = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = rs * (g[i][k] * gv[i][k] - s1 - xh[i][k] * s2);
-      if (dres) o += *reinterpret_cast<const f32x4*>(dres + base + c);
-      *reinterpret_cast<f32x4*>(dx + base + c) = o;
-      if (dr) *reinterpret_cast<u32x2*>(dr + base + c) = u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+      for (int i = 0; i < V; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xh[r][i][k] = (xh[r][i][k] - mu[r]) * rs[r];
+          const float dxh = g[r][i][k] * gv[i][k];
+          s1[r] += dxh;
+          s2[r] += dxh * xh[r][i][k];
+          if (ok[r]) {
+            ag[i][k] += g[r][i][k] * xh[r][i][k];
+            ab[i][k] += g[r][i][k];
+          }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+      s1[r] = wave_sum(s1[r]) * (1.f / D);
+      s2[r] = wave_sum(s2[r]) * (1.f / D);
+    }
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+      if (!ok[r]) continue;  // wave-uniform
+      const int64_t base = (int64_t)(row0 + r * stride) * D;
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = 256 * i + 4 * lane;
+        f32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = rs[r] * (g[r][i][k] * gv[i][k] - s1[r] - xh[r][i][k] * s2[r]);
+        o += rd[r][i];
+        *reinterpret_cast<f32x4*>(dx + base + c) = o;
+        if (dr) *reinterpret_cast<u32x2*>(dr + base + c) = u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+      }
     }
   }
 #pragma unroll
@@ -893,7 +924,16 @@ hipError_t ln_fwd(const float* x32, const bf16* r, float* xo, const bf16* gamma,
   return hipGetLastError();
 }
 
-int ln_bwd_blocks(int M) { return (M + 3) / 4 < kLnBwdBlocks ? (M + 3) / 4 : kLnBwdBlocks; }
+// (one workgroup per CU: the partial rows stay few for ln_reduce_k; each wave keeps two rows in flight,
+// see ln_bwd_k). KATIB_LN_BWD_BLOCKS overrides (A/B).
+int ln_bwd_blocks(int M) {
+  static const int cap = [] {
+    const char* e = getenv("KATIB_LN_BWD_BLOCKS");
+    const int v = e ? atoi(e) : kLnBwdBlocks;
+    return v > 0 ? v : kLnBwdBlocks;
+  }();
+  return (M + 3) / 4 < cap ? (M + 3) / 4 : cap;
+}
 
 hipError_t ln_bwd(const bf16* dy, const float* xin, const float* mean, const float* rstd, const bf16* gamma,
                   const float* dres, float* dx, bf16* dr, float* part_g, float* part_b, int M, int D,
