@@ -20,9 +20,11 @@ hipError_t ln_fwd(const float* x32, const bf16* r, float* xo, const bf16* gamma,
 int ln_bwd_blocks(int M);
 hipError_t ln_bwd(const bf16* dy, const float* xin, const float* mean, const float* rstd, const bf16* gamma,
                   const float* dres, float* dx, bf16* dr, float* part_g, float* part_b, int M, int D,
-                  hipStream_t st);
+                  hipStream_t st, float* part_r = nullptr);
+// part_r / dbias (optional): column sums of the bf16 dr output -> the bias gradient of the linear
+// layer whose output gradient dr is.
 hipError_t ln_reduce_params(const float* part_g, const float* part_b, int nblk, int D, bf16* dgamma, bf16* dbeta,
-                            hipStream_t st);
+                            hipStream_t st, const float* part_r = nullptr, bf16* dbias = nullptr);
 
 // tanh-approximate GELU on bf16 (n % 8 == 0).
 hipError_t gelu_fwd(const bf16* u, bf16* g, int64_t n, hipStream_t st);

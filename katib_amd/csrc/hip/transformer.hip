@@ -116,15 +116,18 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const u16* __restrict__ dy, cons
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
                                                 const u16* __restrict__ gamma, const float* dres, float* dx,
                                                 u16* __restrict__ dr, float* __restrict__ part_g,
-                                                float* __restrict__ part_b, int M) {
+                                                float* __restrict__ part_b, float* __restrict__ part_r, int M) {
   constexpr int D = 256 * V;
   __shared__ float red[2][4][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  f32x4 ag[V], ab[V], gv[V];
+  // part_r != nullptr: also the column sums of the bf16 gradient written to dr - the bias gradient
+  // of the linear layer whose output dr is (GPT-2: attn proj / fc2), so no separate column-sum pass
+  f32x4 ag[V], ab[V], ar[V], gv[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     ag[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     ab[i] = ag[i];
+    ar[i] = ag[i];
     const u32x2 gg = *reinterpret_cast<const u32x2*>(gamma + 256 * i + 4 * lane);
     gv[i] = f32x4{lo2f(gg[0]), hi2f(gg[0]), lo2f(gg[1]), hi2f(gg[1])};
   }
@@ -188,7 +191,11 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const u16* __restrict__ dy, cons
         for (int k = 0; k < 4; ++k) o[k] = rs[r] * (g[r][i][k] * gv[i][k] - s1[r] - xh[r][i][k] * s2[r]);
         o += rd[r][i];
         *reinterpret_cast<f32x4*>(dx + base + c) = o;
-        if (dr) *reinterpret_cast<u32x2*>(dr + base + c) = u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+        if (dr) {
+          const u32x2 ob = u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+          *reinterpret_cast<u32x2*>(dr + base + c) = ob;
+          if (part_r) ar[i] += f32x4{lo2f(ob[0]), hi2f(ob[0]), lo2f(ob[1]), hi2f(ob[1])};  // what colsum(dr) sums
+        }
       }
     }
   }
@@ -202,27 +209,53 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const u16* __restrict__ dy, cons
     part_g[(int64_t)blockIdx.x * D + c] = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
     part_b[(int64_t)blockIdx.x * D + c] = (red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c]);
   }
+  if (part_r == nullptr) return;  // uniform
+  __syncthreads();  // red[0] is reused (a third [4][D] array would pass the 64 KB static LDS limit at D = 2048)
+#pragma unroll
+  for (int i = 0; i < V; ++i) *reinterpret_cast<f32x4*>(&red[0][w][256 * i + 4 * lane]) = ar[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256)
+    part_r[(int64_t)blockIdx.x * D + c] = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
 }
 
 // sum nblk partial rows per column: block = 64 columns x 4 row groups
-__global__ __launch_bounds__(256) void ln_reduce_k(const float* __restrict__ pg, const float* __restrict__ pb,
-                                                   int nblk, int D, u16* __restrict__ dg, u16* __restrict__ db) {
-  __shared__ float red[2][4][64];
+// block = 64 columns x 16 row groups (1024 threads): only D / 64 workgroups exist, so each needs
+// many loads in flight; the optional third array (bias gradient) is read in the same loop
+constexpr int kLnRedGroups = 16;
+__global__ __launch_bounds__(64 * kLnRedGroups) void ln_reduce_k(const float* __restrict__ pg,
+                                                                 const float* __restrict__ pb,
+                                                                 const float* __restrict__ pr, int nblk, int D,
+                                                                 u16* __restrict__ dg, u16* __restrict__ db,
+                                                                 u16* __restrict__ dbias) {
+  __shared__ float red[3][kLnRedGroups][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6, c = blockIdx.x * 64 + tx;
-  float sg = 0.f, sb = 0.f;
+  float sg = 0.f, sb = 0.f, sr = 0.f;
   if (c < D) {
-#pragma unroll 8
-    for (int r = ty; r < nblk; r += 4) {
-      sg += pg[(int64_t)r * D + c];
-      sb += pb[(int64_t)r * D + c];
+    if (pr) {
+#pragma unroll 4
+      for (int r = ty; r < nblk; r += kLnRedGroups) {
+        sg += pg[(int64_t)r * D + c];
+        sb += pb[(int64_t)r * D + c];
+        sr += pr[(int64_t)r * D + c];
+      }
+    } else {
+#pragma unroll 4
+      for (int r = ty; r < nblk; r += kLnRedGroups) {
+        sg += pg[(int64_t)r * D + c];
+        sb += pb[(int64_t)r * D + c];
+      }
     }
   }
   red[0][ty][tx] = sg;
   red[1][ty][tx] = sb;
+  red[2][ty][tx] = sr;
   __syncthreads();
-  if (ty == 0 && c < D) {
-    dg[c] = f2bf((red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]));
-    db[c] = f2bf((red[1][0][tx] + red[1][1][tx]) + (red[1][2][tx] + red[1][3][tx]));
+  if (ty < 3 && c < D) {  // one wave per output array, fixed summation order
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLnRedGroups; ++k) t += red[ty][k][tx];
+    u16* out = ty == 0 ? dg : (ty == 1 ? db : dbias);
+    if (out) out[c] = f2bf(t);
   }
 }
 
@@ -937,7 +970,7 @@ int ln_bwd_blocks(int M) {
 
 hipError_t ln_bwd(const bf16* dy, const float* xin, const float* mean, const float* rstd, const bf16* gamma,
                   const float* dres, float* dx, bf16* dr, float* part_g, float* part_b, int M, int D,
-                  hipStream_t st) {
+                  hipStream_t st, float* part_r) {
   const dim3 grid(ln_bwd_blocks(M)), blk(256);
   const u16* d = reinterpret_cast<const u16*>(dy);
   const u16* gg = reinterpret_cast<const u16*>(gamma);
@@ -945,7 +978,8 @@ hipError_t ln_bwd(const bf16* dy, const float* xin, const float* mean, const flo
   switch (D / 256) {
 #define LN_CASE(V) \
   case V:          \
-    hipLaunchKernelGGL(ln_bwd_k<V>, grid, blk, 0, st, d, xin, mean, rstd, gg, dres, dx, rr, part_g, part_b, M); break;
+    hipLaunchKernelGGL(ln_bwd_k<V>, grid, blk, 0, st, d, xin, mean, rstd, gg, dres, dx, rr, part_g, part_b, part_r, M); \
+    break;
     LN_CASE(1) LN_CASE(2) LN_CASE(3) LN_CASE(4) LN_CASE(5) LN_CASE(6) LN_CASE(8)
 #undef LN_CASE
     default: return hipErrorInvalidValue;
@@ -954,9 +988,9 @@ hipError_t ln_bwd(const bf16* dy, const float* xin, const float* mean, const flo
 }
 
 hipError_t ln_reduce_params(const float* part_g, const float* part_b, int nblk, int D, bf16* dgamma, bf16* dbeta,
-                            hipStream_t st) {
-  hipLaunchKernelGGL(ln_reduce_k, dim3((D + 63) / 64), dim3(256), 0, st, part_g, part_b, nblk, D,
-                     reinterpret_cast<u16*>(dgamma), reinterpret_cast<u16*>(dbeta));
+                            hipStream_t st, const float* part_r, bf16* dbias) {
+  hipLaunchKernelGGL(ln_reduce_k, dim3((D + 63) / 64), dim3(64 * kLnRedGroups), 0, st, part_g, part_b, part_r, nblk, D,
+                     reinterpret_cast<u16*>(dgamma), reinterpret_cast<u16*>(dbeta), reinterpret_cast<u16*>(dbias));
   return hipGetLastError();
 }
 

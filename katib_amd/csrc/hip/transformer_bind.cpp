@@ -53,7 +53,7 @@ int64_t ln_bwd_blocks(int64_t M) { return T_::ln_bwd_blocks((int)M); }
 
 void ln_bwd(const Tensor& dy, const Tensor& xin, const Tensor& mean, const Tensor& rstd, const Tensor& gamma,
             const c10::optional<Tensor>& dres, const Tensor& dx, const c10::optional<Tensor>& dr,
-            const Tensor& part_g, const Tensor& part_b) {
+            const Tensor& part_g, const Tensor& part_b, const c10::optional<Tensor>& part_r) {
   TORCH_CHECK(xin.dim() == 2, "xin must be [M, D]");
   const int64_t M = xin.size(0), D = xin.size(1);
   TORCH_CHECK(D % 256 == 0 && D / 256 >= 1 && D / 256 <= 8 && D / 256 != 7, "ln_bwd: D must be 256*{1..6,8}");
@@ -76,13 +76,20 @@ void ln_bwd(const Tensor& dy, const Tensor& xin, const Tensor& mean, const Tenso
     chk(*dr, at::kBFloat16, M * D, "dr");
     drp = bp(*dr);
   }
+  float* prp = nullptr;
+  if (part_r.has_value()) {
+    TORCH_CHECK(drp != nullptr, "ln_bwd: part_r (bias-gradient column sums of dr) needs dr");
+    chk(*part_r, at::kFloat, nb * D, "part_r");
+    prp = part_r->data_ptr<float>();
+  }
   ok(T_::ln_bwd(bp(dy), xin.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), bp(gamma), dresp,
                 dx.data_ptr<float>(), drp, part_g.data_ptr<float>(), part_b.data_ptr<float>(), (int)M, (int)D,
-                stream()),
+                stream(), prp),
      "ln_bwd");
 }
 
-void ln_reduce(const Tensor& part_g, const Tensor& part_b, const Tensor& dgamma, const Tensor& dbeta) {
+void ln_reduce(const Tensor& part_g, const Tensor& part_b, const Tensor& dgamma, const Tensor& dbeta,
+               const c10::optional<Tensor>& part_r, const c10::optional<Tensor>& dbias) {
   const int64_t D = dgamma.numel();
   TORCH_CHECK(D > 0 && part_g.numel() % D == 0, "ln_reduce: partials must be [nblk, D]");
   const int64_t nb = part_g.numel() / D;
@@ -90,8 +97,14 @@ void ln_reduce(const Tensor& part_g, const Tensor& part_b, const Tensor& dgamma,
   chk(part_b, at::kFloat, nb * D, "part_b");
   chk(dgamma, at::kBFloat16, D, "dgamma");
   chk(dbeta, at::kBFloat16, D, "dbeta");
+  TORCH_CHECK(part_r.has_value() == dbias.has_value(), "ln_reduce: part_r and dbias go together");
+  if (part_r.has_value()) {
+    chk(*part_r, at::kFloat, nb * D, "part_r");
+    chk(*dbias, at::kBFloat16, D, "dbias");
+  }
   ok(T_::ln_reduce_params(part_g.data_ptr<float>(), part_b.data_ptr<float>(), (int)nb, (int)D, bp(dgamma), bp(dbeta),
-                          stream()),
+                          stream(), part_r.has_value() ? part_r->data_ptr<float>() : nullptr,
+                          dbias.has_value() ? bp(*dbias) : nullptr),
      "ln_reduce");
 }
 
@@ -275,9 +288,13 @@ void register_transformer(py::module& m) {
     return M < (1 << 30) && N < (1 << 30) && K < (1 << 30) && katib_hip::gemm::supported((int)M, (int)N, (int)K);
   });
   m.def("ln_fwd", &ln_fwd, "residual add + LayerNorm forward (fp32 stream, bf16 out)");
-  m.def("ln_bwd", &ln_bwd, "LayerNorm backward (+ residual grad), per-block dgamma/dbeta partials");
+  m.def("ln_bwd", &ln_bwd, "LayerNorm backward (+ residual grad), per-block dgamma/dbeta (+ dr column-sum) partials",
+        py::arg("dy"), py::arg("xin"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("dres"),
+        py::arg("dx"), py::arg("dr"), py::arg("part_g"), py::arg("part_b"), py::arg("part_r") = py::none());
   m.def("ln_bwd_blocks", &ln_bwd_blocks);
-  m.def("ln_reduce", &ln_reduce, "sum LayerNorm parameter-gradient partials into bf16 grads");
+  m.def("ln_reduce", &ln_reduce, "sum LayerNorm parameter-gradient partials into bf16 grads (+ a bias gradient)",
+        py::arg("part_g"), py::arg("part_b"), py::arg("dgamma"), py::arg("dbeta"), py::arg("part_r") = py::none(),
+        py::arg("dbias") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("xent_fwd", &xent_fwd, "vocabulary cross-entropy forward (per-row loss and lse)");

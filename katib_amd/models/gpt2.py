@@ -35,6 +35,10 @@ from typing import Dict, List, Tuple
 import torch
 import torch.nn.functional as F
 
+# attn-proj / fc2 bias gradients summed by the LayerNorm backward that writes their output gradient
+# (KATIB_GPT2_LN_BIAS=0: a separate column-sum pass per bias, as before; A/B switch)
+_LN_BIAS = __import__("os").environ.get("KATIB_GPT2_LN_BIAS", "1") != "0"
+
 from ..utils.tracing import gpu_range
 
 
@@ -212,24 +216,29 @@ class GPT2Flat:
         del dlog, logits
         G = torch.empty((M, d), device=self.device, dtype=torch.float32)  # residual-stream gradient
         dr = torch.empty((M, d), device=self.device, dtype=self.dtype)
+        # each LayerNorm backward also column-sums the dr it writes: the bias gradient of the linear layer
+        # whose output gradient dr is (the top block's fc2 here, proj after ln2, the lower block's fc2 after ln1)
+        lb = _LN_BIAS
         ops.ln_bwd(dh, sf, muf, rsf, self.w["ln_f.weight"], G, dr, g["ln_f.weight"], g["ln_f.bias"],
-                   accumulate=False)
+                   accumulate=False, dbias=g["blocks.%d.fc2.bias" % (c.n_layer - 1)] if lb else None)
         for i in reversed(range(c.n_layer)):
             pre = "blocks.%d." % i
             sa, h1, mu1, rs1, qkv, o, lse, sb, h2, mu2, rs2, u, gl = acts.pop()
             # MLP: dr is the gradient of fc2's output
-            ops.wgrad(dr, gl, g[pre + "fc2.weight"])
-            ops.colsum(dr, g[pre + "fc2.bias"])
+            ops.wgrad(dr, gl, g[pre + "fc2.weight"])  # fc2.bias: summed by the LayerNorm backward that wrote dr
+            if not lb:
+                ops.colsum(dr, g[pre + "fc2.bias"])
             du = ops.gelu_bwd(u, ops.dgrad(dr, self.w[pre + "fc2.weight"]))
             ops.wgrad(du, h2, g[pre + "fc.weight"])
             ops.colsum(du, g[pre + "fc.bias"])
             dh2 = ops.dgrad(du, self.w[pre + "fc.weight"])
             del du
             ops.ln_bwd(dh2, sb, mu2, rs2, self.w[pre + "ln2.weight"], G, dr, g[pre + "ln2.weight"],
-                       g[pre + "ln2.bias"])
+                       g[pre + "ln2.bias"], dbias=g[pre + "proj.bias"] if lb else None)
             # attention: dr is now the gradient of proj's output
             ops.wgrad(dr, o, g[pre + "proj.weight"])
-            ops.colsum(dr, g[pre + "proj.bias"])
+            if not lb:
+                ops.colsum(dr, g[pre + "proj.bias"])
             do = ops.dgrad(dr, self.w[pre + "proj.weight"])
             dqkv = ops.attn_bwd(qkv, o, do, lse, B, T, H, d // H)
             ops.wgrad(dqkv, h1, g[pre + "qkv.weight"])
@@ -237,7 +246,8 @@ class GPT2Flat:
             dh1 = ops.dgrad(dqkv, self.w[pre + "qkv.weight"])
             del dqkv
             ops.ln_bwd(dh1, sa, mu1, rs1, self.w[pre + "ln1.weight"], G, dr if i > 0 else None,
-                       g[pre + "ln1.weight"], g[pre + "ln1.bias"])
+                       g[pre + "ln1.weight"], g[pre + "ln1.bias"],
+                       dbias=g["blocks.%d.fc2.bias" % (i - 1)] if (i > 0 and lb) else None)
         # embeddings: G is the gradient of wte[idx] + wpe[:T]
         Gb = G.to(self.dtype)
         g["wte.weight"].index_add_(0, idx.reshape(-1), Gb)

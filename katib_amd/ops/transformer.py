@@ -60,7 +60,7 @@ class TorchOps:
         y = ((xin - mean[:, None]) * rstd[:, None] * gamma.float() + beta.float()).to(gamma.dtype)
         return xin, y, mean, rstd
 
-    def ln_bwd(self, dy, xin, mean, rstd, gamma, G, dr, dgamma, dbeta, accumulate=True):
+    def ln_bwd(self, dy, xin, mean, rstd, gamma, G, dr, dgamma, dbeta, accumulate=True, dbias=None):
         D = xin.shape[-1]
         g = dy.float()
         xh = (xin - mean[:, None]) * rstd[:, None]
@@ -74,6 +74,8 @@ class TorchOps:
             dr.copy_(G)
         dgamma.copy_((g * xh).sum(0))
         dbeta.copy_(g.sum(0))
+        if dbias is not None and dr is not None:
+            dbias.copy_(dr.float().sum(0))
 
     # ---------------------------------------------------------------- GELU
     def gelu_fwd(self, u):
@@ -207,12 +209,16 @@ class HipOps:
         self.k.ln_fwd(x32, r, None if r is None else xin, gamma, beta, y, mean, rstd, self.eps)
         return xin, y, mean, rstd
 
-    def ln_bwd(self, dy, xin, mean, rstd, gamma, G, dr, dgamma, dbeta, accumulate=True):
+    def ln_bwd(self, dy, xin, mean, rstd, gamma, G, dr, dgamma, dbeta, accumulate=True, dbias=None):
+        """``dbias``: also the bias gradient of the linear layer whose output gradient ``dr`` is
+        (column sums of dr, accumulated by the same kernel instead of a colsum pass)."""
         M, D = xin.shape
         nb = self.k.ln_bwd_blocks(M)
-        part = torch.empty((2, nb, D), device=xin.device, dtype=torch.float32)
-        self.k.ln_bwd(dy, xin, mean, rstd, gamma, G if accumulate else None, G, dr, part[0], part[1])
-        self.k.ln_reduce(part[0], part[1], dgamma, dbeta)
+        want = dbias is not None and dr is not None
+        part = torch.empty((3 if want else 2, nb, D), device=xin.device, dtype=torch.float32)
+        self.k.ln_bwd(dy, xin, mean, rstd, gamma, G if accumulate else None, G, dr, part[0], part[1],
+                      part[2] if want else None)
+        self.k.ln_reduce(part[0], part[1], dgamma, dbeta, part[2] if want else None, dbias if want else None)
 
     def gelu_fwd(self, u):
         g = torch.empty_like(u)
