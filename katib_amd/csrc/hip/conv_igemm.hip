@@ -378,6 +378,141 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(ConvGeom g, const bf16*
     }
 }
 
+
+// ---------------------------------------------------------------- 3x3 / stride 1 / pad 1 from an LDS patch
+// The im2col gather of igemm_kernel re-reads every input pixel for each of the 9 taps (9x the
+// input through L2 per output-channel tile). For the unit-stride 3x3 layers a workgroup instead
+// owns TH full output rows of one image: per 64-channel chunk it stages the (TH + 2) x (W + 2)
+// input patch once (zero border), then walks the 9 taps, staging only that tap's [BN][64] filter
+// slice and reading the MFMA A fragments from the patch at the tap's shifted pixel offsets.
+// FLIP = the input gradient (dgrad of a 3x3 / s1 / p1 conv is the same conv of dy with the
+// filter rotated by 180 degrees: patch offset (2 - r, 2 - s) with the weights of tap (r, s)).
+template <int BN, int TW, bool FLIP>
+__global__ __launch_bounds__(kThreads) void conv3x3_patch_kernel(ConvGeom g, const bf16* __restrict__ src,
+                                                                 const bf16* __restrict__ wmat,
+                                                                 bf16* __restrict__ y, int Cin, int Cout,
+                                                                 const bf16* __restrict__ add_d,
+                                                                 const bf16* __restrict__ add_y) {
+  constexpr int BM = 128, TH = BM / TW, PW = TW + 2, PH = TH + 2, NPIX = PH * PW;
+  constexpr int WM = BM / 2, WN = BN / 2, RM = WM / 16, RN = WN / 16;
+  constexpr int LD = kBK + kPad;
+  extern __shared__ __align__(16) bf16 dsm[];
+  bf16* Ps = dsm;                  // [NPIX][LD]   input patch, one 64-channel chunk
+  bf16* Bs = dsm + NPIX * LD;      // [BN][LD]     one tap's filter slice
+  const int H = g.H;               // == OH (stride 1, pad 1); W == TW
+  const int rows_tiles = H / TH;
+  const int tilesN = Cout / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = wg / tilesN, n0 = (wg % tilesN) * BN;
+  const int img = tm / rows_tiles, oh0 = (tm % rows_tiles) * TH;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int64_t wrow = 9 * (int64_t)Cin;
+  const bf16* srcn = src + (int64_t)img * H * TW * Cin;
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int a = 0; a < RM; ++a)
+#pragma unroll
+    for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fragment pixel -> patch row base (tap (0, 0)); the tap adds (r, s)
+  int prow[RM];
+#pragma unroll
+  for (int a = 0; a < RM; ++a) {
+    const int m = wr * WM + a * 16 + fr, ohl = m / TW, ow = m - ohl * TW;
+    prow[a] = ohl * PW + ow;
+  }
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const int nch = Cin / kBK;
+  for (int cc = 0; cc < nch; ++cc) {
+    // stage the patch: NPIX pixels x 8 chunks of 8 channels
+    for (int i = tid; i < NPIX * 8; i += kThreads) {
+      const int px = i >> 3, ch = (i & 7) * 8, pr = px / PW, pc = px - pr * PW;
+      const int ih = oh0 - 1 + pr, iw = pc - 1;
+      u32x4 v = zero;
+      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)TW)
+        v = *reinterpret_cast<const u32x4*>(srcn + ((int64_t)ih * TW + iw) * Cin + cc * kBK + ch);
+      *reinterpret_cast<u32x4*>(Ps + px * LD + ch) = v;
+    }
+    for (int t = 0; t < 9; ++t) {
+      // this tap's filter slice [BN][64]
+      for (int i = tid; i < BN * 8; i += kThreads) {
+        const int row = i >> 3, ch = (i & 7) * 8;
+        *reinterpret_cast<u32x4*>(Bs + row * LD + ch) =
+            *reinterpret_cast<const u32x4*>(wmat + (int64_t)(n0 + row) * wrow + (int64_t)t * Cin + cc * kBK + ch);
+      }
+      __syncthreads();
+      const int r = t / 3, sx = t - 3 * r;
+      const int off = FLIP ? (2 - r) * PW + (2 - sx) : r * PW + sx;
+#pragma unroll
+      for (int ks = 0; ks < kBK / 32; ++ks) {
+        bf16x8 af[RM], bfg[RN];
+#pragma unroll
+        for (int a = 0; a < RM; ++a)
+          af[a] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Ps + (prow[a] + off) * LD + ks * 32 + fk));
+#pragma unroll
+        for (int b = 0; b < RN; ++b)
+          bfg[b] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Bs + (wc * WN + b * 16 + fr) * LD + ks * 32 + fk));
+#pragma unroll
+        for (int a = 0; a < RM; ++a)
+#pragma unroll
+          for (int b = 0; b < RN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfg[b], acc[a][b], 0, 0, 0);
+      }
+      __syncthreads();  // Bs (and, after the last tap, Ps) are rewritten next
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < RM; ++a)
+#pragma unroll
+    for (int b = 0; b < RN; ++b) {
+      const int col = n0 + wc * WN + b * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = wr * WM + a * 16 + 4 * (lane >> 4) + j, ohl = m / TW, ow = m - ohl * TW;
+        const int64_t o = ((int64_t)(img * H + oh0 + ohl) * TW + ow) * Cout + col;
+        float v = acc[a][b][j];
+        if (add_d != nullptr) {
+          const float ad = __bfloat162float(add_d[o]);
+          v += (add_y == nullptr || __bfloat162float(add_y[o]) > 0.f) ? ad : 0.f;
+        }
+        y[o] = __float2bfloat16(v);
+      }
+    }
+}
+
+template <int BN, int TW, bool FLIP>
+hipError_t launch_patch(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, int Cin, int Cout, hipStream_t st,
+                        const bf16* add_d, const bf16* add_y) {
+  constexpr int TH = 128 / TW, NPIX = (TH + 2) * (TW + 2);
+  const size_t lds = sizeof(bf16) * (size_t)(NPIX + BN) * (kBK + kPad);
+  const int grid = g.N * (g.H / TH) * (Cout / BN);
+  hipLaunchKernelGGL((conv3x3_patch_kernel<BN, TW, FLIP>), dim3(grid), dim3(kThreads), lds, st, g, src, wm, y, Cin, Cout,
+                     add_d, add_y);
+  return hipGetLastError();
+}
+
+// 3x3 / s1 / p1 / d1 with full rows of 16 or 32 pixels, 128-pixel tiles and 64-channel chunks on
+// both sides; anything else keeps the im2col kernel. KATIB_CONV_PATCH=0 turns the path off (A/B).
+bool patch_ok(const ConvGeom& g, int Cin, int Cout) {
+  static const bool on = [] {
+    const char* e = getenv("KATIB_CONV_PATCH");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on && g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 && g.pw == 1 && g.dh == 1 && g.dw == 1 &&
+         g.OH == g.H && g.OW == g.W && (g.W == 16 || g.W == 32) && g.H % (128 / g.W) == 0 && Cin % 64 == 0 &&
+         Cout % 64 == 0;
+}
+
+template <bool FLIP>
+hipError_t dispatch_patch(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, int Cin, int Cout,
+                          hipStream_t st, const bf16* add_d, const bf16* add_y) {
+  const bool wide = Cout % 128 == 0 && (int64_t)g.N * g.H * g.W / 128 * (Cout / 128) >= 512;
+  if (g.W == 32) return wide ? launch_patch<128, 32, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y)
+                             : launch_patch<64, 32, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y);
+  return wide ? launch_patch<128, 16, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y)
+              : launch_patch<64, 16, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y);
+}
+
 template <int MODE, int BM, int BN>
 hipError_t launch_igemm(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, float* y32, int M, int N, int Kd,
                         hipStream_t st, const bf16* add_d, const bf16* add_y) {
@@ -403,6 +538,7 @@ hipError_t dispatch(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y,
 }  // namespace
 
 hipError_t launch_fwd(const ConvGeom& g, const bf16* x, const bf16* w, bf16* y, float* out_f32, hipStream_t st) {
+  if (out_f32 == nullptr && patch_ok(g, g.C, g.K)) return dispatch_patch<false>(g, x, w, y, g.C, g.K, st, nullptr, nullptr);
   return dispatch<0>(g, x, w, y, out_f32, g.N * g.OH * g.OW, g.K, g.R * g.S * g.C, st);
 }
 
@@ -412,6 +548,7 @@ hipError_t launch_dgrad(const ConvGeom& g, const bf16* dy, const bf16* wt, bf16*
     const char* e = getenv("KATIB_CONV_DGRAD_PHASES");
     return e == nullptr || atoi(e) != 0;
   }();
+  if (patch_ok(g, g.K, g.C)) return dispatch_patch<true>(g, dy, wt, dx, g.K, g.C, st, add_d, add_y);
   // 1x1 strided (the shortcut): one class holds every tap, the unit-stride path is as fast (measured)
   if (phase_split && (g.sh > 1 || g.sw > 1) && g.dh == 1 && g.dw == 1 && g.R * g.S > 1) {
     const int M0 = g.N * ((g.H + g.sh - 1) / g.sh) * ((g.W + g.sw - 1) / g.sw);  // class (0, 0): the largest

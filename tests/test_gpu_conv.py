@@ -17,6 +17,8 @@ SHAPES = [
     (2, 24, 15, 15, 40, 7, 7, 2, 3, 1),     # 7x7 stride 2 (ENAS child op)
     (4, 256, 8, 8, 512, 3, 3, 2, 1, 1),
     (8, 512, 4, 4, 512, 3, 3, 1, 1, 1),
+    (2, 128, 16, 16, 128, 3, 3, 1, 1, 1),   # LDS-patch 3x3 path, 16-pixel rows
+    (64, 64, 32, 32, 128, 3, 3, 1, 1, 1),   # LDS-patch path, 128-channel tiles
 ]
 
 
@@ -99,8 +101,8 @@ def test_same_conv_asymmetric_padding(k, s, size):
     assert _rel(wh.grad, wr.grad) < 2e-3
 
 
-@pytest.mark.parametrize("stride", [1, 2])
-def test_dgrad_residual_epilogue(stride):
+@pytest.mark.parametrize("stride,C", [(1, 32), (2, 32), (1, 64)])
+def test_dgrad_residual_epilogue(stride, C):
     """conv_dgrad(add_d, add_y): dx + (add_y > 0 ? add_d : 0) in the GEMM epilogue (the ResNet
     residual join), on the unit-stride and the phase-split strided paths."""
     from katib_amd.ops import conv as hc
@@ -108,7 +110,7 @@ def test_dgrad_residual_epilogue(stride):
     k = hc.kernels()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(11)
-    N, C, H, K, R = 4, 32, 16, 64, 3
+    N, H, K, R = 4, 16, 64, 3  # C = 64 at stride 1: the LDS-patch 3x3 kernel
     OH = (H + 2 - R) // stride + 1
     geom = [N, H, H, C, K, R, R, OH, OH, stride, stride, 1, 1, 1, 1]
     w = (torch.randn(K, R, R, C, device=dev, generator=g) * 0.1).to(torch.bfloat16)
