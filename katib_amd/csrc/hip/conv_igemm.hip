@@ -387,28 +387,30 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(ConvGeom g, const bf16*
 // slice and reading the MFMA A fragments from the patch at the tap's shifted pixel offsets.
 // FLIP = the input gradient (dgrad of a 3x3 / s1 / p1 conv is the same conv of dy with the
 // filter rotated by 180 degrees: patch offset (2 - r, 2 - s) with the weights of tap (r, s)).
-template <int BN, int TW, bool FLIP>
+template <int BN, int TW, int TH, bool FLIP>
 __global__ __launch_bounds__(kThreads) void conv3x3_patch_kernel(ConvGeom g, const bf16* __restrict__ src,
                                                                  const bf16* __restrict__ wmat,
                                                                  bf16* __restrict__ y, int Cin, int Cout,
                                                                  const bf16* __restrict__ add_d,
                                                                  const bf16* __restrict__ add_y) {
-  constexpr int BM = 128, TH = BM / TW, PW = TW + 2, PH = TH + 2, NPIX = PH * PW;
+  // a tile = IPT images x TH output rows x TW (= W) columns = 128 pixels; small planes (8x8, 4x4)
+  // put several whole images in one tile, each with its own zero-bordered patch
+  constexpr int BM = 128, IPT = BM / (TH * TW), PW = TW + 2, PH = TH + 2, NPIX = IPT * PH * PW;
+  static_assert(IPT * TH * TW == BM, "tile must be 128 pixels");
   constexpr int WM = BM / 2, WN = BN / 2, RM = WM / 16, RN = WN / 16;
   constexpr int LD = kBK + kPad;
   extern __shared__ __align__(16) bf16 dsm[];
-  bf16* Ps = dsm;                  // [NPIX][LD]   input patch, one 64-channel chunk
+  bf16* Ps = dsm;                  // [NPIX][LD]   input patch(es), one 64-channel chunk
   bf16* Bs = dsm + NPIX * LD;      // [BN][LD]     one tap's filter slice
   const int H = g.H;               // == OH (stride 1, pad 1); W == TW
-  const int rows_tiles = H / TH;
+  const int rows_tiles = H / TH;   // IPT > 1 only when TH == H (rows_tiles == 1)
   const int tilesN = Cout / BN;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = wg / tilesN, n0 = (wg % tilesN) * BN;
-  const int img = tm / rows_tiles, oh0 = (tm % rows_tiles) * TH;
+  const int img0 = (tm / rows_tiles) * IPT, oh0 = (tm % rows_tiles) * TH;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
   const int fr = lane & 15, fk = 8 * (lane >> 4);
   const int64_t wrow = 9 * (int64_t)Cin;
-  const bf16* srcn = src + (int64_t)img * H * TW * Cin;
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -419,19 +421,21 @@ __global__ __launch_bounds__(kThreads) void conv3x3_patch_kernel(ConvGeom g, con
   int prow[RM];
 #pragma unroll
   for (int a = 0; a < RM; ++a) {
-    const int m = wr * WM + a * 16 + fr, ohl = m / TW, ow = m - ohl * TW;
-    prow[a] = ohl * PW + ow;
+    const int m = wr * WM + a * 16 + fr, im = m / (TH * TW), rem = m - im * (TH * TW), ohl = rem / TW,
+              ow = rem - ohl * TW;
+    prow[a] = im * PH * PW + ohl * PW + ow;
   }
   const u32x4 zero = {0u, 0u, 0u, 0u};
   const int nch = Cin / kBK;
   for (int cc = 0; cc < nch; ++cc) {
-    // stage the patch: NPIX pixels x 8 chunks of 8 channels
+    // stage the patch(es): NPIX pixels x 8 chunks of 8 channels
     for (int i = tid; i < NPIX * 8; i += kThreads) {
-      const int px = i >> 3, ch = (i & 7) * 8, pr = px / PW, pc = px - pr * PW;
+      const int px = i >> 3, ch = (i & 7) * 8, im = px / (PH * PW), q = px - im * (PH * PW), pr = q / PW,
+                pc = q - pr * PW;
       const int ih = oh0 - 1 + pr, iw = pc - 1;
       u32x4 v = zero;
       if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)TW)
-        v = *reinterpret_cast<const u32x4*>(srcn + ((int64_t)ih * TW + iw) * Cin + cc * kBK + ch);
+        v = *reinterpret_cast<const u32x4*>(src + (((int64_t)(img0 + im) * H + ih) * TW + iw) * Cin + cc * kBK + ch);
       *reinterpret_cast<u32x4*>(Ps + px * LD + ch) = v;
     }
     for (int t = 0; t < 9; ++t) {
@@ -468,8 +472,9 @@ __global__ __launch_bounds__(kThreads) void conv3x3_patch_kernel(ConvGeom g, con
       const int col = n0 + wc * WN + b * 16 + fr;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = wr * WM + a * 16 + 4 * (lane >> 4) + j, ohl = m / TW, ow = m - ohl * TW;
-        const int64_t o = ((int64_t)(img * H + oh0 + ohl) * TW + ow) * Cout + col;
+        const int m = wr * WM + a * 16 + 4 * (lane >> 4) + j, im = m / (TH * TW), rem = m - im * (TH * TW),
+                  ohl = rem / TW, ow = rem - ohl * TW;
+        const int64_t o = (((int64_t)(img0 + im) * H + oh0 + ohl) * TW + ow) * Cout + col;
         float v = acc[a][b][j];
         if (add_d != nullptr) {
           const float ad = __bfloat162float(add_d[o]);
@@ -480,37 +485,49 @@ __global__ __launch_bounds__(kThreads) void conv3x3_patch_kernel(ConvGeom g, con
     }
 }
 
-template <int BN, int TW, bool FLIP>
+template <int BN, int TW, int TH, bool FLIP>
 hipError_t launch_patch(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, int Cin, int Cout, hipStream_t st,
                         const bf16* add_d, const bf16* add_y) {
-  constexpr int TH = 128 / TW, NPIX = (TH + 2) * (TW + 2);
+  constexpr int IPT = 128 / (TW * TH), NPIX = IPT * (TH + 2) * (TW + 2);
   const size_t lds = sizeof(bf16) * (size_t)(NPIX + BN) * (kBK + kPad);
-  const int grid = g.N * (g.H / TH) * (Cout / BN);
-  hipLaunchKernelGGL((conv3x3_patch_kernel<BN, TW, FLIP>), dim3(grid), dim3(kThreads), lds, st, g, src, wm, y, Cin, Cout,
-                     add_d, add_y);
+  const int grid = (g.N / IPT) * (g.H / TH) * (Cout / BN);
+  hipLaunchKernelGGL((conv3x3_patch_kernel<BN, TW, TH, FLIP>), dim3(grid), dim3(kThreads), lds, st, g, src, wm, y, Cin,
+                     Cout, add_d, add_y);
   return hipGetLastError();
 }
 
-// 3x3 / s1 / p1 / d1 with full rows of 16 or 32 pixels, 128-pixel tiles and 64-channel chunks on
-// both sides; anything else keeps the im2col kernel. KATIB_CONV_PATCH=0 turns the path off (A/B).
+// 3x3 / s1 / p1 / d1 on 32x32 (4-row tiles), 16x16 (8-row tiles) or 8x8 (2 images per tile) planes
+// with 64-channel chunks on both sides; anything else keeps the im2col kernel. KATIB_CONV_PATCH=0
+// turns the path off (A/B); =1 limits it to the 16 / 32-wide planes; =3 adds 4x4 planes.
 bool patch_ok(const ConvGeom& g, int Cin, int Cout) {
-  static const bool on = [] {
+  static const int mode = [] {
     const char* e = getenv("KATIB_CONV_PATCH");
-    return e == nullptr || atoi(e) != 0;
+    return e == nullptr ? 2 : atoi(e);
   }();
-  return on && g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 && g.pw == 1 && g.dh == 1 && g.dw == 1 &&
-         g.OH == g.H && g.OW == g.W && (g.W == 16 || g.W == 32) && g.H % (128 / g.W) == 0 && Cin % 64 == 0 &&
-         Cout % 64 == 0;
+  if (mode == 0 || !(g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 && g.pw == 1 && g.dh == 1 &&
+                     g.dw == 1 && g.OH == g.H && g.OW == g.W && Cin % 64 == 0 && Cout % 64 == 0))
+    return false;
+  if (g.W == 32 && g.H % 4 == 0) return true;
+  if (g.W == 16 && g.H % 8 == 0) return true;
+  if (mode < 2) return false;
+  if (g.W == 8 && g.H == 8 && g.N % 2 == 0) return true;  // l3: fwd 44.7 -> 38.3, dgrad 48.8 -> 37.1 us
+  // 4x4 planes (8 images per tile) measured slower than the im2col kernel at ResNet-18's l4 (fwd 72 ->
+  // 102 us: 256 workgroups of 9 serial tap stages for 512 channels); opt-in with KATIB_CONV_PATCH=3
+  return mode >= 3 && g.W == 4 && g.H == 4 && g.N % 8 == 0;
 }
 
 template <bool FLIP>
 hipError_t dispatch_patch(const ConvGeom& g, const bf16* src, const bf16* wm, bf16* y, int Cin, int Cout,
                           hipStream_t st, const bf16* add_d, const bf16* add_y) {
   const bool wide = Cout % 128 == 0 && (int64_t)g.N * g.H * g.W / 128 * (Cout / 128) >= 512;
-  if (g.W == 32) return wide ? launch_patch<128, 32, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y)
-                             : launch_patch<64, 32, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y);
-  return wide ? launch_patch<128, 16, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y)
-              : launch_patch<64, 16, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y);
+#define PATCH(TW, TH)                                                                      \
+  return wide ? launch_patch<128, TW, TH, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y) \
+              : launch_patch<64, TW, TH, FLIP>(g, src, wm, y, Cin, Cout, st, add_d, add_y)
+  if (g.W == 32) PATCH(32, 4);
+  if (g.W == 16) PATCH(16, 8);
+  if (g.W == 8) PATCH(8, 8);
+  PATCH(4, 4);
+#undef PATCH
 }
 
 template <int MODE, int BM, int BN>

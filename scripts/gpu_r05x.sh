@@ -10,8 +10,8 @@ L=gpurun_out/r05x.log
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_conv.py >> $L 2>&1 || exit 1
 echo "=== conv table patch on $(date +%T)" >> $L
 timeout -k 10 300 python benchmarks/bench_conv.py --graph >> $L 2>&1 || exit 1
-echo "=== conv table patch off $(date +%T)" >> $L
-KATIB_CONV_PATCH=0 timeout -k 10 120 python benchmarks/bench_conv.py --graph --hip-only >> $L 2>&1 || exit 1
+echo "=== conv table patch 16/32-wide only $(date +%T)" >> $L
+KATIB_CONV_PATCH=1 timeout -k 10 120 python benchmarks/bench_conv.py --graph --hip-only >> $L 2>&1 || exit 1
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_resnet_step.py tests/test_gpu_workloads.py -k "resnet" >> $L 2>&1 || exit 1
 echo "=== resnet run $(date +%T)" >> $L
 timeout -k 10 300 python -m katib_amd.workloads.resnet_cifar --epochs 2 >> $L 2>&1 || exit 1

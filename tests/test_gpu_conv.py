@@ -19,6 +19,7 @@ SHAPES = [
     (8, 512, 4, 4, 512, 3, 3, 1, 1, 1),
     (2, 128, 16, 16, 128, 3, 3, 1, 1, 1),   # LDS-patch 3x3 path, 16-pixel rows
     (64, 64, 32, 32, 128, 3, 3, 1, 1, 1),   # LDS-patch path, 128-channel tiles
+    (4, 64, 8, 8, 128, 3, 3, 1, 1, 1),      # LDS-patch path, 2 images per tile
 ]
 
 
