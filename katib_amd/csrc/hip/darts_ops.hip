@@ -112,11 +112,19 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
     else if (k == kMaxOps) sW[i] = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
   }
   __syncthreads();
-  if (blockIdx.x == 0) {
+  // running-statistic updates spread over the grid's threads (one (edge, op, channel) each), not
+  // looped by block 0: its fp64 moments then delayed that one block's elementwise work - the tail
+  // of every launch
+  {
+    int base = 0;
+    const int gt = blockIdx.x * 256 + threadIdx.x;
     for (int e = 0; e < ne; ++e) {
       const CombineFwdArgs& a = bt.e[e];
       if (!a.update_running) continue;
-      for (int i = threadIdx.x; i < (a.nops + a.nupd) * C; i += 256) {
+      const int n_e = (a.nops + a.nupd) * C, S = gridDim.x * 256;
+      int i0 = (gt - base) % S;  // global entry base + i goes to thread (base + i) mod S
+      if (i0 < 0) i0 += S;
+      for (int i = i0; i < n_e; i += S) {
         int k = i / C, c = i % C;
         const BNRef& b = k < a.nops ? a.bn[k] : a.upd[k - a.nops];
         if (!b.rmean || b.eval) continue;
@@ -127,6 +135,7 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
         b.rmean[c] = (1.f - a.momentum) * b.rmean[c] + a.momentum * (float)m;
         b.rvar[c] = (1.f - a.momentum) * b.rvar[c] + a.momentum * (float)vu;
       }
+      base += n_e;
     }
   }
   if (V4) {
