@@ -36,6 +36,10 @@ hipError_t xent_fwd(const bf16* logits, const int64_t* tgt, float* loss, float* 
 // dlogits = (softmax - onehot) * (*gscale) * inv_n, written in place over logits (pad columns -> 0).
 hipError_t xent_bwd(bf16* logits, const int64_t* tgt, const float* lse, const float* gscale, float inv_n, int N,
                     int V, int Vp, hipStream_t st);
+// Training cross-entropy in one pass: per-row loss and lse, and the gradient written in place over the
+// logits (Vp <= 53248); hipErrorInvalidValue for wider rows (use xent_fwd + xent_bwd).
+hipError_t xent_fused(bf16* logits, const int64_t* tgt, float* loss, float* lse, const float* gscale, float inv_n,
+                      int N, int V, int Vp, hipStream_t st);
 
 // sumsq[0] += sum(g^2) over a flat bf16 gradient (caller zeroes sumsq).
 hipError_t grad_sumsq(const bf16* g, int64_t n, float* sumsq, hipStream_t st);

@@ -396,6 +396,95 @@ __global__ __launch_bounds__(256) void xent_bwd_k(u16* __restrict__ logits, cons
   }
 }
 
+// Forward + backward in one pass over the row (training): the row's 8-bf16 vectors are held in
+// registers between the (max, sum) reduction and the gradient write, so the logits are read from HBM
+// once instead of twice (xent_fwd_k then xent_bwd_k: 1.6 GB read twice per GPT-2 step at 16k tokens).
+template <int NV>  // vectors of 8 bf16 per thread: Vp <= 8 * kXentThreads * NV
+__global__ __launch_bounds__(512, 4) void xent_fused_k(u16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                    float* __restrict__ loss, float* __restrict__ lse,
+                                                    const float* __restrict__ gscale, float inv_n, int V, int Vp) {
+  constexpr int kT = 512, kW = kT / 64;  // 8 waves: ~13 vectors per thread for GPT-2's 50304 columns
+  __shared__ float sh[2 * kW];
+  const int row = blockIdx.x;
+  u16* L = logits + (int64_t)row * Vp;
+  const int nch = Vp >> 3;
+  const int64_t t = tgt[row];
+  const bool tok = t >= 0 && t < V;
+  const float xt = (threadIdx.x == 0 && tok) ? bf2f(L[t]) : 0.f;  // read before any thread overwrites the row
+  u32x4 q[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = threadIdx.x + kT * j;
+    q[j] = c < nch ? reinterpret_cast<const u32x4*>(L)[c] : u32x4{0u, 0u, 0u, 0u};
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = threadIdx.x + kT * j;
+    if (c >= nch) continue;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int col = 8 * c + 2 * k;
+      if (col < V) m = fmaxf(m, lo2f(q[j][k]));
+      if (col + 1 < V) m = fmaxf(m, hi2f(q[j][k]));
+    }
+  }
+  // block max, then the sum of exp2 against it (two reductions; no online rescaling needed)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = sh[0];
+#pragma unroll
+  for (int i = 1; i < kW; ++i) m = fmaxf(m, sh[i]);
+  m *= kLog2e;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = threadIdx.x + kT * j;
+    if (c >= nch) continue;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int col = 8 * c + 2 * k;
+      if (col < V) s += __builtin_amdgcn_exp2f(lo2f(q[j][k]) * kLog2e - m);
+      if (col + 1 < V) s += __builtin_amdgcn_exp2f(hi2f(q[j][k]) * kLog2e - m);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[kW + (threadIdx.x >> 6)] = s;
+  __syncthreads();
+  s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kW; ++i) s += sh[kW + i];
+  const float l2 = m + log2f(s);  // log2-domain lse
+  if (threadIdx.x == 0) {
+    lse[row] = l2 * kLn2;
+    loss[row] = l2 * kLn2 - xt;  // xt = 0 for an out-of-range target, as in xent_fwd_k
+  }
+  const float sc = gscale[0] * inv_n;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = threadIdx.x + kT * j;
+    if (c >= nch) continue;
+    float g[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      g[2 * k] = __builtin_amdgcn_exp2f(lo2f(q[j][k]) * kLog2e - l2);
+      g[2 * k + 1] = __builtin_amdgcn_exp2f(hi2f(q[j][k]) * kLog2e - l2);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int col = 8 * c + e;
+      g[e] = col >= V ? 0.f : (g[e] - (col == t ? 1.f : 0.f)) * sc;
+    }
+    u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = pack2(g[2 * k], g[2 * k + 1]);
+    reinterpret_cast<u32x4*>(L)[c] = o;
+  }
+}
+
 // ============================================================== AdamW
 __global__ __launch_bounds__(256) void sumsq_k(const u16* __restrict__ g, int64_t n8, float* __restrict__ out) {
   __shared__ float sh[4];
@@ -1017,6 +1106,19 @@ hipError_t xent_bwd(bf16* logits, const int64_t* tgt, const float* lse, const fl
                     int V, int Vp, hipStream_t st) {
   hipLaunchKernelGGL(xent_bwd_k, dim3(N), dim3(256), 0, st, reinterpret_cast<u16*>(logits), tgt, lse, gscale, inv_n,
                      V, Vp);
+  return hipGetLastError();
+}
+
+hipError_t xent_fused(bf16* logits, const int64_t* tgt, float* loss, float* lse, const float* gscale, float inv_n,
+                      int N, int V, int Vp, hipStream_t st) {
+  const int nch = Vp / 8;
+  u16* L = reinterpret_cast<u16*>(logits);
+  if (nch <= 512 * 4)
+    hipLaunchKernelGGL(xent_fused_k<4>, dim3(N), dim3(512), 0, st, L, tgt, loss, lse, gscale, inv_n, V, Vp);
+  else if (nch <= 512 * 13)
+    hipLaunchKernelGGL(xent_fused_k<13>, dim3(N), dim3(512), 0, st, L, tgt, loss, lse, gscale, inv_n, V, Vp);
+  else
+    return hipErrorInvalidValue;  // wider vocabularies: the two-pass kernels
   return hipGetLastError();
 }
 

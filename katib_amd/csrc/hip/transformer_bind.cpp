@@ -150,6 +150,23 @@ void xent_bwd(const Tensor& logits, const Tensor& tgt, const Tensor& lse, const 
      "xent_bwd");
 }
 
+bool xent_fused(const Tensor& logits, const Tensor& tgt, const Tensor& loss, const Tensor& lse, const Tensor& gscale,
+                double inv_n, int64_t V) {
+  TORCH_CHECK(logits.dim() == 2, "logits must be [N, Vp]");
+  const int64_t N = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(Vp % 8 == 0 && V > 0 && V <= Vp, "xent: Vp % 8 == 0 and 0 < V <= Vp");
+  chk(logits, at::kBFloat16, N * Vp, "logits");
+  TORCH_CHECK(tgt.is_cuda() && tgt.scalar_type() == at::kLong && tgt.is_contiguous() && tgt.numel() == N, "tgt");
+  chk(loss, at::kFloat, N, "loss");
+  chk(lse, at::kFloat, N, "lse");
+  TORCH_CHECK(gscale.is_cuda() && gscale.scalar_type() == at::kFloat && gscale.numel() == 1, "gscale");
+  if (Vp / 8 > 512 * 13) return false;  // the caller falls back to xent_fwd + xent_bwd
+  ok(T_::xent_fused(bp(logits), tgt.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(),
+                    gscale.data_ptr<float>(), (float)inv_n, (int)N, (int)V, (int)Vp, stream()),
+     "xent_fused");
+  return true;
+}
+
 void grad_sumsq(const Tensor& g, const Tensor& sumsq) {
   TORCH_CHECK(g.numel() % 8 == 0, "grad_sumsq: numel must be a multiple of 8");
   chk(g, at::kBFloat16, g.numel(), "g");
@@ -299,6 +316,9 @@ void register_transformer(py::module& m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("xent_fwd", &xent_fwd, "vocabulary cross-entropy forward (per-row loss and lse)");
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward, in place over the logits");
+  m.def("xent_fused", &xent_fused,
+        "training cross-entropy in one pass over the logits: per-row loss / lse + the gradient in place "
+        "(False: row too wide, use xent_fwd + xent_bwd)");
   m.def("grad_sumsq", &grad_sumsq);
   m.def("adamw", &adamw, "flat AdamW with global-norm clip, writes bf16 shadow weights");
   m.def("reduce_rows", &reduce_rows, "bf16 out = sum of fp32 partial rows (split-K reduction)");

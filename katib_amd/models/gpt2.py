@@ -203,13 +203,13 @@ class GPT2Flat:
         c, ops = self.cfg, self.ops
         acts, sf, hf, muf, rsf = self._saved
         self._saved = None
-        loss_rows, lse_ce = ops.xent_fwd(logits, tgt, self.V)
+        # forward + backward of the cross-entropy in one pass over the logits (the gradient overwrites them)
+        loss_rows, lse_ce, dlog = ops.xent_train(logits, tgt, self.gscale, self.V)
         # mean as a GEMV, not torch.mean: a single-output reduction over B*T rows takes
         # PyTorch's cross-workgroup path, which reads stale staging memory when replayed from a
         # HIP graph on this ROCm stack (katib_amd/utils/graphcheck.py)
         n = loss_rows.numel()
         loss = (loss_rows.view(1, n) @ torch.ones(n, 1, device=loss_rows.device, dtype=loss_rows.dtype)).view(()) / n
-        dlog = ops.xent_bwd(logits, tgt, lse_ce, self.gscale, self.V)
         g = self.g
         torch.mm(dlog.t(), hf, out=g["wte.weight"])  # tied LM head (pad rows get 0)
         dh = torch.mm(dlog, self.w["wte.weight"])

@@ -45,6 +45,9 @@ def _kern():
         raise ImportError("katib_amd._hipkern is not built (run __graft_entry__.build()): %s" % e)
 
 
+# one-pass training cross-entropy (KATIB_XENT_FUSED=0: the two-pass xent_fwd + xent_bwd; A/B switch)
+_XENT_FUSED = os.environ.get("KATIB_XENT_FUSED", "1") != "0"
+
 class TorchOps:
     name = "torch"
 
@@ -122,6 +125,10 @@ class TorchOps:
         logits[:, :V] = (p * (gscale.float() / N)).to(logits.dtype)
         logits[:, V:] = 0
         return logits
+
+    def xent_train(self, logits, tgt, gscale, V):
+        loss, lse = self.xent_fwd(logits, tgt, V)
+        return loss, lse, self.xent_bwd(logits, tgt, lse, gscale, V)
 
     # ---------------------------------------------------------------- GEMM helpers
     def linear(self, x, w, b):
@@ -253,6 +260,17 @@ class HipOps:
     def xent_bwd(self, logits, tgt, lse, gscale, V):
         self.k.xent_bwd(logits, tgt, lse, gscale, 1.0 / logits.shape[0], V)
         return logits
+
+    def xent_train(self, logits, tgt, gscale, V):
+        """(loss_rows, lse, dlogits): forward + backward in one read of the logits (the gradient
+        overwrites them); falls back to the two-pass kernels for rows wider than 53248."""
+        N = logits.shape[0]
+        loss = torch.empty(N, device=logits.device, dtype=torch.float32)
+        lse = torch.empty_like(loss)
+        if not (_XENT_FUSED and self.k.xent_fused(logits, tgt, loss, lse, gscale, 1.0 / N, V)):
+            self.k.xent_fwd(logits, tgt, loss, lse, V)
+            self.k.xent_bwd(logits, tgt, lse, gscale, 1.0 / N, V)
+        return loss, lse, logits
 
     def colsum(self, x, out):
         """Bias gradient: bf16 column sums of [M, N] (two-stage, fp32 partials)."""

@@ -82,6 +82,11 @@ def test_cross_entropy(ops, V, Vp):
     dr = ref.xent_bwd(logits.clone(), tgt, sr, gs, V)
     assert _rel(dh, dr) < 1e-2
     assert V == Vp or float(dh[:, V:].abs().max()) == 0.0
+    # one-pass training form (forward + backward over a single read of the logits)
+    lf, sf, df = hip.xent_train(logits.clone(), tgt, gs, V)
+    assert _rel(lf, lr) < 1e-4 and _rel(sf, sr) < 1e-5
+    assert _rel(df, dr) < 1e-2
+    assert V == Vp or float(df[:, V:].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("B,T,H", [(2, 128, 3), (1, 512, 2), (2, 256, 4)])
