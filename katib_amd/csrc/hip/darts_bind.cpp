@@ -796,6 +796,7 @@ void register_dwconv(py::module& m);  // dwconv_bind.cpp
 void register_darts_optim(py::module& m);  // darts_optim_bind.cpp
 void register_darts_head(py::module& m);  // darts_head_bind.cpp
 void register_resnet(py::module& m);  // resnet_bind.cpp
+void register_lt_epilogue(py::module& m);  // lt_epilogue.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, transformer, xGMI all-reduce)";
@@ -832,6 +833,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_xgmi(m);
   register_conv(m);
   register_transformer(m);
+  register_lt_epilogue(m);
   register_batchnorm(m);
   register_enas(m);
   register_dwconv(m);

@@ -229,8 +229,7 @@ class GPT2Flat:
             if not lb:
                 ops.colsum(dr, g[pre + "fc2.bias"])
             du = ops.gelu_bwd(u, ops.dgrad(dr, self.w[pre + "fc2.weight"]))
-            ops.wgrad(du, h2, g[pre + "fc.weight"])
-            ops.colsum(du, g[pre + "fc.bias"])
+            ops.wgrad_bgrad(du, h2, g[pre + "fc.weight"], g[pre + "fc.bias"])
             dh2 = ops.dgrad(du, self.w[pre + "fc.weight"])
             del du
             ops.ln_bwd(dh2, sb, mu2, rs2, self.w[pre + "ln2.weight"], G, dr, g[pre + "ln2.weight"],
@@ -241,8 +240,7 @@ class GPT2Flat:
                 ops.colsum(dr, g[pre + "proj.bias"])
             do = ops.dgrad(dr, self.w[pre + "proj.weight"])
             dqkv = ops.attn_bwd(qkv, o, do, lse, B, T, H, d // H)
-            ops.wgrad(dqkv, h1, g[pre + "qkv.weight"])
-            ops.colsum(dqkv, g[pre + "qkv.bias"])
+            ops.wgrad_bgrad(dqkv, h1, g[pre + "qkv.weight"], g[pre + "qkv.bias"])
             dh1 = ops.dgrad(dqkv, self.w[pre + "qkv.weight"])
             del dqkv
             ops.ln_bwd(dh1, sa, mu1, rs1, self.w[pre + "ln1.weight"], G, dr if i > 0 else None,

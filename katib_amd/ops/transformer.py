@@ -47,6 +47,11 @@ def _kern():
 
 # one-pass training cross-entropy (KATIB_XENT_FUSED=0: the two-pass xent_fwd + xent_bwd; A/B switch)
 _XENT_FUSED = os.environ.get("KATIB_XENT_FUSED", "1") != "0"
+# hipBLASLt BGRADB epilogue: weight + bias gradient in one GEMM for GPT-2's fc1 / qkv layers
+# (csrc/hip/lt_epilogue.cpp). Opt-in (KATIB_LT_EPILOGUE=1): gfx950's only BGRADB solutions are
+# unsplit 256x128 MI32x32 tiles, 197 / 115 us against 65-72 us for the split-K wgrad + a 14.5 us
+# colsum, 782k -> 743k tokens/s (profiles/lt_epilogue_r05.log).
+_LT_EPILOGUE = os.environ.get("KATIB_LT_EPILOGUE", "0") == "1"
 
 class TorchOps:
     name = "torch"
@@ -143,6 +148,11 @@ class TorchOps:
     def colsum(self, x, out):
         torch.sum(x, 0, out=out)
 
+    def wgrad_bgrad(self, dy, x, dw, db):
+        """dw = dy^T x; db = column sums of dy (a linear layer's weight + bias gradients)."""
+        self.wgrad(dy, x, dw)
+        self.colsum(dy, db)
+
     def dgrad(self, dy, w):
         return torch.mm(dy, w)
 
@@ -198,6 +208,10 @@ class HipOps:
         self.k.gemm_nt(x, w, b, c, None)
         return c
 
+    def _lt_epi_ok(self, *ts):
+        return _LT_EPILOGUE and all(t is not None and t.dtype == torch.bfloat16 and t.is_contiguous()
+                                    and t.data_ptr() % 16 == 0 for t in ts)
+
     def linear_gelu(self, x, w, b):
         if not self._gemm_ok(x, w):
             u = torch.addmm(b, x, w.t())
@@ -236,6 +250,15 @@ class HipOps:
         du = torch.empty_like(u)
         self.k.gelu_bwd(u, dy, du)
         return du
+
+    def wgrad_bgrad(self, dy, x, dw, db):
+        """dw = dy^T x and db = column sums of dy: one hipBLASLt GEMM with the BGRADB epilogue where
+        it has a solution (csrc/hip/lt_epilogue.cpp), else wgrad + colsum."""
+        if self._lt_epi_ok(dy, x, dw, db) and dy.dim() == 2 and self._bwd_mode() != "all":
+            if self.k.lt_wgrad_bgrad(dy, x, dw, db):
+                return
+        self.wgrad(dy, x, dw)
+        self.colsum(dy, db)
 
     def attn_fwd(self, qkv, B, T, H, hd=64):
         assert hd == 64
