@@ -461,6 +461,195 @@ __global__ void __launch_bounds__(512) gemm_lt2_kernel(const uint16_t* __restric
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 256 x 256 output tile, 4 waves of 128 x 128 (8 x 8 v_mfma_f32_16x16x32_bf16 accumulators = 256
+// AGPRs per lane, one wave per SIMD), K-step 32, four LDS stages (32 KB each, three K-tiles in flight).
+// Why: a 64 x 64 wave tile reads (64 + 64) x 32 x 2 B of fragments per 64 x 64 x 32 MFMA block - at
+// 128 B/clk of LDS per CU that is exactly the matrix cores' 4096 FLOP/clk, so the 128^2 kernels above
+// are LDS-bound at ~60-70 % of peak; a 128 x 128 wave tile halves the fragment bytes per FLOP.
+// LDS image: 64-byte rows (32 bf16 of k), 16-byte chunk c of row r stored at slot c ^ ((r >> 2) & 3)
+// (the 8 lanes of a ds_read_b128 phase, rows r..r+7 of one chunk, hit 8 distinct 16-byte bank groups).
+// MEASURED SLOWER than both the 128^2 kernel and hipBLASLt (profiles/gemm_big_tile_r05.log: 490-730
+// TF/s vs 750-960 and 850-1260): with one wave per SIMD the compiler waits lgkmcnt(0) for all 16
+// fragment reads of a K-tile before the first MFMA (4 waves x 16 KB burst = ~512 LDS cycles against
+// 1024 MFMA cycles), and the software-pipelined variant (PIPE 1) spills accumulator renames into
+// v_accvgpr moves. Kept selectable (gemm_nt(..., big=0|1)) for that record; not used by the model.
+// Epilogue: accumulators -> bf16 pairs (adjacent columns swapped across lane pairs with one DPP
+// exchange, 32-bit LDS writes) into a per-wave 128 x 128 tile with 272-byte rows (16-byte pad: the
+// 4 row groups of a write land 4 banks apart), then 16-byte row-segment global stores.
+// ------------------------------------------------------------------------------------------------
+constexpr int BM3 = 256, BK3 = 32, ST3 = 4, SUB3 = BM3 * BK3 * 2;  // SUB3: one operand's K-tile (16 KB)
+constexpr int ROW3 = 272, WTILE3 = 128 * ROW3;                        // epilogue tile row / wave tile bytes
+constexpr int LDS3 = (ST3 * 2 * SUB3 > 4 * WTILE3) ? ST3 * 2 * SUB3 : 4 * WTILE3;
+
+__device__ __forceinline__ void stage3(const uint16_t* __restrict__ src, int ld, int row0, int k0, char* img, int wave,
+                                       int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = wave * 4 + i;             // 1 KB block = 16 rows of 64 B
+    const int row = blk * 16 + (lane >> 2);
+    const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+    __builtin_amdgcn_global_load_lds(src + (size_t)(row0 + row) * ld + k0 + chunk * 8, (lds_ptr)(img + blk * 1024),
+                                     16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag3(const char* img, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4));
+}
+
+template <int EPI, int PIPE>
+__global__ void __launch_bounds__(256) gemm_nt_big_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
+                                                          const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
+                                                          uint16_t* __restrict__ G, int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [stage][A | W][256 rows][64 B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+  const int NB = N / BM3, nwg = NB * (M / BM3), b = blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, xcd = b % 8, loc = b / 8;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  const int m0 = (t / NB) * BM3, n0 = (t % NB) * BM3;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK3;
+  if constexpr (PIPE == 0) {
+    // plain form: wait for tile kt, barrier, refill the buffer of tile kt - 1, fragments, 64 MFMAs
+    auto stage_tile = [&](int kt) {
+      char* d = lds + (kt % ST3) * 2 * SUB3;
+      stage3(A, K, m0, kt * BK3, d, wave, lane);
+      stage3(W, K, n0, kt * BK3, d + SUB3, wave, lane);
+    };
+#pragma unroll
+    for (int p = 0; p < ST3 - 1; ++p)
+      if (p < nk) stage_tile(p);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int younger = min(nk - 1 - kt, ST3 - 2);
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + ST3 - 1 < nk) stage_tile(kt + ST3 - 1);
+      const char* la = lds + (kt % ST3) * 2 * SUB3;
+      const char* lb = la + SUB3;
+      const int chunk = lane >> 4;
+      bf16x8 a[8], w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        a[i] = frag3(la, wr * 128 + i * 16 + (lane & 15), chunk);
+        w[i] = frag3(lb, wc * 128 + i * 16 + (lane & 15), chunk);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  } else {
+  // Software pipeline, branch-free body (so the scheduler can interleave it): step kt waits for tile
+  // kt + 1 (its own 8 DMA; tiles kt + 2, kt + 3 stay in flight), refills tile kt's buffer with tile
+  // kt + 4 (clamped to the last tile past the end: a harmless re-load into a dead buffer), reads tile
+  // kt + 1's fragments into the other register set while tile kt's 64 MFMAs issue (1 ds_read per 4
+  // MFMAs, the 8 DMA spread over the first half). The lgkmcnt(0) before the barrier makes every wave's
+  // tile-kt fragments resident before any wave's DMA overwrites that buffer.
+  auto stage_tile = [&](int kt) {
+    const int kc = min(kt, nk - 1);
+    char* d = lds + (kt % ST3) * 2 * SUB3;
+    stage3(A, K, m0, kc * BK3, d, wave, lane);
+    stage3(W, K, n0, kc * BK3, d + SUB3, wave, lane);
+  };
+  auto read_frags = [&](int kt, bf16x8 (&fa)[8], bf16x8 (&fw)[8]) {
+    const char* la = lds + (kt % ST3) * 2 * SUB3;
+    const char* lb = la + SUB3;
+    const int chunk = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      fa[i] = frag3(la, wr * 128 + i * 16 + (lane & 15), chunk);
+      fw[i] = frag3(lb, wc * 128 + i * 16 + (lane & 15), chunk);
+    }
+  };
+  auto step = [&](int kt, bf16x8 (&ca)[8], bf16x8 (&cw)[8], bf16x8 (&na)[8], bf16x8 (&nw)[8]) {
+    asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stage_tile(kt + ST3);
+    read_frags(kt + 1, na, nw);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i], cw[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 ds_read
+      if (g < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 DMA (VMEM read)
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < ST3; ++p) stage_tile(p);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // own loads of tile 0
+  __builtin_amdgcn_s_barrier();
+  bf16x8 a0[8], w0[8], a1[8], w1[8];
+  read_frags(0, a0, w0);
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, a0, w0, a1, w1);
+    step(kt + 1, a1, w1, a0, w0);
+  }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the clamped tail DMA writes LDS too
+  __builtin_amdgcn_s_barrier();  // all fragment reads done before the epilogue reuses the LDS
+
+  char* tile = lds + wave * WTILE3;
+  const bool odd = lane & 1;
+  const int orow = m0 + wr * 128, ocol = n0 + wc * 128;
+#pragma unroll
+  for (int pass = 0; pass < (EPI == 1 ? 2 : 1); ++pass) {
+    uint16_t* out = pass ? G : C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = j * 16 + (lane & 15);
+      const float bv = bias ? bf2f(bias[ocol + col]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float u = bf2f(f2bf(acc[i][j][e] + bv));
+          v[e] = pass ? gelu_tanh(u) : u;
+        }
+        // lane pair (c, c+1): the even lane writes rows 0-1, the odd lane rows 2-3, as column pairs
+        const float s0 = odd ? v[0] : v[2], s1 = odd ? v[1] : v[3];
+        const float r0 = __shfl_xor(s0, 1, 64), r1 = __shfl_xor(s1, 1, 64);
+        const int row = i * 16 + (lane >> 4) * 4 + (odd ? 2 : 0);
+        const int c2 = col & ~1;
+        const uint32_t w0 = odd ? ((uint32_t)f2bf(r0) | ((uint32_t)f2bf(v[2]) << 16))
+                                : ((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(r0) << 16));
+        const uint32_t w1 = odd ? ((uint32_t)f2bf(r1) | ((uint32_t)f2bf(v[3]) << 16))
+                                : ((uint32_t)f2bf(v[1]) | ((uint32_t)f2bf(r1) << 16));
+        *reinterpret_cast<uint32_t*>(tile + row * ROW3 + c2 * 2) = w0;
+        *reinterpret_cast<uint32_t*>(tile + (row + 1) * ROW3 + c2 * 2) = w1;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // wave-private tile: LDS writes before reads
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 8
+    for (int it = 0; it < 32; ++it) {
+      const int row = it * 4 + (lane >> 4), ch = lane & 15;
+      *reinterpret_cast<uint4*>(out + (size_t)(orow + row) * N + ocol + ch * 8) =
+          *reinterpret_cast<const uint4*>(tile + row * ROW3 + ch * 16);
+    }
+    if (EPI == 1 && pass == 0) {  // the G pass rewrites the tile: every lane's reads first
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
@@ -522,6 +711,36 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
 }
 
 bool supported(int M, int N, int K) { return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0; }
+
+bool supported_big(int M, int N, int K) {
+  return M > 0 && N > 0 && K > 0 && M % BM3 == 0 && N % BM3 == 0 && K % (2 * BK3) == 0;
+}
+
+hipError_t launch_nt_big(const void* A, const void* W, const void* bias, void* C, void* G, int M, int N, int K,
+                         int variant, hipStream_t st) {
+  if (!supported_big(M, N, K)) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {  // > 64 KB of dynamic LDS is opted into per kernel
+    const void* ks_[] = {(const void*)gemm_nt_big_kernel<0, 0>, (const void*)gemm_nt_big_kernel<1, 0>,
+                         (const void*)gemm_nt_big_kernel<0, 1>, (const void*)gemm_nt_big_kernel<1, 1>};
+    for (const void* f : ks_) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS3);
+    attr = true;
+  }
+  const dim3 grid((M / BM3) * (N / BM3));
+  const uint16_t* a = static_cast<const uint16_t*>(A);
+  const uint16_t* w = static_cast<const uint16_t*>(W);
+  const uint16_t* bb = static_cast<const uint16_t*>(bias);
+  uint16_t* c = static_cast<uint16_t*>(C);
+  uint16_t* g = static_cast<uint16_t*>(G);
+  if (variant == 1) {
+    if (g) hipLaunchKernelGGL((gemm_nt_big_kernel<1, 1>), grid, dim3(256), LDS3, st, a, w, bb, c, g, M, N, K);
+    else hipLaunchKernelGGL((gemm_nt_big_kernel<0, 1>), grid, dim3(256), LDS3, st, a, w, bb, c, nullptr, M, N, K);
+  } else {
+    if (g) hipLaunchKernelGGL((gemm_nt_big_kernel<1, 0>), grid, dim3(256), LDS3, st, a, w, bb, c, g, M, N, K);
+    else hipLaunchKernelGGL((gemm_nt_big_kernel<0, 0>), grid, dim3(256), LDS3, st, a, w, bb, c, nullptr, M, N, K);
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_nt(const void* A, const void* W, const void* bias, void* C, void* G, int M, int N, int K,
                      hipStream_t st) {
