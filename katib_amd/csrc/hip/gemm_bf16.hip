@@ -39,9 +39,17 @@ __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float((uint
 __device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
 __device__ __forceinline__ float gelu_tanh(float u) {
-  const float z = 0.7978845608028654f * (u + 0.044715f * u * u * u);
-  const float e = __expf(2.f * z);
-  return 0.5f * u * (1.f + (1.f - 2.f / (e + 1.f)));
+  const float z2 = (2.f * 0.7978845608028654f * 1.4426950408889634f) * u * (1.f + 0.044715f * u * u);  // 2z log2(e)
+  return 0.5f * u * (2.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z2) + 1.f));
+}
+
+// d gelu_tanh / du (the contract of transformer.hip gelu_df: tanh through exp)
+// (hardware exp2 + reciprocal: in a GEMM epilogue the full-precision divide was most of the cost)
+__device__ __forceinline__ float gelu_tanh_df(float u) {
+  const float u2 = u * u;
+  const float z2 = (2.f * 0.7978845608028654f * 1.4426950408889634f) * u * (1.f + 0.044715f * u2);  // 2z log2(e)
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z2) + 1.f);
+  return 0.5f * (1.f + t) + (0.5f * 0.7978845608028654f) * u * (1.f - t * t) * (1.f + 3.f * 0.044715f * u2);
 }
 
 // one operand K-tile (128 rows x 64 bf16) -> LDS: 4 DMA instructions per thread
@@ -213,11 +221,13 @@ __device__ __forceinline__ bf16x8 frag_mn(const char* lds, int mn_base, int kk, 
 }
 
 // C (+)= op(A) op(B) over k slice blockIdx.y; OUT_F32: fp32 slab [slice][M][N], else bf16 (+ bias)
+// gu (bf16 output only): C = (op(A) op(B) (+ bias)) * gelu_tanh'(gu), the GELU backward folded into the
+// dgrad epilogue (gu = the pre-activation, same [M][N] layout as C)
 template <bool A_MN, bool B_MN, bool OUT_F32>
 __global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict__ A, int lda,
                                                       const uint16_t* __restrict__ B, int ldb,
                                                       const uint16_t* __restrict__ bias, void* __restrict__ Cv,
-                                                      int M, int N, int kslice) {
+                                                      int M, int N, int kslice, const uint16_t* __restrict__ gu) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * TILE_BYTES];  // [stage][A|B][16 KB]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
   const int NB = N / BN, nwg = NB * (M / BM), b = blockIdx.x;
@@ -298,6 +308,16 @@ __global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict
   } else {
     uint16_t* C = static_cast<uint16_t*>(Cv);
     char* tile_u = lds + wave * 8192;
+    // GELU-backward epilogue: the pre-activation segments this lane stores, loaded before the
+    // accumulator shuffle so their latency hides behind it
+    uint4 uu[8];
+    if (gu) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int row = it * 8 + (lane >> 3), ch = lane & 7;
+        uu[it] = *reinterpret_cast<const uint4*>(gu + (size_t)(m0 + wr * 64 + row) * N + n0 + wc * 64 + ch * 8);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = j * 16 + (lane & 15);
@@ -314,8 +334,18 @@ __global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int row = it * 8 + (lane >> 3), ch = lane & 7;
-      *reinterpret_cast<uint4*>(C + (size_t)(m0 + wr * 64 + row) * N + n0 + wc * 64 + ch * 8) =
-          *reinterpret_cast<const uint4*>(tile_u + row * 128 + ch * 16);
+      uint4 v = *reinterpret_cast<const uint4*>(tile_u + row * 128 + ch * 16);
+      if (gu) {
+        uint32_t* pv = reinterpret_cast<uint32_t*>(&v);
+        const uint32_t* pu = reinterpret_cast<const uint32_t*>(&uu[it]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float lo = bf2f((uint16_t)(pv[k] & 0xffff)) * gelu_tanh_df(bf2f((uint16_t)(pu[k] & 0xffff)));
+          const float hi = bf2f((uint16_t)(pv[k] >> 16)) * gelu_tanh_df(bf2f((uint16_t)(pu[k] >> 16)));
+          pv[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+        }
+      }
+      *reinterpret_cast<uint4*>(C + (size_t)(m0 + wr * 64 + row) * N + n0 + wc * 64 + ch * 8) = v;
     }
   }
 }
@@ -653,10 +683,11 @@ __global__ void __launch_bounds__(256) gemm_nt_big_kernel(const uint16_t* __rest
 }  // namespace
 
 hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
-                     bool out_f32, int splitk, int M, int N, int K, hipStream_t st) {
+                     bool out_f32, int splitk, int M, int N, int K, hipStream_t st, const void* gelu_u) {
   if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || splitk < 1 || K % (splitk * BK) ||
-      (!out_f32 && splitk != 1))
+      (!out_f32 && splitk != 1) || (gelu_u && out_f32))
     return hipErrorInvalidValue;
+  const uint16_t* gu = static_cast<const uint16_t*>(gelu_u);
   const uint16_t* a = static_cast<const uint16_t*>(A);
   const uint16_t* b = static_cast<const uint16_t*>(B);
   const uint16_t* bb = static_cast<const uint16_t*>(bias);
@@ -665,7 +696,7 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
   // (256 x 128, 3 stages, 8 waves, 1 per CU): measured 15-25 % slower on every GPT-2 backward shape
   // (profiles/gemm_fwd_bwd_table_r05.log), kept selectable
   static const int tile = getenv("KATIB_HIP_GEMM_TILE") ? atoi(getenv("KATIB_HIP_GEMM_TILE")) : 128;
-  if (tile == 256 && M % BM2 == 0) {
+  if (tile == 256 && M % BM2 == 0 && !gu) {
     static bool attr = false;
     if (!attr) {  // > 64 KB of dynamic LDS must be opted into per kernel
       const void* ks_[] = {(const void*)gemm_lt2_kernel<false, false, false>, (const void*)gemm_lt2_kernel<false, true, false>,
@@ -694,7 +725,7 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
   }
   const dim3 grid((M / BM) * (N / BN), splitk);
 #define LT_LAUNCH(AM, BMN, F32) \
-  hipLaunchKernelGGL((gemm_lt_kernel<AM, BMN, F32>), grid, dim3(256), 0, st, a, lda, b, ldb, bb, C, M, N, ks)
+  hipLaunchKernelGGL((gemm_lt_kernel<AM, BMN, F32>), grid, dim3(256), 0, st, a, lda, b, ldb, bb, C, M, N, ks, gu)
   if (out_f32) {
     if (a_mn && b_mn) LT_LAUNCH(true, true, true);
     else if (a_mn) LT_LAUNCH(true, false, true);

@@ -263,9 +263,8 @@ __global__ __launch_bounds__(64 * kLnRedGroups) void ln_reduce_k(const float* __
 constexpr float kGeluK0 = 0.7978845608028654f;  // sqrt(2/pi)
 constexpr float kGeluK1 = 0.044715f;
 
-__device__ __forceinline__ float tanh_fast(float z) {
-  const float e = __expf(2.f * z);
-  return 1.f - 2.f / (e + 1.f);
+__device__ __forceinline__ float tanh_fast(float z) {  // hardware exp2 + reciprocal (no IEEE divide)
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z * 2.8853900817779268f) + 1.f);  // 2 log2(e)
 }
 __device__ __forceinline__ float gelu_f(float u) {
   return 0.5f * u * (1.f + tanh_fast(kGeluK0 * (u + kGeluK1 * u * u * u)));

@@ -228,7 +228,7 @@ class GPT2Flat:
             ops.wgrad(dr, gl, g[pre + "fc2.weight"])  # fc2.bias: summed by the LayerNorm backward that wrote dr
             if not lb:
                 ops.colsum(dr, g[pre + "fc2.bias"])
-            du = ops.gelu_bwd(u, ops.dgrad(dr, self.w[pre + "fc2.weight"]))
+            du = ops.dgrad_gelu(dr, self.w[pre + "fc2.weight"], u)  # GELU backward in the dgrad epilogue
             ops.wgrad_bgrad(du, h2, g[pre + "fc.weight"], g[pre + "fc.bias"])
             dh2 = ops.dgrad(du, self.w[pre + "fc.weight"])
             del du

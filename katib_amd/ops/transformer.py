@@ -52,6 +52,8 @@ _XENT_FUSED = os.environ.get("KATIB_XENT_FUSED", "1") != "0"
 # unsplit 256x128 MI32x32 tiles, 197 / 115 us against 65-72 us for the split-K wgrad + a 14.5 us
 # colsum, 782k -> 743k tokens/s (profiles/lt_epilogue_r05.log).
 _LT_EPILOGUE = os.environ.get("KATIB_LT_EPILOGUE", "0") == "1"
+# GELU backward folded into the fc2 dgrad epilogue (HipOps.dgrad_gelu; =0: hipBLASLt dgrad + gelu_bwd)
+_GELU_DGRAD = os.environ.get("KATIB_GELU_DGRAD", "1") != "0"
 
 class TorchOps:
     name = "torch"
@@ -153,6 +155,10 @@ class TorchOps:
         self.wgrad(dy, x, dw)
         self.colsum(dy, db)
 
+    def dgrad_gelu(self, dy, w, u):
+        """(dy @ w) * gelu_tanh'(u): the MLP's fc2 input gradient taken back through the GELU."""
+        return self.gelu_bwd(u, self.dgrad(dy, w))
+
     def dgrad(self, dy, w):
         return torch.mm(dy, w)
 
@@ -250,6 +256,20 @@ class HipOps:
         du = torch.empty_like(u)
         self.k.gelu_bwd(u, dy, du)
         return du
+
+    def dgrad_gelu(self, dy, w, u):
+        """(dy @ w) * gelu_tanh'(u) in one launch: the NN dgrad kernel (gemm_lt) with the GELU backward
+        in its epilogue (reads u where it writes the gradient) - against hipBLASLt's dgrad + the
+        gelu_bwd pass, which writes the gradient, then re-reads it with u and writes it again.
+        KATIB_GELU_DGRAD=0: the two-launch form."""
+        M, N = dy.shape
+        K = w.shape[1]
+        if (_GELU_DGRAD and self._bwd_mode() != "0" and self._lt_ok(dy, w, u) and u.shape == (M, K)
+                and M % 128 == 0 and K % 128 == 0 and N % 64 == 0):
+            out = torch.empty((M, K), device=dy.device, dtype=torch.bfloat16)
+            self.k.gemm_lt(dy, False, w, True, None, out, 1, u)
+            return out
+        return self.gelu_bwd(u, self.dgrad(dy, w))
 
     def wgrad_bgrad(self, dy, x, dw, db):
         """dw = dy^T x and db = column sums of dy: one hipBLASLt GEMM with the BGRADB epilogue where

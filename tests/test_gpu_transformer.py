@@ -66,6 +66,29 @@ def test_gelu(ops):
     assert _rel(hip.gelu_bwd(u, dy), ref.gelu_bwd(u, dy)) < 1e-2
 
 
+@pytest.mark.parametrize("M", [256, 16384])
+def test_dgrad_gelu_epilogue(ops, M):
+    """gemm_lt NN dgrad with the GELU backward in its epilogue vs fp32 (dy @ w) * gelu'(u)."""
+    hip, ref = ops
+    g = _gen(7)
+    D, F4 = 768, 3072
+    dy = torch.randn(M, D, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(D, F4, device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    u = (torch.randn(M, F4, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    du = hip.dgrad_gelu(dy, w, u)
+    x = u.float()
+    k0, k1 = math.sqrt(2.0 / math.pi), 0.044715
+    t = torch.tanh(k0 * (x + k1 * x ** 3))
+    d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+    want = (dy.float() @ w.float()) * d
+    assert _rel(du, want) < 2e-2
+    assert _rel(du, ref.dgrad_gelu(dy, w, u)) < 2e-2
+    # the epilogue path really ran (same bits as a direct call)
+    out = torch.empty_like(du)
+    hip.k.gemm_lt(dy, False, w, True, None, out, 1, u)
+    assert torch.equal(out, du)
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 3072, 768), (16384, 3072, 768), (16384, 2304, 768)])
 def test_lt_wgrad_bgrad(ops, M, N, K):
     """hipBLASLt BGRADB (weight + bias gradient in one GEMM) vs the fp32 products."""
