@@ -40,6 +40,9 @@ from .common import CapturedStep, Timer, device, phase, process_start_time, repo
 _T_TORCH = _time.time()
 
 
+_SET_TO_NONE = __import__("os").environ.get("KATIB_MLP_SET_TO_NONE", "1") != "0"
+
+
 def parse_args(argv):
     p = argparse.ArgumentParser(description="MNIST MLP trial (katib-amd)")
     p.add_argument("--lr", type=float, default=0.05)
@@ -228,7 +231,10 @@ def main(argv=None):
         with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=amp):
             logits = model(xb)
             loss = F.cross_entropy(logits, yb)
-        opt.zero_grad(set_to_none=False)
+        # set_to_none: backward writes each gradient instead of a fill + an accumulate-add per
+        # parameter (the captured step replays into the graph pool's same addresses; ~19 of the
+        # ~75 kernels of a 3-layer bf16 step, profiles/b1_module_step_r05.log). =0: the old form.
+        opt.zero_grad(set_to_none=_SET_TO_NONE)
         loss.backward()
         opt.step()
         loss_buf.add_(loss.detach())
@@ -243,7 +249,7 @@ def main(argv=None):
     step = CapturedStep(train_step, enabled=bool(args.capture))
     # one eager warm-up chunk (U real steps) creates the optimizer state and the allocator blocks
     chunk = CapturedStep(train_chunk, enabled=bool(args.capture), warmup=1) if U > 1 else None
-    # zero grads exist before capture (set_to_none=False keeps the same buffers)
+    # zero grads exist before the first (eager) step: the capturable-Adam state pre-step below needs them
     for p_ in model.parameters():
         p_.grad = torch.zeros_like(p_)
     if args.optimizer == "adam" and dev.type == "cuda":  # capturable Adam: state on the device before capture
