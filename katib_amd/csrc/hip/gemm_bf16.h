@@ -21,9 +21,11 @@ hipError_t launch_nt_big(const void* A, const void* W, const void* bias, void* C
 // the stored row strides (elements). out_f32: C is an fp32 slab [splitk][M][N] (one slab per K
 // slice), else bf16 [M][N] (+ bias[N], splitk 1). M, N multiples of 128, K of 64 * splitk.
 // gelu_u (bf16 output only): C = (product + bias) * gelu_tanh'(gelu_u[M][N]) - the GELU backward of the
-// MLP folded into its dgrad epilogue.
+// MLP folded into its dgrad epilogue. colpart (bf16 output only): fp32 column sums of the stored C per
+// 64-row block, colpart[M / 64][N] (reduced over blocks by the caller: the bias gradient).
 hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
-                     bool out_f32, int splitk, int M, int N, int K, hipStream_t st, const void* gelu_u = nullptr);
+                     bool out_f32, int splitk, int M, int N, int K, hipStream_t st, const void* gelu_u = nullptr,
+                     float* colpart = nullptr);
 
 }  // namespace gemm
 }  // namespace katib_hip

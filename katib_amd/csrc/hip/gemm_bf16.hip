@@ -222,12 +222,14 @@ __device__ __forceinline__ bf16x8 frag_mn(const char* lds, int mn_base, int kk, 
 
 // C (+)= op(A) op(B) over k slice blockIdx.y; OUT_F32: fp32 slab [slice][M][N], else bf16 (+ bias)
 // gu (bf16 output only): C = (op(A) op(B) (+ bias)) * gelu_tanh'(gu), the GELU backward folded into the
-// dgrad epilogue (gu = the pre-activation, same [M][N] layout as C)
+// dgrad epilogue (gu = the pre-activation, same [M][N] layout as C). cpart (bf16 output only): fp32
+// column sums of the stored C per 64-row block, cpart[M / 64][N] (the bias gradient's first stage)
 template <bool A_MN, bool B_MN, bool OUT_F32>
 __global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict__ A, int lda,
                                                       const uint16_t* __restrict__ B, int ldb,
                                                       const uint16_t* __restrict__ bias, void* __restrict__ Cv,
-                                                      int M, int N, int kslice, const uint16_t* __restrict__ gu) {
+                                                      int M, int N, int kslice, const uint16_t* __restrict__ gu,
+                                                      float* __restrict__ cpart) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * TILE_BYTES];  // [stage][A|B][16 KB]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
   const int NB = N / BN, nwg = NB * (M / BM), b = blockIdx.x;
@@ -331,6 +333,7 @@ __global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int row = it * 8 + (lane >> 3), ch = lane & 7;
@@ -345,7 +348,31 @@ __global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict
           pv[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
         }
       }
+      if (cpart) {
+        const uint32_t* pv = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          cs[2 * k] += bf2f((uint16_t)(pv[k] & 0xffff));
+          cs[2 * k + 1] += bf2f((uint16_t)(pv[k] >> 16));
+        }
+      }
       *reinterpret_cast<uint4*>(C + (size_t)(m0 + wr * 64 + row) * N + n0 + wc * 64 + ch * 8) = v;
+    }
+    if (cpart) {
+      // the 8 lanes sharing a column chunk (lane & 7) hold the wave's 64 rows: fold them, lanes 0-7 store
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = cs[e];
+        x += __shfl_xor(x, 8, 64);
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
+        cs[e] = x;
+      }
+      if (lane < 8) {
+        float* dst = cpart + (size_t)((m0 + wr * 64) >> 6) * N + n0 + wc * 64 + lane * 8;
+        *reinterpret_cast<float4*>(dst) = float4{cs[0], cs[1], cs[2], cs[3]};
+        *reinterpret_cast<float4*>(dst + 4) = float4{cs[4], cs[5], cs[6], cs[7]};
+      }
     }
   }
 }
@@ -683,9 +710,10 @@ __global__ void __launch_bounds__(256) gemm_nt_big_kernel(const uint16_t* __rest
 }  // namespace
 
 hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
-                     bool out_f32, int splitk, int M, int N, int K, hipStream_t st, const void* gelu_u) {
+                     bool out_f32, int splitk, int M, int N, int K, hipStream_t st, const void* gelu_u,
+                     float* colpart) {
   if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || splitk < 1 || K % (splitk * BK) ||
-      (!out_f32 && splitk != 1) || (gelu_u && out_f32))
+      (!out_f32 && splitk != 1) || ((gelu_u || colpart) && out_f32))
     return hipErrorInvalidValue;
   const uint16_t* gu = static_cast<const uint16_t*>(gelu_u);
   const uint16_t* a = static_cast<const uint16_t*>(A);
@@ -696,7 +724,7 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
   // (256 x 128, 3 stages, 8 waves, 1 per CU): measured 15-25 % slower on every GPT-2 backward shape
   // (profiles/gemm_fwd_bwd_table_r05.log), kept selectable
   static const int tile = getenv("KATIB_HIP_GEMM_TILE") ? atoi(getenv("KATIB_HIP_GEMM_TILE")) : 128;
-  if (tile == 256 && M % BM2 == 0 && !gu) {
+  if (tile == 256 && M % BM2 == 0 && !gu && !colpart) {
     static bool attr = false;
     if (!attr) {  // > 64 KB of dynamic LDS must be opted into per kernel
       const void* ks_[] = {(const void*)gemm_lt2_kernel<false, false, false>, (const void*)gemm_lt2_kernel<false, true, false>,
@@ -725,7 +753,8 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
   }
   const dim3 grid((M / BM) * (N / BN), splitk);
 #define LT_LAUNCH(AM, BMN, F32) \
-  hipLaunchKernelGGL((gemm_lt_kernel<AM, BMN, F32>), grid, dim3(256), 0, st, a, lda, b, ldb, bb, C, M, N, ks, gu)
+  hipLaunchKernelGGL((gemm_lt_kernel<AM, BMN, F32>), grid, dim3(256), 0, st, a, lda, b, ldb, bb, C, M, N, ks, gu, \
+                     colpart)
   if (out_f32) {
     if (a_mn && b_mn) LT_LAUNCH(true, true, true);
     else if (a_mn) LT_LAUNCH(true, false, true);

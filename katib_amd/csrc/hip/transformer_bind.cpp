@@ -275,7 +275,8 @@ void gemm_nt(const Tensor& A, const Tensor& W, const c10::optional<Tensor>& bias
 // [K][M] (else [M][K]); b_mn: B stored [K][N] (else [N][K]). C: bf16 [M][N] (splitk 1, optional
 // bias) or fp32 [splitk][M][N] slabs (one per K slice, summed by the caller).
 void gemm_lt(const Tensor& A, bool a_mn, const Tensor& B, bool b_mn, const c10::optional<Tensor>& bias,
-             const Tensor& C, int64_t splitk, const c10::optional<Tensor>& gelu_u) {
+             const Tensor& C, int64_t splitk, const c10::optional<Tensor>& gelu_u,
+             const c10::optional<Tensor>& colpart) {
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "gemm_lt: 2-D operands");
   const int64_t M = a_mn ? A.size(1) : A.size(0), K = a_mn ? A.size(0) : A.size(1);
   const int64_t N = b_mn ? B.size(1) : B.size(0), KB = b_mn ? B.size(0) : B.size(1);
@@ -303,8 +304,14 @@ void gemm_lt(const Tensor& A, bool a_mn, const Tensor& B, bool b_mn, const c10::
     chk(*gelu_u, at::kBFloat16, M * N, "gelu_u");
     gu = gelu_u->data_ptr();
   }
+  float* cp = nullptr;
+  if (colpart.has_value() && colpart->defined()) {
+    TORCH_CHECK(!f32, "gemm_lt: column partial sums need a bf16 output");
+    chk(*colpart, at::kFloat, (M / 64) * N, "colpart");
+    cp = colpart->data_ptr<float>();
+  }
   ok(katib_hip::gemm::launch_lt(A.data_ptr(), (int)A.size(1), a_mn, B.data_ptr(), (int)B.size(1), b_mn, bp_,
-                                C.data_ptr(), f32, (int)splitk, (int)M, (int)N, (int)K, stream(), gu),
+                                C.data_ptr(), f32, (int)splitk, (int)M, (int)N, (int)K, stream(), gu, cp),
      "gemm_lt");
 }
 
@@ -313,7 +320,7 @@ void gemm_lt(const Tensor& A, bool a_mn, const Tensor& B, bool b_mn, const c10::
 void register_transformer(py::module& m) {
   m.def("gemm_lt", &gemm_lt, "bf16 C = op(A) op(B), layout-native operands (NN / TN / NT), split-K fp32 slabs",
         py::arg("A"), py::arg("a_mn"), py::arg("B"), py::arg("b_mn"), py::arg("bias"), py::arg("C"),
-        py::arg("splitk") = 1, py::arg("gelu_u") = py::none());
+        py::arg("splitk") = 1, py::arg("gelu_u") = py::none(), py::arg("colpart") = py::none());
   m.def("gemm_nt", &gemm_nt, "bf16 C = A W^T (+ bias) (+ GELU) on MFMA (gemm_bf16.hip)", py::arg("A"), py::arg("W"),
         py::arg("bias"), py::arg("C"), py::arg("G"), py::arg("big") = -1);
   m.def("gemm_nt_big_supported", [](int64_t M, int64_t N, int64_t K) {

@@ -228,8 +228,9 @@ class GPT2Flat:
             ops.wgrad(dr, gl, g[pre + "fc2.weight"])  # fc2.bias: summed by the LayerNorm backward that wrote dr
             if not lb:
                 ops.colsum(dr, g[pre + "fc2.bias"])
-            du = ops.dgrad_gelu(dr, self.w[pre + "fc2.weight"], u)  # GELU backward in the dgrad epilogue
-            ops.wgrad_bgrad(du, h2, g[pre + "fc.weight"], g[pre + "fc.bias"])
+            # GELU backward and the fc.bias column sums in the dgrad epilogue
+            du = ops.dgrad_gelu(dr, self.w[pre + "fc2.weight"], u, g[pre + "fc.bias"])
+            ops.wgrad(du, h2, g[pre + "fc.weight"])
             dh2 = ops.dgrad(du, self.w[pre + "fc.weight"])
             del du
             ops.ln_bwd(dh2, sb, mu2, rs2, self.w[pre + "ln2.weight"], G, dr, g[pre + "ln2.weight"],

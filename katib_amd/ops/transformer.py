@@ -54,6 +54,10 @@ _XENT_FUSED = os.environ.get("KATIB_XENT_FUSED", "1") != "0"
 _LT_EPILOGUE = os.environ.get("KATIB_LT_EPILOGUE", "0") == "1"
 # GELU backward folded into the fc2 dgrad epilogue (HipOps.dgrad_gelu; =0: hipBLASLt dgrad + gelu_bwd)
 _GELU_DGRAD = os.environ.get("KATIB_GELU_DGRAD", "1") != "0"
+# ... and the fc1 bias gradient's column sums from the same epilogue + one row-sum launch. Opt-in
+# (KATIB_GELU_DGRAD_BIAS=1): measured neutral, 806.3k vs 807.1k tokens/s against the colsum pass over du
+# (profiles/gpt2_gelu_dgrad_bias_ab_r05.log) - the epilogue's shuffles cost what the 100 MB re-read saved
+_GELU_DGRAD_BIAS = os.environ.get("KATIB_GELU_DGRAD_BIAS", "0") == "1"
 
 class TorchOps:
     name = "torch"
@@ -155,9 +159,13 @@ class TorchOps:
         self.wgrad(dy, x, dw)
         self.colsum(dy, db)
 
-    def dgrad_gelu(self, dy, w, u):
-        """(dy @ w) * gelu_tanh'(u): the MLP's fc2 input gradient taken back through the GELU."""
-        return self.gelu_bwd(u, self.dgrad(dy, w))
+    def dgrad_gelu(self, dy, w, u, db=None):
+        """(dy @ w) * gelu_tanh'(u): the MLP's fc2 input gradient taken back through the GELU;
+        ``db``: also its column sums (the fc1 bias gradient)."""
+        du = self.gelu_bwd(u, self.dgrad(dy, w))
+        if db is not None:
+            self.colsum(du, db)
+        return du
 
     def dgrad(self, dy, w):
         return torch.mm(dy, w)
@@ -257,19 +265,32 @@ class HipOps:
         self.k.gelu_bwd(u, dy, du)
         return du
 
-    def dgrad_gelu(self, dy, w, u):
+    def dgrad_gelu(self, dy, w, u, db=None):
         """(dy @ w) * gelu_tanh'(u) in one launch: the NN dgrad kernel (gemm_lt) with the GELU backward
         in its epilogue (reads u where it writes the gradient) - against hipBLASLt's dgrad + the
         gelu_bwd pass, which writes the gradient, then re-reads it with u and writes it again.
-        KATIB_GELU_DGRAD=0: the two-launch form."""
+        ``db`` (the fc1 bias gradient): per-64-row column sums from the same epilogue + one row-sum
+        launch, instead of a colsum pass re-reading the gradient. KATIB_GELU_DGRAD=0: the
+        two-launch form."""
         M, N = dy.shape
         K = w.shape[1]
         if (_GELU_DGRAD and self._bwd_mode() != "0" and self._lt_ok(dy, w, u) and u.shape == (M, K)
                 and M % 128 == 0 and K % 128 == 0 and N % 64 == 0):
             out = torch.empty((M, K), device=dy.device, dtype=torch.bfloat16)
+            if (_GELU_DGRAD_BIAS and db is not None and db.is_contiguous() and db.numel() == K
+                    and db.dtype == torch.bfloat16 and db.data_ptr() % 16 == 0):
+                part = torch.empty((M // 64, K), device=dy.device, dtype=torch.float32)
+                self.k.gemm_lt(dy, False, w, True, None, out, 1, u, part)
+                self.k.reduce_rows(part, db)
+                return out
             self.k.gemm_lt(dy, False, w, True, None, out, 1, u)
+            if db is not None:
+                self.colsum(out, db)
             return out
-        return self.gelu_bwd(u, self.dgrad(dy, w))
+        du = self.gelu_bwd(u, self.dgrad(dy, w))
+        if db is not None:
+            self.colsum(du, db)
+        return du
 
     def wgrad_bgrad(self, dy, x, dw, db):
         """dw = dy^T x and db = column sums of dy: one hipBLASLt GEMM with the BGRADB epilogue where

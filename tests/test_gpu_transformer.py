@@ -87,6 +87,19 @@ def test_dgrad_gelu_epilogue(ops, M):
     out = torch.empty_like(du)
     hip.k.gemm_lt(dy, False, w, True, None, out, 1, u)
     assert torch.equal(out, du)
+    # + the bias gradient (default: colsum pass; the epilogue's per-64-row column sums directly)
+    db = torch.empty(F4, device=DEV, dtype=torch.bfloat16)
+    du2 = hip.dgrad_gelu(dy, w, u, db)
+    assert torch.equal(du2, du)
+    assert _rel(db, du.float().sum(0)) < 1e-2
+    part = torch.empty(M // 64, F4, device=DEV, dtype=torch.float32)
+    out2 = torch.empty_like(du)
+    hip.k.gemm_lt(dy, False, w, True, None, out2, 1, u, part)
+    assert torch.equal(out2, du)
+    assert _rel(part.sum(0), du.float().sum(0)) < 1e-3
+    dbr = torch.empty_like(db)
+    ref.dgrad_gelu(dy, w, u, dbr)
+    assert _rel(db, dbr) < 2e-2
 
 
 @pytest.mark.parametrize("M,N,K", [(2048, 3072, 768), (16384, 3072, 768), (16384, 2304, 768)])
