@@ -81,6 +81,9 @@ def main():
                          "its measured wall clock next to the projection (-1: on for the b5 config)")
     ap.add_argument("--floor", type=int, default=1,
                     help="N>1: rank 0 also times a dp1 step at the per-rank batch (per_rank_floor_ms)")
+    ap.add_argument("--per-rank-bn", type=int, default=1,
+                    help="N>1 with SyncBN: also time the step with per-rank BatchNorm (DDP semantics) -> "
+                         "per_rank_bn_ms_per_step")
     ap.add_argument("--sync-bn", type=int, default=-1,
                     help="BatchNorm statistics over the global batch (all ranks) instead of per rank; "
                          "-1: on for strong scaling (keeps B5's BN over 128 images at every N)")
@@ -218,6 +221,30 @@ def main():
         sync()
         full_s = comm.allreduce_max(time.perf_counter() - t2)
 
+    # the reference's own data-parallel semantic (DDP with per-rank BatchNorm,
+    # examples/v1beta1/trial-images/pytorch-mnist/mnist.py:190-191) next to the SyncBN headline: the
+    # same search step with each rank normalising over its own 128/N images (4 rendezvous per step:
+    # the gradient buckets only), timed the same way on every rank
+    per_rank_bn_ms = ms_step if (comm.distributed and not sync_bn) else None
+    if comm.distributed and sync_bn and args.per_rank_bn:
+        prb = DartsSearch(layout, dev, comm, capture=bool(args.capture) and dev.type == "cuda", sync_bn=False)
+        for i in range(args.warmup):
+            (tx, ty), (vx, vy) = batches[i % len(batches)]
+            prb.step(tx, ty, vx, vy)
+        sync()
+        comm.barrier()
+        sync()
+        t5 = time.perf_counter()
+        for i in range(args.steps):
+            (tx, ty), (vx, vy) = batches[i % len(batches)]
+            prb.step(tx, ty, vx, vy)
+        sync()
+        comm.barrier()
+        sync()
+        per_rank_bn_ms = comm.allreduce_max((time.perf_counter() - t5) * 1000.0 / args.steps)
+        del prb
+    distinct = comm.distinct_devices() if comm.distributed else 1
+
     # per-rank floor: what one rank's step costs on its own at the per-rank batch (dp1, rank 0's
     # GPU, the other ranks parked at the barrier) - the best an N-rank step could do without the
     # all-reduces and BN synchronisation
@@ -312,6 +339,13 @@ def main():
             "batchnorm": ("global batch (sync-bn)" if sync_bn else
                           ("per rank" if comm.distributed else "global batch")),
             "per_rank_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,
+            # DDP semantics (per-rank BN, the reference's DP); with it the projected search wall clock
+            "per_rank_bn_ms_per_step": round(per_rank_bn_ms, 4) if per_rank_bn_ms is not None else None,
+            "per_rank_bn_search_wall_s": (round(cfg["epochs"] * steps_per_epoch * (per_rank_bn_ms + ms_valid) / 1000.0, 3)
+                                          if per_rank_bn_ms is not None else None),
+            # physical GPUs behind the ranks: < n_gpus means a shared-GPU rehearsal (IPC copies on one
+            # device, no xGMI link crossed)
+            "distinct_devices": distinct,
             "ms_valid_batch": round(ms_valid, 4),
             "measured_search_wall_s": round(full_s, 3) if full_s is not None else None,
             "train_images_per_s": round(bs * comm.world_size * 1000.0 / ms_step, 1),

@@ -369,8 +369,10 @@ class ApiServer:
                     k, _, v = part.strip().partition("=")
                     if k == COOKIE and hmac.compare_digest(v.encode(), want):
                         return True
+                # ?token= only on the UI entry path, answered with a redirect that sets the cookie and
+                # strips the query (_do): the token never sits in a page URL the UI then works under
                 q = (query.get("token") or [""])[0]
-                if q and hmac.compare_digest(q.encode(), want):
+                if q and path == "/" and hmac.compare_digest(q.encode(), want):
                     self._set_cookie = "%s=%s; HttpOnly; SameSite=Strict; Path=/" % (COOKIE, server.token)
                     return True
                 return False
@@ -383,7 +385,16 @@ class ApiServer:
                 try:
                     if not self._authorized(u.path, query):
                         raise _Err(401, "Unauthorized", "missing or wrong bearer token")
-                    query.pop("token", None)
+                    if "token" in query:
+                        if self._set_cookie is None:
+                            raise _Err(400, "BadRequest", "the token query parameter is only accepted on /")
+                        self.send_response(303)
+                        self.send_header("Location", "/")
+                        self.send_header("Set-Cookie", self._set_cookie)
+                        self.send_header("Referrer-Policy", "no-referrer")
+                        self.send_header("Content-Length", "0")
+                        self.end_headers()
+                        return
                     code, ctype, data = server.handle(method, u.path, query, body)
                 except _Err as e:
                     code, ctype = e.code, "application/json"
@@ -396,8 +407,7 @@ class ApiServer:
                 self.send_response(code)
                 self.send_header("Content-Type", ctype)
                 self.send_header("Content-Length", str(len(data)))
-                if getattr(self, "_set_cookie", None):
-                    self.send_header("Set-Cookie", self._set_cookie)
+                self.send_header("Referrer-Policy", "no-referrer")
                 self.end_headers()
                 self.wfile.write(data)
 

@@ -935,21 +935,29 @@ class Manager:
     def start_zygote(self, wait: bool = True) -> bool:
         """Start the trial fork server now (a daemon does this at start-up; otherwise it starts with
         the first eligible trial and the trials launched before it is up are exec'd)."""
-        from .zygote import Zygote
-
         if self._zygote is None and not self._zygote_failed and self._zygote_thread is None:
-            def start():
-                try:
-                    self._zygote = Zygote(self.state_dir)
-                except Exception as e:  # noqa: BLE001
-                    log.warning("fork server unavailable (%s): trials are exec'd", e)
-                    self._zygote_failed = True
-
-            self._zygote_thread = threading.Thread(target=start, name="katib-zygote", daemon=True)
-            self._zygote_thread.start()
+            self._zygote_start_thread()
         if wait and self._zygote_thread is not None:
             self._zygote_thread.join(timeout=180)
         return self._zygote is not None
+
+    def _zygote_start_thread(self):
+        """Start the fork server on a helper thread. It makes this process a child subreaper
+        (trials and their orphaned descendants re-parent here), so the native runtime is told to
+        reap zombie children it does not track, except the server itself (its Popen waits for it)."""
+        from .zygote import Zygote
+
+        def start():
+            try:
+                z = Zygote(self.state_dir)
+                self.runtime.set_reap_orphans(True, [z.proc.pid])
+                self._zygote = z
+            except Exception as e:  # noqa: BLE001 - the exec path always works
+                log.warning("fork server unavailable (%s): trials are exec'd", e)
+                self._zygote_failed = True
+
+        self._zygote_thread = threading.Thread(target=start, name="katib-zygote", daemon=True)
+        self._zygote_thread.start()
 
     def _zygote_spawn(self, proc_name, argv, env, cwd, log_path, cfg, deadline) -> int:
         """Start a cold Python trial from the fork server (controller/zygote.py) and hand it to the
@@ -966,15 +974,7 @@ class Manager:
             # trials launched meanwhile instead of making them wait for it
             self._zygote = None
             if self._zygote_thread is None or not self._zygote_thread.is_alive():
-                def start():
-                    try:
-                        self._zygote = Zygote(self.state_dir)
-                    except Exception as e:  # noqa: BLE001 - the exec path always works
-                        log.warning("fork server unavailable (%s): trials are exec'd", e)
-                        self._zygote_failed = True
-
-                self._zygote_thread = threading.Thread(target=start, name="katib-zygote", daemon=True)
-                self._zygote_thread.start()
+                self._zygote_start_thread()
             return -1
         full = dict(os.environ)
         full.update(env)

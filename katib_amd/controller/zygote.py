@@ -76,13 +76,15 @@ def _run_child(req: Dict, out_fd: int, keep_parent: int) -> None:
         os.environ.update(req.get("env") or {})
         if req.get("cwd"):
             os.chdir(req["cwd"])
+        argv: List[str] = list(req["argv"])
+        _child_imports(argv)
         # stdout is a pipe: line buffering keeps metrics flowing to the collector as they are printed
         sys.stdout.reconfigure(line_buffering=True)
         sys.stderr.reconfigure(line_buffering=True)
         nthreads = os.environ.get("OMP_NUM_THREADS")
         if nthreads and nthreads.isdigit() and "torch" in sys.modules:
             sys.modules["torch"].set_num_threads(int(nthreads))
-        argv: List[str] = list(req["argv"])
+        _restore_blas_threads()
         import runpy
 
         try:
@@ -122,6 +124,72 @@ def _run_child(req: Dict, out_fd: int, keep_parent: int) -> None:
         except Exception:  # noqa: BLE001
             pass
         os._exit(code & 0xFF)
+
+
+# sys.path entries of this interpreter's installation (stdlib, site-packages, .pth additions): what a
+# freshly exec'd interpreter has after its script directory and PYTHONPATH. Set by serve().
+_SITE_PATH: List[str] = []
+
+
+def _site_path() -> List[str]:
+    """sys.path minus entry 0 (the server's launch directory) and this server's own PYTHONPATH."""
+    own = [os.path.abspath(p) for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p]
+    return [p for p in sys.path[1:] if not p or os.path.abspath(p) not in own]
+
+
+def _child_imports(argv: List[str]) -> None:
+    """Make imports in the forked trial resolve as they would after ``exec``:
+
+    * ``sys.path`` = [the script directory (``script.py``), the working directory (``-m``) or ''
+      (``-c``)] + the trial environment's ``PYTHONPATH`` + the installation's paths - the server's
+      own launch directory and PYTHONPATH do not leak into the trial;
+    * every ``katib_amd`` module the server preloaded (other than this server) is dropped from
+      ``sys.modules``: such modules read ``KATIB_*`` switches and phase clocks at import time, so the
+      trial re-imports them under ITS environment (torch and other third-party modules stay loaded -
+      that is the saving the server exists for);
+    * finder caches are invalidated, the working directory having changed under them."""
+    if argv[1] == "-m":
+        head = os.getcwd()
+    elif argv[1] == "-c":
+        head = ""
+    else:
+        head = os.path.dirname(os.path.realpath(argv[1]))
+    extra = [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p]
+    sys.path[:] = [head] + extra + [p for p in _SITE_PATH if p not in extra]
+    for name in list(sys.modules):
+        if (name == "katib_amd" or name.startswith("katib_amd.")) and name not in (
+                "katib_amd", "katib_amd.controller", "katib_amd.controller.zygote"):
+            del sys.modules[name]
+    for k in ("", "."):
+        sys.path_importer_cache.pop(k, None)
+    importlib.invalidate_caches()
+
+
+def _restore_blas_threads() -> None:
+    """The server runs with ``OPENBLAS_NUM_THREADS=1`` (numpy's OpenBLAS otherwise starts a thread
+    pool at import, and a forked child would inherit it half-copied); the trial gets the BLAS pool
+    an exec'd interpreter would have started under its environment."""
+    if "numpy" not in sys.modules:
+        return
+    n = os.environ.get("OPENBLAS_NUM_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    want = int(n) if n and n.isdigit() else (os.cpu_count() or 1)
+    if want <= 1:
+        return
+    try:
+        import threadpoolctl
+
+        threadpoolctl.threadpool_limits(limits=want, user_api="blas")
+    except Exception:  # noqa: BLE001 - a single-threaded BLAS is slower, never wrong
+        pass
+
+
+def os_threads() -> int:
+    """Threads of this process as the kernel counts them (native pools included, which
+    ``threading.active_count()`` does not see)."""
+    try:
+        return len(os.listdir("/proc/self/task"))
+    except OSError:
+        return threading.active_count()
 
 
 def _handle(conn: socket.socket, listener: socket.socket) -> None:
@@ -194,7 +262,15 @@ def serve(path: str, preload: List[str]) -> int:
     if "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized():
         print("zygote: refusing to serve - the GPU was initialised during preload", file=sys.stderr, flush=True)
         return 3
-    threads = threading.active_count()
+    # fork() copies only the calling thread: a mutex another thread holds (an intra-op pool a torch
+    # build starts at import, an OpenMP runtime) stays locked forever in every forked trial. Refuse
+    # to serve rather than hand out trials that can deadlock; the scheduler then execs them.
+    threads = os_threads()
+    if threads > 1:
+        print("zygote: refusing to serve - %d threads after preload (fork is only safe from a "
+              "single-threaded process)" % threads, file=sys.stderr, flush=True)
+        return 4
+    _SITE_PATH[:] = _site_path()
     try:
         os.unlink(path)
     except FileNotFoundError:
@@ -246,6 +322,7 @@ class Zygote:
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(os.environ)
         env["PYTHONPATH"] = os.pathsep.join(p for p in (root, env.get("PYTHONPATH", "")) if p)
+        env["OPENBLAS_NUM_THREADS"] = "1"  # no BLAS thread pool in the forking process (_restore_blas_threads)
         self.proc = subprocess.Popen([sys.executable, "-m", "katib_amd.controller.zygote", "--socket", self.path,
                                       "--preload", preload], stdout=subprocess.PIPE, stdin=subprocess.DEVNULL,
                                      env=env, text=True)

@@ -219,6 +219,8 @@ PYBIND11_MODULE(_native, m) {
           py::arg("deadline") = 0.0)
       .def("kill_trial", &TrialRuntime::kill_trial, py::arg("trial"), py::arg("early_stop") = false)
       .def("stop_worker", &TrialRuntime::stop_worker)
+      .def("set_reap_orphans", &TrialRuntime::set_reap_orphans, py::arg("on"), py::arg("keep") = std::vector<int>{})
+      .def("orphans_reaped", &TrialRuntime::orphans_reaped)
       .def("shutdown", &TrialRuntime::shutdown)
       .def("poll",
            [](TrialRuntime& r, int timeout_ms) {

@@ -1,5 +1,6 @@
 #include "trial_runtime.hpp"
 
+#include <dirent.h>
 #include <fcntl.h>
 #include <signal.h>
 #include <sys/epoll.h>
@@ -680,6 +681,62 @@ void TrialRuntime::check_deadlines(std::vector<Event>&) {
   }
 }
 
+// Orphans re-parented to this process (child subreaper): zombie children that no table here knows.
+// waitpid(-1) would also take the exit status of a tracked trial or of a child some other code in
+// this process waits for, so the zombies are found by pid instead: /proc/<pid>/stat with this process
+// as parent and state Z, at most once a second. Children in this process's own process group are left
+// alone (every trial and worker leads its own group; a Popen / subprocess.run of the scheduler's own
+// code stays in ours and is reaped by its caller), as are the pids registered in keep_.
+void TrialRuntime::reap_orphans() {
+  if (!reap_orphans_) return;
+  double t = mono_now();
+  if (t < orphan_scan_at_) return;
+  orphan_scan_at_ = t + 1.0;
+  const pid_t self = getpid(), grp = getpgrp();
+  DIR* d = opendir("/proc");
+  if (!d) return;
+  std::vector<pid_t> zombies;
+  while (struct dirent* de = readdir(d)) {
+    const char* nm = de->d_name;
+    if (nm[0] < '1' || nm[0] > '9') continue;
+    char path[64];
+    snprintf(path, sizeof(path), "/proc/%s/stat", nm);
+    FILE* f = fopen(path, "re");
+    if (!f) continue;
+    char buf[512];
+    size_t len = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[len] = 0;
+    const char* rp = strrchr(buf, ')');  // comm may hold spaces and parentheses
+    if (!rp) continue;
+    char state = 0;
+    int ppid = 0, pgrp = 0;
+    if (sscanf(rp + 1, " %c %d %d", &state, &ppid, &pgrp) != 3) continue;
+    if (state != 'Z' || ppid != self || pgrp == grp) continue;
+    pid_t pid = static_cast<pid_t>(atoi(nm));
+    if (pid_trial_.count(pid) || pid_worker_.count(pid) || keep_.count(pid)) continue;
+    zombies.push_back(pid);
+  }
+  closedir(d);
+  for (pid_t pid : zombies) {
+    int st;
+    if (waitpid(pid, &st, WNOHANG) == pid) ++orphans_reaped_;
+  }
+}
+
+void TrialRuntime::set_reap_orphans(bool on, const std::vector<int>& keep) {
+  std::lock_guard<std::mutex> g(mu_);
+  reap_orphans_ = on;
+  keep_.clear();
+  for (int p : keep) keep_.insert(static_cast<pid_t>(p));
+  orphan_scan_at_ = 0.0;
+}
+
+long TrialRuntime::orphans_reaped() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return orphans_reaped_;
+}
+
 std::vector<Event> TrialRuntime::poll(int timeout_ms) {
   std::vector<Event> ev;
   struct epoll_event evs[64];
@@ -687,6 +744,7 @@ std::vector<Event> TrialRuntime::poll(int timeout_ms) {
   std::lock_guard<std::mutex> g(mu_);
   for (int i = 0; i < n; ++i) read_fd(evs[i].data.fd, ev);
   reap(ev);
+  reap_orphans();
   check_deadlines(ev);
   return ev;
 }

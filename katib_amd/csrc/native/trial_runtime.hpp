@@ -125,6 +125,13 @@ class TrialRuntime {
   bool worker_idle(int worker) const;
   bool worker_alive(int worker) const;
   int num_running() const;
+  // Child subreaper mode (controller/zygote.py): orphaned descendants of trials re-parent to this
+  // process. With `on`, poll() also reaps zombie children this runtime does not track, except the
+  // pids in `keep` (children that their own owner waits for, e.g. the fork server's Popen) and
+  // children in this process's own process group (a caller's subprocess.run / Popen waits for
+  // those itself). Returns the number of orphans reaped so far.
+  void set_reap_orphans(bool on, const std::vector<int>& keep);
+  long orphans_reaped() const;
 
  private:
   void track(const std::string& trial, pid_t pid, int fd, const std::string& log_path, const CollectorConfig& cfg,
@@ -142,6 +149,7 @@ class TrialRuntime {
   void trigger_early_stop(Proc& p, std::vector<Event>* ev);
   void reap(std::vector<Event>& ev);
   void check_deadlines(std::vector<Event>& ev);
+  void reap_orphans();
 
   std::shared_ptr<ObservationStore> store_;
   int epfd_ = -1;
@@ -152,6 +160,10 @@ class TrialRuntime {
   std::map<pid_t, std::string> pid_trial_;
   std::map<pid_t, int> pid_worker_;
   int next_worker_ = 0;
+  bool reap_orphans_ = false;
+  std::set<pid_t> keep_;
+  double orphan_scan_at_ = 0.0;
+  long orphans_reaped_ = 0;
   mutable std::mutex mu_;
 };
 

@@ -36,12 +36,6 @@ import torch.nn.functional as F
 from ..parallel.comm import Comm
 from .darts import BNState, DartsLayout, DartsNetwork, accuracy
 
-# KATIB_DARTS_DEBUG_SKIP_HESSIAN_PASSES=1 drops the two finite-difference forward/backward passes (the
-# step then computes a wrong architecture gradient). It exists only to measure how much of the step
-# those passes cost on their concurrent graph branches - the upper bound of what stacking both passes
-# into the same edge-batched launches could save (profiles/darts_hessian_stack_bound_r05.log).
-_SKIP_HESSIAN_PASSES = __import__("os").environ.get("KATIB_DARTS_DEBUG_SKIP_HESSIAN_PASSES") == "1"
-
 # validation batches merged per captured eval forward (eval-mode BN normalises every sample with
 # the running statistics, so k batches of n give the same losses and correct counts as one of k*n;
 # at B5 sizes the forward is launch / latency bound: per 128-image batch 0.54 ms at k = 1, 0.31 at 4,
@@ -80,6 +74,12 @@ class _Leaves:
 
 
 class DartsSearch:
+    # Measurement hook, never an environment switch: True drops the two finite-difference
+    # forward/backward passes (the alpha gradient is then WRONG). Only a profiling script sets it,
+    # on its own instance, to bound what stacking both passes into the same edge-batched launches
+    # could save (profiles/darts_hessian_stack_bound_r05.log); the step warns when it is on.
+    debug_skip_hessian_passes = False
+
     def __init__(self, layout: DartsLayout, device, comm: Optional[Comm] = None, seed: int = 2,
                  settings: Optional[Dict] = None, capture: bool = False, ops=None, sync_bn: bool = False):
         self.layout = layout
@@ -267,7 +267,12 @@ class DartsSearch:
                     self.bn_plus.buf, self.bn_zero.buf, self.net.momentum)
             # eps = 0.01/||dw'||; Wp = w + eps dw', Wm = Wp - 2 eps dw'; zeroed d(alpha)+-; BN snapshots
             K.optim_hessian_split(3, self.W, self.gWv, *args, nparts, *tail)
-            if _SKIP_HESSIAN_PASSES:  # measurement only (wrong alpha gradient): bounds what stacking could save
+            if self.debug_skip_hessian_passes:  # measurement only (wrong alpha gradient): see the class attribute
+                if not getattr(self, "_warned_skip", False):
+                    import warnings
+
+                    warnings.warn("DartsSearch.debug_skip_hessian_passes is set: the architecture gradient is wrong")
+                    self._warned_skip = True
                 K.optim_hessian_split(2, self.W, self.gWv, *args, nparts, *tail)
                 return
             main = torch.cuda.current_stream()

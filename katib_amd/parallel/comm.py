@@ -85,7 +85,8 @@ class Comm:
 
             self.xgmi = xgmi.create(self)
             if self.xgmi is not None:
-                self.xgmi_status = "passed"
+                # a self-test between ranks that share one GPU exercises IPC mappings, not an xGMI link
+                self.xgmi_status = "passed" if self.distinct_devices() == self.world_size else "passed (same device)"
             elif os.environ.get("KATIB_AMD_XGMI", "1") == "0":
                 self.xgmi_status = "disabled"
             elif int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world_size))) != self.world_size \
@@ -94,6 +95,32 @@ class Comm:
             else:
                 self.xgmi_status = "failed"  # mapping or self-test failed on some rank: RCCL fallback
         return self.xgmi is not None
+
+    def device_identity(self) -> str:
+        """Host + physical identity of this rank's device (UUID / PCI location, not the visible
+        index, which every rank of a shared-GPU rehearsal reports as 0)."""
+        import socket
+
+        if self.device.type != "cuda":
+            return "%s/cpu" % socket.gethostname()
+        p = torch.cuda.get_device_properties(self.device)
+        ident = str(getattr(p, "uuid", "") or "")
+        pci = tuple(getattr(p, k, -1) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+        if not ident or ident.strip("0-") == "":
+            ident = "pci%s" % (pci,)
+        return "%s/%s" % (socket.gethostname(), ident)
+
+    def distinct_devices(self) -> int:
+        """Collective: how many distinct physical devices the ranks drive (1 per rank on a real
+        multi-GPU node; 1 in total when every rank shares one GPU). Cached after the first call."""
+        if getattr(self, "_distinct", None) is None:
+            if self.world_size <= 1:
+                self._distinct = 1
+            else:
+                ids = [None] * self.world_size
+                dist.all_gather_object(ids, self.device_identity(), group=self.group)
+                self._distinct = len(set(ids))
+        return self._distinct
 
     def subgroup(self) -> "Comm":
         """Collective: the same ranks on a communicator of their own (a new process group of this

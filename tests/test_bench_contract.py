@@ -59,6 +59,10 @@ def test_bench_two_ranks_strong_scaling():
     assert abs(r["value"] - want) <= 0.01 * want
     assert abs(r["vs_baseline"] - r["value"] / r["baseline_b5_s"]) < 1e-3
     assert r["final_loss"] == r["final_loss"]  # finite
+    # DDP semantics (per-rank BN) timed next to the SyncBN headline, and the
+    # physical devices behind the ranks (both ranks on this one host's CPU: 1)
+    assert r["per_rank_bn_ms_per_step"] > 0 and r["per_rank_bn_search_wall_s"] > 0
+    assert r["distinct_devices"] == 1
 
 
 def test_bench_two_ranks_weak_scaling_label():
@@ -86,6 +90,7 @@ def test_bench_refuses_world_size_mismatch():
 def test_bench_per_rank_bn_label():
     r = _run(2, "--sync-bn", "0")
     assert r["batchnorm"] == "per rank" and r["config"]["sync_bn"] is False
+    assert r["per_rank_bn_ms_per_step"] == r["ms_per_step"]
 
 
 def test_bench_eight_ranks_syncbn_rehearsal():

@@ -161,9 +161,23 @@ def test_ui_token_cookie(tmp_path):
         assert ei.value.code == 401
         with pytest.raises(urllib.error.HTTPError):
             urllib.request.urlopen(base + "/?token=wrong")
-        r = urllib.request.urlopen(base + "/?token=s3cret")
+        import http.client
+
+        # the token query is answered with a 303 to "/" that sets the cookie (the token
+        # leaves the URL at once) and no-referrer; elsewhere it is refused
+        conn = http.client.HTTPConnection("127.0.0.1", api.port)
+        conn.request("GET", "/?token=s3cret")
+        r = conn.getresponse()
+        r.read()
+        assert r.status == 303 and r.headers["Location"] == "/"
+        assert r.headers["Referrer-Policy"] == "no-referrer"
         cookie = r.headers["Set-Cookie"]
         assert cookie.startswith("katib_amd_token=s3cret") and "HttpOnly" in cookie
+        conn.request("GET", "/katib/fetch_experiments?namespace=default&token=s3cret")
+        r = conn.getresponse()
+        r.read()
+        assert r.status == 401
+        conn.close()
         req = urllib.request.Request(base + "/katib/fetch_experiments?namespace=default",
                                      headers={"Cookie": cookie.split(";")[0]})
         assert urllib.request.urlopen(req).status == 200

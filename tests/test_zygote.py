@@ -128,3 +128,129 @@ def test_trials_before_the_server_is_up_are_execd(tmp_path):
         assert first.launcher == "exec"
     finally:
         m.shutdown()
+
+
+def _spawn_and_wait(z, argv, env, cwd):
+    r, w = os.pipe()
+    pid = z.spawn(argv, env, cwd, w)
+    os.close(w)
+    out = _read_all(r)
+    os.close(r)
+    _, st = os.waitpid(pid, 0)
+    return os.WEXITSTATUS(st), out
+
+
+def test_zygote_child_imports_resolve_like_exec(tmp_path):
+    """a forked trial resolves imports the way an exec'd interpreter would -
+    ``-m localmod`` from its working directory, ``script.py`` importing a sibling module, the trial
+    environment's PYTHONPATH - and the server's own launch directory does not leak in."""
+    work = tmp_path / "work"
+    (work / "lib").mkdir(parents=True)
+    (work / "localmod.py").write_text("import helper_in_cwd\nprint('M', helper_in_cwd.V)\n")
+    (work / "helper_in_cwd.py").write_text("V = 7\n")
+    sdir = tmp_path / "opt" / "x"
+    sdir.mkdir(parents=True)
+    (sdir / "train.py").write_text("import sibling, frompp\nprint('S', sibling.V, frompp.V)\n")
+    (sdir / "sibling.py").write_text("V = 11\n")
+    pp = tmp_path / "pp"
+    pp.mkdir()
+    (pp / "frompp.py").write_text("V = 13\n")
+    z = Zygote(str(tmp_path), preload="")
+    try:
+        env = dict(os.environ)
+        code, out = _spawn_and_wait(z, [sys.executable, "-m", "localmod"], env, str(work))
+        assert code == 0 and "M 7" in out, out
+        env_pp = dict(os.environ, PYTHONPATH=str(pp))
+        code, out = _spawn_and_wait(z, [sys.executable, str(sdir / "train.py")], env_pp, str(tmp_path))
+        assert code == 0 and "S 11 13" in out, out
+        # without the PYTHONPATH entry the import fails, as it would after exec
+        code, out = _spawn_and_wait(z, [sys.executable, str(sdir / "train.py")], dict(os.environ), str(tmp_path))
+        assert code == 1 and "ModuleNotFoundError" in out and "frompp" in out, out
+        code, out = _spawn_and_wait(z, [sys.executable, "-c", "import sys; print(repr(sys.path[0]))"], env, str(work))
+        assert code == 0 and out.strip() == "''", out
+    finally:
+        z.close()
+
+
+def test_zygote_trial_rereads_env_switches(tmp_path):
+    """module-level KATIB_* switches of preloaded katib_amd modules are read
+    under the TRIAL's environment, not frozen at the server's preload."""
+    pytest.importorskip("torch")
+    z = Zygote(str(tmp_path), preload="torch,katib_amd.workloads.mnist_mlp")
+    try:
+        probe = "import katib_amd.workloads.mnist_mlp as m; print('SETNONE', m._SET_TO_NONE)"
+        env = dict(os.environ, KATIB_MLP_SET_TO_NONE="0")
+        code, out = _spawn_and_wait(z, [sys.executable, "-c", probe], env, str(tmp_path))
+        assert code == 0 and "SETNONE False" in out, out
+        env["KATIB_MLP_SET_TO_NONE"] = "1"
+        code, out = _spawn_and_wait(z, [sys.executable, "-c", probe], env, str(tmp_path))
+        assert code == 0 and "SETNONE True" in out, out
+    finally:
+        z.close()
+
+
+def test_zygote_refuses_multithreaded_preload(tmp_path, monkeypatch):
+    """fork is only safe from a single-threaded process, so a preload that
+    leaves a thread running makes the server refuse to start (the scheduler then execs trials)."""
+    (tmp_path / "threadmod.py").write_text(
+        "import threading, time\nthreading.Thread(target=time.sleep, args=(30,), daemon=True).start()\n")
+    monkeypatch.setenv("PYTHONPATH", os.pathsep.join(p for p in (str(tmp_path), os.environ.get("PYTHONPATH", "")) if p))
+    with pytest.raises(RuntimeError, match="did not start"):
+        Zygote(str(tmp_path), preload="threadmod", timeout=60)
+    from katib_amd.controller.zygote import os_threads
+
+    assert os_threads() >= 1
+
+
+def _zombie_children():
+    me, out = os.getpid(), []
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open("/proc/%s/stat" % d) as f:
+                st = f.read()
+        except OSError:
+            continue
+        fields = st[st.rindex(")") + 2:].split()
+        if fields[0] == "Z" and int(fields[1]) == me:
+            out.append(int(d))
+    return out
+
+
+def test_orphaned_grandchild_is_reaped(tmp_path):
+    """with the fork server up the scheduler is a child subreaper, so a
+    trial's daemonised grandchild re-parents to it when the trial exits; the native runtime reaps
+    such orphans (it would otherwise stay a zombie for the daemon's lifetime)."""
+    from katib_amd.api.models import V1beta1Experiment
+    from katib_amd.controller.manager import Manager
+
+    pidfile = tmp_path / "gc.pid"
+    prog = ("import os, time\npid = os.fork()\nif pid == 0:\n    os.setsid()\n    if os.fork():\n        os._exit(0)\n"
+            "    open(%r, 'w').write(str(os.getpid()))\n    time.sleep(1.0)\n    os._exit(0)\n"
+            "os.waitpid(pid, 0)\nprint('loss=1.0', flush=True)\n" % str(pidfile))
+    c = {"name": "c", "command": [sys.executable, "-c", prog, "${trialParameters.x}"]}
+    exp = {"apiVersion": "kubeflow.org/v1beta1", "kind": "Experiment",
+           "metadata": {"name": "zy-orphan", "namespace": "default"},
+           "spec": {"objective": {"type": "minimize", "objectiveMetricName": "loss"},
+                    "algorithm": {"algorithmName": "random"}, "parallelTrialCount": 1, "maxTrialCount": 1,
+                    "parameters": [{"name": "x", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "2"}}],
+                    "trialTemplate": {"primaryContainerName": "c", "trialParameters": [{"name": "x", "reference": "x"}],
+                                      "trialSpec": {"apiVersion": "batch/v1", "kind": "Job", "spec": {
+                                          "template": {"spec": {"containers": [c]}}}}}}}
+    m = Manager(state_dir=str(tmp_path / "s"), num_devices=0, journal=False)
+    assert m.start_zygote(wait=True)
+    try:
+        m.create_experiment(V1beta1Experiment.from_k8s(exp))
+        m.run_until_complete("zy-orphan", timeout=60)
+        assert {r.launcher for r in m.runs.values()} == {"zygote"}
+        gc = int(pidfile.read_text())
+        t0 = time.time()
+        while time.time() - t0 < 15:
+            m.runtime.poll(100)
+            if m.runtime.orphans_reaped() >= 1 and gc not in _zombie_children() and not os.path.exists("/proc/%d" % gc):
+                break
+        assert m.runtime.orphans_reaped() >= 1
+        assert gc not in _zombie_children() and not os.path.exists("/proc/%d" % gc)
+    finally:
+        m.shutdown()
