@@ -27,5 +27,12 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
                      bool out_f32, int splitk, int M, int N, int K, hipStream_t st, const void* gelu_u = nullptr,
                      float* colpart = nullptr);
 
+// 256 x 256-tile, 8-wave ping-pong GEMM (gemm256.hip): the same operand layouts as launch_lt; C bf16
+// [M][N] (+ bias) with G = gelu_tanh(C) when G is given (forward fc), or fp32 slabs [splitk][M][N]
+// (out_f32). M, N multiples of 128 (a half-outside last tile is clamped), K of 64 * splitk.
+bool supported256(int M, int N, int K, int splitk);
+hipError_t launch_g256(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
+                       void* G, bool out_f32, int splitk, int M, int N, int K, hipStream_t st);
+
 }  // namespace gemm
 }  // namespace katib_hip

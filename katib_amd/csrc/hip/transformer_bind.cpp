@@ -315,9 +315,51 @@ void gemm_lt(const Tensor& A, bool a_mn, const Tensor& B, bool b_mn, const c10::
      "gemm_lt");
 }
 
+// C = op(A) op(B) on the 256 x 256-tile 8-wave ping-pong kernel (gemm256.hip): operand layouts as
+// gemm_lt; bf16 C (+ bias) with G = gelu_tanh(C) when G is given, or fp32 [splitk][M][N] slabs.
+void gemm256(const Tensor& A, bool a_mn, const Tensor& B, bool b_mn, const c10::optional<Tensor>& bias,
+             const Tensor& C, const c10::optional<Tensor>& G, int64_t splitk) {
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "gemm256: 2-D operands");
+  const int64_t M = a_mn ? A.size(1) : A.size(0), K = a_mn ? A.size(0) : A.size(1);
+  const int64_t N = b_mn ? B.size(1) : B.size(0), KB = b_mn ? B.size(0) : B.size(1);
+  TORCH_CHECK(KB == K, "gemm256: inner dimensions differ");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm256: dims");
+  TORCH_CHECK(katib_hip::gemm::supported256((int)M, (int)N, (int)K, (int)splitk),
+              "gemm256: M, N % 128 and K % (64 splitk) required");
+  chk(A, at::kBFloat16, M * K, "A");
+  chk(B, at::kBFloat16, N * K, "B");
+  const bool f32 = C.scalar_type() == at::kFloat;
+  if (f32) chk(C, at::kFloat, splitk * M * N, "C");
+  else {
+    TORCH_CHECK(splitk == 1, "gemm256: a bf16 output needs splitk 1");
+    chk(C, at::kBFloat16, M * N, "C");
+  }
+  const void* bp_ = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(!f32, "gemm256: bias only with a bf16 output");
+    chk(*bias, at::kBFloat16, N, "bias");
+    bp_ = bias->data_ptr();
+  }
+  void* gp = nullptr;
+  if (G.has_value() && G->defined()) {
+    TORCH_CHECK(!f32, "gemm256: the GELU output needs a bf16 C");
+    chk(*G, at::kBFloat16, M * N, "G");
+    gp = G->data_ptr();
+  }
+  ok(katib_hip::gemm::launch_g256(A.data_ptr(), (int)A.size(1), a_mn, B.data_ptr(), (int)B.size(1), b_mn, bp_,
+                                  C.data_ptr(), gp, f32, (int)splitk, (int)M, (int)N, (int)K, stream()),
+     "gemm256");
+}
+
 }  // namespace
 
 void register_transformer(py::module& m) {
+  m.def("gemm256", &gemm256, "C = op(A) op(B), 256^2 tile 8-wave ping-pong (bias / GELU / split-K fp32 slabs)",
+        py::arg("A"), py::arg("a_mn"), py::arg("B"), py::arg("b_mn"), py::arg("bias"), py::arg("C"),
+        py::arg("G") = py::none(), py::arg("splitk") = 1);
+  m.def("gemm256_supported", [](int64_t M, int64_t N, int64_t K, int64_t splitk) {
+    return M < (1 << 30) && N < (1 << 30) && K < (1 << 30) && katib_hip::gemm::supported256((int)M, (int)N, (int)K, (int)splitk);
+  }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splitk") = 1);
   m.def("gemm_lt", &gemm_lt, "bf16 C = op(A) op(B), layout-native operands (NN / TN / NT), split-K fp32 slabs",
         py::arg("A"), py::arg("a_mn"), py::arg("B"), py::arg("b_mn"), py::arg("bias"), py::arg("C"),
         py::arg("splitk") = 1, py::arg("gelu_u") = py::none(), py::arg("colpart") = py::none());
