@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""The 256x256-tile 8-wave ping-pong GEMM (gemm256.hip) against hipBLASLt and the 128^2 kernels on
+every GPT-2-small GEMM of a PBT member step (M = 16 x 1024 tokens by default): forward (A W^T, bias /
+GELU fused), dgrad (dY W, W read MN-major) and wgrad (dY^T X, both MN-major, split-K fp32 slabs +
+one row-sum launch, split chosen per shape by timing). hipBLASLt runs the same products through
+torch (addmm / mm on the strided views, and its split-K batched form for wgrad). Random data;
+interleaved rounds in one process, median of per-round means. ``--square`` adds 4096^3 / 8192^3."""
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from katib_amd import _hipload
+
+SHAPES = [("qkv", 2304, 768), ("proj", 768, 768), ("fc", 3072, 768), ("fc2", 768, 3072), ("lm_head", 50304, 768)]
+
+
+def timeit(fn, iters=20):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000.0 / iters
+
+
+def run(fns, rounds):
+    for f in fns.values():
+        timeit(f, 3)
+    t = {k_: [] for k_ in fns}
+    for _ in range(rounds):
+        for k_, f in fns.items():
+            t[k_].append(timeit(f))
+    return {k_: statistics.median(v) for k_, v in t.items()}
+
+
+def check(out, ref, what):
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 1e-2, (what, err)
+
+
+def main():
+    M = int(sys.argv[sys.argv.index("--tokens") + 1]) if "--tokens" in sys.argv else 16384
+    rounds = 5
+    k = _hipload.hipkern()
+    dev = torch.device("cuda", 0)
+    rows = []
+
+    def row(name, kind, m, n, kk, med, ours, libs, extra=None):
+        fl = 2.0 * m * n * kk
+        lib = min(med[x] for x in libs)
+        r = {"shape": name, "kind": kind, "M": m, "N": n, "K": kk, "gemm256_us": round(med[ours], 2),
+             "gemm256_tflops": round(fl / med[ours] / 1e6, 1), "hipblaslt_us": round(lib, 2),
+             "hipblaslt_tflops": round(fl / lib / 1e6, 1), "speedup_vs_hipblaslt": round(lib / med[ours], 3)}
+        for x in med:
+            if x not in (ours,) and x not in libs:
+                r[x + "_us"] = round(med[x], 2)
+        r.update(extra or {})
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+
+    for name, N, K in SHAPES:
+        g = torch.Generator(device=dev).manual_seed(N * 7 + K)
+        X = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+        W = (torch.randn(N, K, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+        b = (torch.randn(N, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+        dY = (torch.randn(M, N, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        Gg = torch.empty_like(C) if name == "fc" else None
+        bias = None if name == "lm_head" else b
+        # forward
+        k.gemm256(X, False, W, False, bias, C, Gg)
+        check(C, X.float() @ W.float().t() + (bias.float() if bias is not None else 0), name + " fwd")
+        fns = {"g256": lambda: k.gemm256(X, False, W, False, bias, C, Gg),
+               "lib": (lambda: torch.addmm(bias, X, W.t(), out=C)) if bias is not None else (lambda: torch.mm(X, W.t(), out=C))}
+        if N % 128 == 0:
+            fns["lt128"] = lambda: k.gemm_nt(X, W, bias, C, Gg)
+        row(name, "fwd", M, N, K, run(fns, rounds), "g256", ["lib"])
+        # dgrad dX[M][K] = dY[M][N] W[N][K]
+        dX = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+        k.gemm256(dY, False, W, True, None, dX)
+        check(dX, dY.float() @ W.float(), name + " dgrad")
+        fns = {"g256": lambda: k.gemm256(dY, False, W, True, None, dX), "lib": lambda: torch.mm(dY, W, out=dX)}
+        if N % 64 == 0 and K % 128 == 0:
+            fns["lt128"] = lambda: k.gemm_lt(dY, False, W, True, None, dX)
+        row(name, "dgrad", M, K, N, run(fns, rounds), "g256", ["lib"])
+        # wgrad dW[N][K] = dY^T X (split-K over the tokens)
+        dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+        splits = [s for s in (1, 2, 4, 8) if M % (64 * s) == 0]
+        parts = {s: torch.empty(s, N, K, device=dev, dtype=torch.float32) for s in splits if s > 1}
+
+        def wg(s):
+            if s == 1:
+                return lambda: k.gemm256(dY, True, X, True, None, dW)
+            p = parts[s]
+            return lambda: (k.gemm256(dY, True, X, True, None, p, None, s), k.reduce_rows(p.view(s, N * K), dW.view(-1)))
+
+        ref = dY.float().t() @ X.float()
+        for s in splits:
+            wg(s)()
+            check(dW, ref, "%s wgrad split %d" % (name, s))
+        ls = 1
+        while (N // 128) * (K // 128) * ls < 512 and M % (2 * ls) == 0 and M // (2 * ls) >= 1024:
+            ls *= 2
+        lpart = torch.empty(ls, N, K, device=dev, dtype=torch.float32)
+
+        def w_lib_split():
+            torch.bmm(dY.view(ls, M // ls, N).transpose(1, 2), X.view(ls, M // ls, K), out_dtype=torch.float32, out=lpart)
+            k.reduce_rows(lpart.view(ls, N * K), dW.view(-1))
+
+        fns = {"lib": lambda: torch.mm(dY.t(), X, out=dW), "lib_split": w_lib_split}
+        for s in splits:
+            fns["g256_s%d" % s] = wg(s)
+        med = run(fns, rounds)
+        best = min(splits, key=lambda s: med["g256_s%d" % s])
+        med["g256"] = med.pop("g256_s%d" % best)
+        row(name, "wgrad", N, K, M, med, "g256", ["lib", "lib_split"], {"splitk": best})
+        del X, W, dY, C, dX, dW, parts
+    if "--square" in sys.argv:
+        for S in (4096, 8192):
+            g = torch.Generator(device=dev).manual_seed(S)
+            A = (torch.rand(S, S, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+            B = (torch.rand(S, S, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+            C = torch.empty(S, S, device=dev, dtype=torch.bfloat16)
+            fns = {"g256": lambda: k.gemm256(A, False, B, False, None, C), "lib": lambda: torch.mm(A, B.t(), out=C)}
+            row("square%d" % S, "fwd", S, S, S, run(fns, rounds), "g256", ["lib"])
+    tot_ours = sum(r["gemm256_us"] for r in rows if not r["shape"].startswith("square"))
+    tot_lib = sum(r["hipblaslt_us"] for r in rows if not r["shape"].startswith("square"))
+    print("%-8s %-6s %6s %6s %6s %10s %8s %10s %8s %8s" % ("shape", "kind", "M", "N", "K", "g256 us", "TF/s",
+                                                           "hipBLASLt", "TF/s", "speedup"))
+    for r in rows:
+        print("%-8s %-6s %6d %6d %6d %10.1f %8.1f %10.1f %8.1f %8.3f" % (
+            r["shape"], r["kind"], r["M"], r["N"], r["K"], r["gemm256_us"], r["gemm256_tflops"], r["hipblaslt_us"],
+            r["hipblaslt_tflops"], r["speedup_vs_hipblaslt"]))
+    print(json.dumps({"gpt2_gemm_total_us": {"gemm256": round(tot_ours, 1), "hipblaslt_best": round(tot_lib, 1),
+                                             "speedup": round(tot_lib / tot_ours, 3)}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

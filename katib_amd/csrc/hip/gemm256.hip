@@ -107,8 +107,19 @@ __device__ __forceinline__ void bar() {
 }
 
 // 16 MFMAs: accumulator rows i0..i0+3 x columns j0..j0+1 over the K-tile's two 32-deep slices
+// The accumulators pass through empty asm statements before and after the cluster: the MFMA
+// intrinsic touches no memory, so without them LLVM sinks part of a cluster past the next barrier
+// (into the partner's compute segment) and the ping-pong collapses (seen in the .s: 6 of 16 MFMAs left).
+__device__ __forceinline__ void pin(f32x4 (&acc)[8][4], int i0, int j0) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i0 + i][j0 + j]));
+}
+
 __device__ __forceinline__ void quad(f32x4 (&acc)[8][4], const bf16x8 (&a)[2][4], const bf16x8 (&b)[2][4], int i0,
                                      int j0) {
+  pin(acc, i0, j0);
   __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
@@ -118,6 +129,7 @@ __device__ __forceinline__ void quad(f32x4 (&acc)[8][4], const bf16x8 (&a)[2][4]
       for (int j = 0; j < 2; ++j)
         acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[kk][j0 + j], acc[i0 + i][j0 + j], 0, 0, 0);
   __builtin_amdgcn_s_setprio(0);
+  pin(acc, i0, j0);
 }
 
 template <bool A_MN, bool B_MN, int EPI>

@@ -31,6 +31,9 @@ hipError_t gelu_fwd(const bf16* u, bf16* g, int64_t n, hipStream_t st);
 hipError_t gelu_bwd(const bf16* u, const bf16* dy, bf16* du, int64_t n, hipStream_t st);
 
 // Cross-entropy over the first V columns of rows of stride Vp (Vp % 8 == 0).
+// evaluation: per-row loss (lse - logit[tgt]) and top-1 hit (argmax == tgt, ties to the lowest index)
+hipError_t xent_eval(const bf16* logits, const int64_t* tgt, float* loss, float* hit, int N, int V, int Vp,
+                     hipStream_t st);
 hipError_t xent_fwd(const bf16* logits, const int64_t* tgt, float* loss, float* lse, int N, int V, int Vp,
                     hipStream_t st);
 // dlogits = (softmax - onehot) * (*gscale) * inv_n, written in place over logits (pad columns -> 0).

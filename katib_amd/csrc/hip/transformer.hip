@@ -367,6 +367,79 @@ __global__ __launch_bounds__(256) void xent_fwd_k(const u16* __restrict__ logits
   }
 }
 
+// Evaluation: per-row loss and top-1 hit in ONE pass over the bf16 logits row (the validation metric
+// PBT ranks members on) - instead of an fp32 copy of the logits, a softmax / NLL and an argmax reduce.
+// argmax ties resolve to the lowest index (torch.argmax's choice).
+__global__ __launch_bounds__(256) void xent_eval_k(const u16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                   float* __restrict__ loss, float* __restrict__ hit, int V, int Vp) {
+  __shared__ float sh[8];
+  __shared__ float shv[4];
+  __shared__ int shi[4];
+  const int row = blockIdx.x;
+  const u16* L = logits + (int64_t)row * Vp;
+  const int nch = Vp >> 3;
+  float m = -INFINITY, s = 0.f, bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = threadIdx.x; c < nch; c += 256) {
+    const u32x4 q = reinterpret_cast<const u32x4*>(L)[c];
+    float r[8], x[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r[2 * k] = lo2f(q[k]);
+      r[2 * k + 1] = hi2f(q[k]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (8 * c + e >= V) r[e] = -INFINITY;
+      x[e] = r[e] * kLog2e;
+      if (r[e] > bv) {  // strictly greater: the first index of a tie stays (columns ascend per thread)
+        bv = r[e];
+        bi = 8 * c + e;
+      }
+    }
+    float cm = x[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) cm = fmaxf(cm, x[e]);
+    const float mn = fmaxf(m, cm);
+    if (mn == -INFINITY) continue;
+    float cs = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs += exp2f(x[e] - mn);
+    s = s * exp2f(m - mn) + cs;
+    m = mn;
+  }
+  block_max_sum(m, s, sh);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(bv, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    if (v2 > bv || (v2 == bv && i2 < bi)) {
+      bv = v2;
+      bi = i2;
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+    shv[threadIdx.x >> 6] = bv;
+    shi[threadIdx.x >> 6] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bv = shv[0];
+    bi = shi[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w)
+      if (shv[w] > bv || (shv[w] == bv && shi[w] < bi)) {
+        bv = shv[w];
+        bi = shi[w];
+      }
+    const float l = (m + log2f(s)) * kLn2;
+    const int64_t t = tgt[row];
+    const float xt = (t >= 0 && t < V) ? bf2f(L[t]) : 0.f;
+    loss[row] = l - xt;
+    hit[row] = (t == (int64_t)bi) ? 1.f : 0.f;
+  }
+}
+
 __global__ __launch_bounds__(256) void xent_bwd_k(u16* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                   const float* __restrict__ lse, const float* __restrict__ gscale,
                                                   float inv_n, int V, int Vp) {
@@ -1097,6 +1170,13 @@ hipError_t gelu_bwd(const bf16* u, const bf16* dy, bf16* du, int64_t n, hipStrea
 hipError_t xent_fwd(const bf16* logits, const int64_t* tgt, float* loss, float* lse, int N, int V, int Vp,
                     hipStream_t st) {
   hipLaunchKernelGGL(xent_fwd_k, dim3(N), dim3(256), 0, st, reinterpret_cast<const u16*>(logits), tgt, loss, lse, V,
+                     Vp);
+  return hipGetLastError();
+}
+
+hipError_t xent_eval(const bf16* logits, const int64_t* tgt, float* loss, float* hit, int N, int V, int Vp,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(xent_eval_k, dim3(N), dim3(256), 0, st, reinterpret_cast<const u16*>(logits), tgt, loss, hit, V,
                      Vp);
   return hipGetLastError();
 }

@@ -136,6 +136,19 @@ void xent_fwd(const Tensor& logits, const Tensor& tgt, const Tensor& loss, const
      "xent_fwd");
 }
 
+void xent_eval(const Tensor& logits, const Tensor& tgt, const Tensor& loss, const Tensor& hit, int64_t V) {
+  TORCH_CHECK(logits.dim() == 2, "logits must be [N, Vp]");
+  const int64_t N = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(Vp % 8 == 0 && V > 0 && V <= Vp, "xent: Vp % 8 == 0 and 0 < V <= Vp");
+  chk(logits, at::kBFloat16, N * Vp, "logits");
+  TORCH_CHECK(tgt.is_cuda() && tgt.scalar_type() == at::kLong && tgt.is_contiguous() && tgt.numel() == N, "tgt");
+  chk(loss, at::kFloat, N, "loss");
+  chk(hit, at::kFloat, N, "hit");
+  ok(T_::xent_eval(bp(logits), tgt.data_ptr<int64_t>(), loss.data_ptr<float>(), hit.data_ptr<float>(), (int)N, (int)V,
+                   (int)Vp, stream()),
+     "xent_eval");
+}
+
 void xent_bwd(const Tensor& logits, const Tensor& tgt, const Tensor& lse, const Tensor& gscale, double inv_n,
               int64_t V) {
   TORCH_CHECK(logits.dim() == 2, "logits must be [N, Vp]");
@@ -379,6 +392,7 @@ void register_transformer(py::module& m) {
   m.def("ln_reduce", &ln_reduce, "sum LayerNorm parameter-gradient partials into bf16 grads (+ a bias gradient)",
         py::arg("part_g"), py::arg("part_b"), py::arg("dgamma"), py::arg("dbeta"), py::arg("part_r") = py::none(),
         py::arg("dbias") = py::none());
+  m.def("xent_eval", &xent_eval, "per-row cross-entropy loss + top-1 hit in one pass over bf16 logits");
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("xent_fwd", &xent_fwd, "vocabulary cross-entropy forward (per-row loss and lse)");

@@ -141,6 +141,11 @@ class TorchOps:
         loss, lse = self.xent_fwd(logits, tgt, V)
         return loss, lse, self.xent_bwd(logits, tgt, lse, gscale, V)
 
+    def xent_eval(self, logits, tgt, V):
+        """(summed loss, top-1 hits) over the rows: the validation metric (0-d fp32 tensors)."""
+        x = logits[:, :V].float()
+        return F.cross_entropy(x, tgt, reduction="sum"), (x.argmax(-1) == tgt).sum().float()
+
     # ---------------------------------------------------------------- GEMM helpers
     def linear(self, x, w, b):
         """x [M, K] . w[N, K]^T (+ b)."""
@@ -335,6 +340,15 @@ class HipOps:
             self.k.xent_fwd(logits, tgt, loss, lse, V)
             self.k.xent_bwd(logits, tgt, lse, gscale, 1.0 / N, V)
         return loss, lse, logits
+
+    def xent_eval(self, logits, tgt, V):
+        """(summed loss, top-1 hits) in one pass over the bf16 logits (xent_eval_k): no fp32 copy of the
+        logits, no softmax / argmax framework kernels on the PBT member's validation path."""
+        N = logits.shape[0]
+        out = torch.empty((2, -(-N // 4) * 4), device=logits.device, dtype=torch.float32)  # 16-byte aligned rows
+        self.k.xent_eval(logits, tgt, out[0, :N], out[1, :N], V)
+        s = out[:, :N].sum(1)
+        return s[0], s[1]
 
     def colsum(self, x, out):
         """Bias gradient: bf16 column sums of [M, N] (two-stage, fp32 partials)."""

@@ -287,9 +287,14 @@ def main(argv=None):
         for _ in range(args.eval_batches):
             o = torch.randint(n_train, len(toks) - T - 1, (B,), device=dev, generator=eg)
             xb, yb = batch(o)
-            logits = (model.forward(xb)[:, :cfg.vocab] if flat else model(xb)).float()
-            tot += float(F.cross_entropy(logits.view(-1, cfg.vocab), yb.reshape(-1), reduction="sum"))
-            correct += float((logits.view(-1, cfg.vocab).argmax(-1) == yb.reshape(-1)).sum())
+            if flat:  # one pass over the bf16 logits: loss + top-1 (HipOps.xent_eval)
+                l_, c_ = model.ops.xent_eval(model.forward(xb), yb.reshape(-1), cfg.vocab)
+                tot += float(l_)
+                correct += float(c_)
+            else:
+                logits = model(xb).float()
+                tot += float(F.cross_entropy(logits.view(-1, cfg.vocab), yb.reshape(-1), reduction="sum"))
+                correct += float((logits.view(-1, cfg.vocab).argmax(-1) == yb.reshape(-1)).sum())
             n += yb.numel()
     if ck:
         os.makedirs(ck, exist_ok=True)

@@ -99,3 +99,49 @@ def test_gemm_lt_bias_and_errors():
         k.gemm_lt(A, False, B[:, :100].contiguous(), True, None, C)  # N % 128
     with pytest.raises(RuntimeError):
         k.gemm_lt(A, False, B, True, None, C, 2)  # bf16 output with split-K
+
+
+@pytest.mark.parametrize("a_mn,b_mn", [(False, False), (False, True), (True, True), (True, False)])
+@pytest.mark.parametrize("M,N,K,splitk", [(256, 256, 64, 1), (512, 768, 768, 1), (384, 640, 192, 1),
+                                          (256, 2304, 3072, 1), (768, 768, 4096, 4), (1280, 384, 2048, 8)])
+def test_gemm256_layouts_match_fp32(a_mn, b_mn, M, N, K, splitk):
+    """256x256-tile 8-wave ping-pong GEMM (gemm256.hip): forward (K, K), dgrad (K, MN), wgrad (MN, MN)
+    and the fourth layout; one K-tile (K 64: the prologue-only path), M / N that leave a half-outside
+    last tile (384, 640, 1280: clamped staging, skipped stores), bf16 output or fp32 split-K slabs.
+    Asymmetric data so a transposed or mis-swizzled fragment fails."""
+    k = _k()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(M * 3 + N * 5 + K + 7 * splitk + 11 * a_mn + 13 * b_mn)
+    opA = torch.randn(M, K, device=dev, generator=g) + (torch.arange(M, device=dev)[:, None] % 7) * 0.1
+    opB = (torch.randn(K, N, device=dev, generator=g) + (torch.arange(N, device=dev)[None, :] % 5) * 0.05) * 0.05
+    opA, opB = opA.to(torch.bfloat16), opB.to(torch.bfloat16)
+    A = opA.t().contiguous() if a_mn else opA
+    B = opB.contiguous() if b_mn else opB.t().contiguous()
+    ref = opA.float() @ opB.float()
+    if splitk == 1:
+        C = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+        k.gemm256(A, a_mn, B, b_mn, None, C)
+        torch.testing.assert_close(C.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()) ** 0.5)
+    C32 = torch.full((splitk, M, N), float("nan"), device=dev, dtype=torch.float32)
+    k.gemm256(A, a_mn, B, b_mn, None, C32, None, splitk)
+    torch.testing.assert_close(C32.sum(0), ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 3072, 768), (256, 50304, 768), (384, 384, 128)])
+def test_gemm256_bias_gelu_epilogue(M, N, K):
+    """Forward epilogues: bias, and U = A W^T + b with G = gelu_tanh(U) (the fc layer); N = 50304 is
+    the padded GPT-2 vocabulary (a half-outside last column tile)."""
+    k = _k()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = (torch.randn(M, K, device=dev, generator=g) + (torch.arange(M, device=dev)[:, None] % 7) * 0.1).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    b = (torch.randn(N, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    U = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    G = torch.empty_like(U)
+    k.gemm256(A, False, W, False, b, U, G)
+    ref = A.float() @ W.float().t() + b.float()
+    torch.testing.assert_close(U.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()) ** 0.5)
+    torch.testing.assert_close(G.float(), F.gelu(U.float(), approximate="tanh"), rtol=2e-2, atol=1e-2)
+    with pytest.raises(RuntimeError):
+        k.gemm256(A, False, W[:100].contiguous(), False, None, U[:, :100].contiguous())  # N % 128

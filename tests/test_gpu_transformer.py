@@ -146,6 +146,29 @@ def test_cross_entropy(ops, V, Vp):
     assert V == Vp or float(df[:, V:].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("V,Vp", [(1000, 1024), (50257, 50304), (512, 512)])
+def test_cross_entropy_eval(ops, V, Vp):
+    """the validation loss + top-1 of the PBT member in one pass over the bf16
+    logits (xent_eval_k) against F.cross_entropy / argmax on the fp32 copy; includes tied maxima
+    (torch.argmax picks the lowest index) and pad columns that must be ignored."""
+    hip, ref = ops
+    g = _gen(V)
+    N = 131
+    logits = (torch.randn(N, Vp, device=DEV, generator=g) * 3).to(torch.bfloat16)
+    logits[:, V:] = 100.0
+    tgt = torch.randint(0, V, (N,), device=DEV, generator=g)
+    am = logits[:, :V].float().argmax(-1)
+    tgt[:40] = am[:40]  # hits
+    logits[40:50, 7] = logits[40:50, :V].float().max(-1).values.to(torch.bfloat16) + 1.0
+    logits[40:50, V - 3] = logits[40:50, 7]  # a tie: index 7 wins
+    tgt[40:45] = 7
+    tgt[45:50] = V - 3
+    lh, ch = hip.xent_eval(logits, tgt, V)
+    lr, cr = ref.xent_eval(logits, tgt, V)
+    assert abs(float(lh) - float(lr)) <= 1e-4 * abs(float(lr))
+    assert float(ch) == float(cr) and float(cr) >= 45
+
+
 @pytest.mark.parametrize("B,T,H", [(2, 128, 3), (1, 512, 2), (2, 256, 4)])
 def test_attention_fwd_bwd(ops, B, T, H):
     hip, ref = ops
