@@ -81,6 +81,9 @@ def main():
                          "its measured wall clock next to the projection (-1: on for the b5 config)")
     ap.add_argument("--floor", type=int, default=1,
                     help="N>1: rank 0 also times a dp1 step at the per-rank batch (per_rank_floor_ms)")
+    ap.add_argument("--hessian", default="stacked", choices=["stacked", "concurrent", "sequential"],
+                    help="finite-difference Hessian passes: stacked into shared launches (default), two concurrent "
+                         "graph branches, or one after the other")
     ap.add_argument("--per-rank-bn", type=int, default=1,
                     help="N>1 with SyncBN: also time the step with per-rank BatchNorm (DDP semantics) -> "
                          "per_rank_bn_ms_per_step")
@@ -145,7 +148,8 @@ def main():
     layout = DartsLayout(PRIMS, init_channels=cfg["init_channels"], num_layers=cfg["num_layers"],
                          num_nodes=cfg["num_nodes"], stem_multiplier=cfg["stem_multiplier"])
     sync_bn = bool(args.sync_bn) and comm.distributed
-    search = DartsSearch(layout, dev, comm, capture=bool(args.capture) and dev.type == "cuda", sync_bn=sync_bn)
+    search = DartsSearch(layout, dev, comm, capture=bool(args.capture) and dev.type == "cuda", sync_bn=sync_bn,
+                         hessian=args.hessian)
     n_train = 50000
     ds = cifar10(dev, n=n_train)
     train, valid = ds.subset(0, n_train // 2), ds.subset(n_train // 2, n_train)
@@ -227,7 +231,8 @@ def main():
     # the gradient buckets only), timed the same way on every rank
     per_rank_bn_ms = ms_step if (comm.distributed and not sync_bn) else None
     if comm.distributed and sync_bn and args.per_rank_bn:
-        prb = DartsSearch(layout, dev, comm, capture=bool(args.capture) and dev.type == "cuda", sync_bn=False)
+        prb = DartsSearch(layout, dev, comm, capture=bool(args.capture) and dev.type == "cuda", sync_bn=False,
+                          hessian=args.hessian)
         for i in range(args.warmup):
             (tx, ty), (vx, vy) = batches[i % len(batches)]
             prb.step(tx, ty, vx, vy)
@@ -251,7 +256,7 @@ def main():
     floor_ms = None
     if comm.distributed and args.floor and dev.type == "cuda":
         if comm.rank == 0:
-            solo = DartsSearch(layout, dev, Comm(device=dev), capture=bool(args.capture))
+            solo = DartsSearch(layout, dev, Comm(device=dev), capture=bool(args.capture), hessian=args.hessian)
             for i in range(max(args.warmup, 2)):
                 (tx, ty), (vx, vy) = batches[i % len(batches)]
                 solo.step(tx, ty, vx, vy)
@@ -327,7 +332,7 @@ def main():
                        "parallelism": "dp%d" % comm.world_size, "epochs": cfg["epochs"],
                        "steps_per_epoch": steps_per_epoch, "ops": args.ops, "hip_graph": bool(search.capture),
                        "allreduce": allreduce, "sync_bn": sync_bn,
-                       "second_order": True},
+                       "second_order": True, "hessian": search.hessian},
             "allreduce": allreduce,
             # one-shot xGMI all-reduce self-test verdict (None at one rank), the SyncBN fold path
             # (xgmi-oneshot / rccl-graph / host), and the cross-rank rendezvous one step issues
@@ -336,6 +341,7 @@ def main():
             "syncbn_path": search._hsync.path if getattr(search, "_hsync", None) is not None else None,
             "rendezvous_per_step": search.rendezvous_per_step if comm.distributed else 0,
             "rendezvous_in_graph": search.rendezvous_in_graph if comm.distributed else None,
+            "hessian_stack": search.stack_stats,
             "batchnorm": ("global batch (sync-bn)" if sync_bn else
                           ("per rank" if comm.distributed else "global batch")),
             "per_rank_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,

@@ -76,8 +76,19 @@ def main():
         # forward
         k.gemm256(X, False, W, False, bias, C, Gg)
         check(C, X.float() @ W.float().t() + (bias.float() if bias is not None else 0), name + " fwd")
-        fns = {"g256": lambda: k.gemm256(X, False, W, False, bias, C, Gg),
-               "lib": (lambda: torch.addmm(bias, X, W.t(), out=C)) if bias is not None else (lambda: torch.mm(X, W.t(), out=C))}
+        from katib_amd.ops.transformer import HipOps
+
+        hops = HipOps()
+
+        def lib_fwd():  # the same contract: the fc layer's GELU runs as its own kernel after hipBLASLt
+            if bias is None:
+                torch.mm(X, W.t(), out=C)
+                return
+            torch.addmm(bias, X, W.t(), out=C)
+            if Gg is not None:
+                hops.k.gelu_fwd(C, Gg)
+
+        fns = {"g256": lambda: k.gemm256(X, False, W, False, bias, C, Gg), "lib": lib_fwd}
         if N % 128 == 0:
             fns["lt128"] = lambda: k.gemm_nt(X, W, bias, C, Gg)
         row(name, "fwd", M, N, K, run(fns, rounds), "g256", ["lib"])
@@ -121,6 +132,18 @@ def main():
         med["g256"] = med.pop("g256_s%d" % best)
         row(name, "wgrad", N, K, M, med, "g256", ["lib", "lib_split"], {"splitk": best})
         del X, W, dY, C, dX, dW, parts
+    if "--ablate" in sys.argv:
+        for S, (n_, kk_) in ((8192, (8192, 8192)), (16384, (3072, 768))):
+            g = torch.Generator(device=dev).manual_seed(S)
+            A = (torch.rand(S, kk_, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+            B = (torch.rand(n_, kk_, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+            C = torch.empty(S, n_, device=dev, dtype=torch.bfloat16)
+            fns = {"v%d" % v: (lambda v=v: k.gemm256_ablate(A, B, C, v)) for v in range(5)}
+            med = run(fns, rounds)
+            fl = 2.0 * S * n_ * kk_
+            print(json.dumps({"ablate": [S, n_, kk_], **{x: [round(t, 1), round(fl / t / 1e6, 1)] for x, t in med.items()},
+                              "legend": "v0 full, v1 no DMA, v2 no frag reads, v3 neither, v4 no stagger; [us, TF/s]"}),
+                  flush=True)
     if "--square" in sys.argv:
         for S in (4096, 8192):
             g = torch.Generator(device=dev).manual_seed(S)

@@ -148,7 +148,7 @@ struct FoldArgs {  // buf[0][i] = sum_r buf[r][i]; rows 1.. zeroed
   float* buf; int n; int rows;
 };
 
-constexpr int kMaxSeg = 64;
+constexpr int kMaxSeg = 128;  // two stacked passes' folds in one launch
 struct FoldF64Args {  // per segment: p[i] = sum_{r < kRep} p[r*rstride + i]; replicas 1.. zeroed
   double* p[kMaxSeg]; int n[kMaxSeg]; int rstride[kMaxSeg]; int nseg; int total;
 };
@@ -182,7 +182,12 @@ struct FoldTail {
 };
 
 // Edge batches: one launch runs the same kernel for up to M edges of a DARTS node that share
-// shapes (blockIdx.y = edge). Passed by value in the kernarg segment (kept <= 4 KB).
+// shapes (blockIdx.y = edge). Passed by value in the kernarg segment: ROCm 7.2 passes by-value
+// arguments beyond 4 KB, eagerly and through captured graphs alike (scripts/kernarg_big_probe.hip:
+// 28,000 B checked on MI355X, profiles/kernarg_big_probe_r06.log), so the capacities hold the
+// entries of BOTH finite-difference Hessian passes (hip_darts.stacked_passes): the +eps and -eps
+// passes go out as one launch per kernel type. combine_fwd stays at 4: its entries are the edges of
+// ONE node summed into one output (register arrays sized by the capacity).
 template <typename A, int M>
 struct Batch {
   A e[M];
@@ -190,15 +195,15 @@ struct Batch {
   FoldTail tail;
   static constexpr int kCap = M;
 };
-using DwPwFwdBatch = Batch<DwPwFwdArgs, 8>;
+using DwPwFwdBatch = Batch<DwPwFwdArgs, 16>;
 using CombineFwdBatch = Batch<CombineFwdArgs, 4>;  // all edges of a node (B5: up to 4) in one launch
-using PwFwdBatch = Batch<PwFwdArgs, 16>;
-using PoolFwdBatch = Batch<PoolFwdArgs, 8>;
-using CombineBwdBatch = Batch<CombineBwdArgs, 4>;
-using PwBwdBatch = Batch<PwBwdArgs, 16>;  // a node's pointwise backward entries (2 sep stages + 2 dil per edge, <= 4 edges)
-using DwBwdBatch = Batch<DwBwdArgs, 20>;  // a node's stage-1 depthwise backward entries (<= 5 edges x 4: darts-gpu.yaml)
-using PoolBwdBatch = Batch<PoolBwdArgs, 8>;
-using DwPwMultiBatch = Batch<DwPwFwdArgs, 20>;  // a node's stage-1 (or stage-2) dw-pw entries (<= 5 edges x 4), mixed K/dil/S
+using PwFwdBatch = Batch<PwFwdArgs, 32>;
+using PoolFwdBatch = Batch<PoolFwdArgs, 16>;
+using CombineBwdBatch = Batch<CombineBwdArgs, 8>;
+using PwBwdBatch = Batch<PwBwdArgs, 32>;  // a node's pointwise backward entries (2 sep stages + 2 dil per edge, <= 4 edges), x2 stacked
+using DwBwdBatch = Batch<DwBwdArgs, 40>;  // a node's stage-1 depthwise backward entries (<= 5 edges x 4: darts-gpu.yaml), x2 stacked
+using PoolBwdBatch = Batch<PoolBwdArgs, 16>;
+using DwPwMultiBatch = Batch<DwPwFwdArgs, 40>;  // a node's stage-1 (or stage-2) dw-pw entries (<= 5 edges x 4, x2 stacked), mixed K/dil/S
 
 // Whole input gradient of one DARTS edge (except the stride-2 skip's FactorizedReduce, which
 // accumulates afterwards): the transposed depthwise convolutions of the separable stage-1 and the
@@ -213,13 +218,14 @@ struct EdgeBwdArgs {
   int N, C, H, W, Ho, Wo, S, nb, nblk;
 };
 using EdgeBwdBatch = Batch<EdgeBwdArgs, 4>;
-static_assert(sizeof(EdgeBwdBatch) <= 4096, "edge_bwd batch must fit the 4 KB kernarg segment");
-static_assert(sizeof(DwPwMultiBatch) <= 4096 && sizeof(PoolBwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096,
-              "kernel argument blocks must fit the 4 KB kernarg segment");
-static_assert(sizeof(DwPwFwdBatch) <= 4096 && sizeof(CombineFwdBatch) <= 4096 && sizeof(PwFwdBatch) <= 4096 && sizeof(PoolFwdBatch) <= 4096 &&
-                  sizeof(CombineBwdBatch) <= 4096 && sizeof(PwBwdBatch) <= 4096 && sizeof(DwBwdBatch) <= 4096 &&
-                  sizeof(PoolBwdBatch) <= 4096,
-              "kernel argument batches must fit the 4 KB kernarg budget");
+constexpr size_t kKernargMax = 24576;  // well inside the 28,000 B checked on MI355X
+static_assert(sizeof(EdgeBwdBatch) <= kKernargMax, "edge_bwd batch exceeds the kernarg budget");
+static_assert(sizeof(DwPwFwdBatch) <= kKernargMax && sizeof(CombineFwdBatch) <= kKernargMax &&
+                  sizeof(PwFwdBatch) <= kKernargMax && sizeof(PoolFwdBatch) <= kKernargMax &&
+                  sizeof(CombineBwdBatch) <= kKernargMax && sizeof(PwBwdBatch) <= kKernargMax &&
+                  sizeof(DwBwdBatch) <= kKernargMax && sizeof(PoolBwdBatch) <= kKernargMax &&
+                  sizeof(DwPwMultiBatch) <= kKernargMax,
+              "kernel argument batches exceed the kernarg budget");
 
 void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st);
 void launch_dw_bwd(const DwBwdBatch& b, int K, int dil, int S, bool prebn, hipStream_t st);
@@ -236,7 +242,7 @@ struct PoolFwdEntries {
   PoolFwdArgs e[PoolFwdBatch::kCap];
   int n;
 };
-static_assert(sizeof(DwPwMultiBatch) + sizeof(PoolFwdEntries) <= 4096, "kernarg segment");
+static_assert(sizeof(DwPwMultiBatch) + sizeof(PoolFwdEntries) <= kKernargMax, "kernarg budget");
 // false: nothing launched (not the fused narrow-layer plane path, or a self-fold tail is on)
 bool launch_dwpw_pool_multi(DwPwMultiBatch b, const PoolFwdBatch& pb, hipStream_t st);
 void launch_pool_bwd_multi(const PoolBwdBatch& b, hipStream_t st);

@@ -124,7 +124,7 @@ void launch_alpha_softmax(const AlphaSoftmaxArgs& a, hipStream_t st);
 // shares the row (cells of one type share their alphas) and written or added into the alpha
 // gradient rows: one launch replaces the replica fold, the row concatenation, the dtype copy, the
 // softmax backward and the gradient accumulation of the autograd path. Workgroup per row.
-constexpr int kAlphaGradMax = 64;
+constexpr int kAlphaGradMax = 128;  // both stacked Hessian passes' entries
 struct AlphaGradArgs {
   const double* g[kAlphaGradMax];
   int rstride[kAlphaGradMax];

@@ -114,7 +114,7 @@ void alpha_softmax(std::vector<Tensor> alphas, std::vector<Tensor> outs, std::op
 // entries: (g: f64 tensor holding kRep replicas of [K], rstride, softmax weight row [K], destination row [K]);
 // entries sharing a destination row are summed (grouped here; the kernel runs a workgroup per row)
 void alpha_grad(std::vector<py::tuple> entries, bool accumulate) {
-  TORCH_CHECK(!entries.empty() && (int)entries.size() <= O_::kAlphaGradMax, "alpha_grad: 1..64 entries");
+  TORCH_CHECK(!entries.empty() && (int)entries.size() <= O_::kAlphaGradMax, "alpha_grad: 1..kAlphaGradMax entries");
   O_::AlphaGradArgs p{};
   p.accumulate = accumulate;
   struct Ent { const double* g; int rs; const float* w; float* d; };

@@ -132,7 +132,9 @@ __device__ __forceinline__ void quad(f32x4 (&acc)[8][4], const bf16x8 (&a)[2][4]
   pin(acc, i0, j0);
 }
 
-template <bool A_MN, bool B_MN, int EPI>
+// ABL (measurement builds only, launch_g256_ablate): 1 no DMA in the K loop (tiles 0 / 1 re-used),
+// 2 no fragment reads in the K loop (registers of the first read re-used), 3 neither, 4 no stagger
+template <bool A_MN, bool B_MN, int EPI, int ABL = 0>
 __global__ void __launch_bounds__(512) g256_kernel(const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B,
                                                    int ldb, const uint16_t* __restrict__ bias, void* __restrict__ Cv,
                                                    uint16_t* __restrict__ G, int M, int N, int kslice) {
@@ -177,56 +179,70 @@ __global__ void __launch_bounds__(512) g256_kernel(const uint16_t* __restrict__ 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   bar();
-  if (g == 1) bar();
+  if (ABL != 4 && g == 1) bar();
+  constexpr bool kDma = ABL != 1 && ABL != 3, kReads = ABL != 2 && ABL != 3;
+  bf16x8 bq[2][4], a4[2][4];
+  if constexpr (!kReads) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bq[kk][j] = frag<B_MN>(lds + 2 * HALF + (wq >> 1) * HALF, cb + j * 16, kk, lane);
+        a4[kk][j] = frag<A_MN>(lds + g * HALF, j * 16, kk, lane);
+      }
+  }
 
   for (int kt = 0; kt < nk; ++kt) {
     const char* ia = lds + (kt & 1) * BUF + g * HALF;
     const char* ib = lds + (kt & 1) * BUF + 2 * HALF + (wq >> 1) * HALF;
-    bf16x8 bq[2][4], a4[2][4];
     // P1: B fragments + A rows 0-63; DMA A(t+1) half 0; quadrant (rows 0-63, cols 0-31)
+    if constexpr (kReads) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bq[kk][j] = frag<B_MN>(ib, cb + j * 16, kk, lane);
+        for (int j = 0; j < 4; ++j) bq[kk][j] = frag<B_MN>(ib, cb + j * 16, kk, lane);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a4[kk][i] = frag<A_MN>(ia, i * 16, kk, lane);
-    if (kt + 1 < nk) stageA(kt + 1, 0);
+        for (int i = 0; i < 4; ++i) a4[kk][i] = frag<A_MN>(ia, i * 16, kk, lane);
+    }
+    if (kDma && kt + 1 < nk) stageA(kt + 1, 0);
     bar();
     quad(acc, a4, bq, 0, 0);
     bar();
     // P2: DMA A(t+1) half 1; quadrant (rows 0-63, cols 32-63)
-    if (kt + 1 < nk) stageA(kt + 1, 1);
+    if (kDma && kt + 1 < nk) stageA(kt + 1, 1);
     bar();
     quad(acc, a4, bq, 0, 2);
     bar();
     // P3: A rows 64-127 (into the registers of rows 0-63); DMA B(t+2) half 0; quadrant (rows 64-127, cols 32-63)
+    if constexpr (kReads) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a4[kk][i] = frag<A_MN>(ia, 64 + i * 16, kk, lane);
-    if (kt + 2 < nk) stageB(kt + 2, 0);
+        for (int i = 0; i < 4; ++i) a4[kk][i] = frag<A_MN>(ia, 64 + i * 16, kk, lane);
+    }
+    if (kDma && kt + 2 < nk) stageB(kt + 2, 0);
     bar();
     quad(acc, a4, bq, 4, 2);
     bar();
     // P4: DMA B(t+2) half 1; retire tile t+1 (this wave's own DMA: the 4 of B(t+2) may stay in flight);
     // group 1 waits in its read segment, group 0 after its MFMAs - both before the barrier that precedes
     // the first reads of tile t+1
-    if (kt + 2 < nk) stageB(kt + 2, 1);
-    if (g == 1) {
+    if (kDma && kt + 2 < nk) stageB(kt + 2, 1);
+    if (ABL != 4 && g == 1) {
       if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bar();
     quad(acc, a4, bq, 4, 0);
-    if (g == 0) {
+    if (ABL == 4 || g == 0) {
       if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bar();
   }
-  if (g == 0) bar();  // group 0 catches up: every wave's reads and MFMAs issued, the LDS is free
+  if (ABL != 4 && g == 0) bar();  // group 0 catches up: every wave's reads and MFMAs issued, the LDS is free
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // epilogue through a wave-private 16 KB LDS tile (row-major), 16-byte row-segment stores
@@ -294,6 +310,25 @@ __global__ void __launch_bounds__(512) g256_kernel(const uint16_t* __restrict__ 
 }
 
 }  // namespace
+
+// measurement-only ablations of the NT bf16 kernel (benchmarks/bench_gemm256.py --ablate): wrong results
+hipError_t launch_g256_ablate(const void* A, const void* B, void* C, int M, int N, int K, int variant, hipStream_t st) {
+  if (!supported256(M, N, K, 1)) return hipErrorInvalidValue;
+  const dim3 grid(((M + T - 1) / T) * ((N + T - 1) / T), 1);
+  const uint16_t* a = static_cast<const uint16_t*>(A);
+  const uint16_t* b = static_cast<const uint16_t*>(B);
+#define G256A(V) \
+  hipLaunchKernelGGL((g256_kernel<false, false, 0, V>), grid, dim3(512), 0, st, a, K, b, K, nullptr, C, nullptr, M, N, K)
+  switch (variant) {
+    case 1: G256A(1); break;
+    case 2: G256A(2); break;
+    case 3: G256A(3); break;
+    case 4: G256A(4); break;
+    default: G256A(0); break;
+  }
+#undef G256A
+  return hipGetLastError();
+}
 
 bool supported256(int M, int N, int K, int splitk) {
   return M > 0 && N > 0 && K > 0 && splitk >= 1 && M % 128 == 0 && N % 128 == 0 && K % (BK * splitk) == 0;

@@ -33,6 +33,8 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
 bool supported256(int M, int N, int K, int splitk);
 hipError_t launch_g256(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
                        void* G, bool out_f32, int splitk, int M, int N, int K, hipStream_t st);
+// measurement only (wrong results): 1 no DMA in the K loop, 2 no fragment reads, 3 neither, 4 no stagger
+hipError_t launch_g256_ablate(const void* A, const void* B, void* C, int M, int N, int K, int variant, hipStream_t st);
 
 }  // namespace gemm
 }  // namespace katib_hip

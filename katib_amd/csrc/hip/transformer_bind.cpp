@@ -370,6 +370,10 @@ void register_transformer(py::module& m) {
   m.def("gemm256", &gemm256, "C = op(A) op(B), 256^2 tile 8-wave ping-pong (bias / GELU / split-K fp32 slabs)",
         py::arg("A"), py::arg("a_mn"), py::arg("B"), py::arg("b_mn"), py::arg("bias"), py::arg("C"),
         py::arg("G") = py::none(), py::arg("splitk") = 1);
+  m.def("gemm256_ablate", [](const Tensor& A, const Tensor& B, const Tensor& C, int64_t variant) {
+    ok(katib_hip::gemm::launch_g256_ablate(A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)A.size(0), (int)B.size(0),
+                                           (int)A.size(1), (int)variant, stream()), "gemm256_ablate");
+  }, "measurement only: gemm256 NT with parts of the K loop removed (wrong results)");
   m.def("gemm256_supported", [](int64_t M, int64_t N, int64_t K, int64_t splitk) {
     return M < (1 << 30) && N < (1 << 30) && K < (1 << 30) && katib_hip::gemm::supported256((int)M, (int)N, (int)K, (int)splitk);
   }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splitk") = 1);

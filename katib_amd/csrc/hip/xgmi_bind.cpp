@@ -126,7 +126,7 @@ class XgmiWorkspace {
   // sync (default true) are also summed over the ranks
   void fold_sync(std::vector<py::tuple> segs) {
     TORCH_CHECK(world_ > 0, "workspace not opened");
-    TORCH_CHECK(!segs.empty() && (int)segs.size() <= katib_hip::kMaxSeg, "1..kMaxSeg segments");
+    TORCH_CHECK(!segs.empty() && (int)segs.size() <= 64, "fold_sync: 1..64 segments (one sync-mask bit each)");
     katib_hip::FoldF64Args f{};
     uint64_t mask = 0;
     f.nseg = segs.size();

@@ -81,7 +81,8 @@ class DartsSearch:
     debug_skip_hessian_passes = False
 
     def __init__(self, layout: DartsLayout, device, comm: Optional[Comm] = None, seed: int = 2,
-                 settings: Optional[Dict] = None, capture: bool = False, ops=None, sync_bn: bool = False):
+                 settings: Optional[Dict] = None, capture: bool = False, ops=None, sync_bn: bool = False,
+                 hessian: str = "stacked"):
         self.layout = layout
         self.device = torch.device(device)
         self.comm = comm or Comm(device=self.device)
@@ -154,26 +155,30 @@ class DartsSearch:
         self.Aw, self.gAw = self._alpha_leaves(self.A, self.gA)
         self.Avw, _ = self._alpha_leaves(self.Av, self.gAv)
         self.W_detached = layout.views(self.W.detach())
-        # concurrent finite-difference Hessian passes (HIP path): w + eps dw' and w - eps dw' as
-        # two independent graph branches - their own weight copies, alpha-gradient leaves and BN
-        # running statistics, merged by one kernel after the join (KATIB_DARTS_HESS_CONCURRENT=0:
-        # the sequential in-place perturbation). Under SyncBN the side branch folds through a
-        # SyncBN of its own: the one-shot fold + cross-rank sum calls of one workspace must pair up
-        # in the same order on every rank, which two concurrently running branches sharing one
-        # workspace do not guarantee (the ranks deadlock); one workspace per branch keeps each
-        # branch's calls in program order. Without the one-shot path (host-side sums) the passes
-        # stay sequential.
-        self.hess_concurrent = (self.device.type == "cuda" and self.hd is not None
-                                and __import__("os").environ.get("KATIB_DARTS_HESS_CONCURRENT", "1") != "0")
+        # finite-difference Hessian passes (HIP path), w + eps dw' and w - eps dw', each with its own
+        # weight copy, alpha-gradient leaves and BN running statistics (merged by one kernel after both):
+        # * "stacked" (default): both passes recorded and issued as ONE pass of edge-batched launches
+        #   (hip_darts.stacked_passes: both entry lists per launch, one SyncBN rendezvous per fold pair);
+        # * "concurrent": two branches of the captured graph (side stream fork / join); under SyncBN the
+        #   side branch folds through a workspace of its own (calls of one workspace must pair up in the
+        #   same order on every rank, which two concurrently running branches do not guarantee);
+        # * "sequential": one in-place perturbation after the other (also the torch-ops path).
+        if hessian not in ("stacked", "concurrent", "sequential"):
+            raise ValueError("hessian must be stacked, concurrent or sequential")
+        if self.device.type != "cuda" or self.hd is None:
+            hessian = "sequential"
         self._hsync_side = None
-        if self.hess_concurrent and self.sync_bn:
+        if hessian == "concurrent" and self.sync_bn:
             if self._hsync is not None and self._hsync.capturable:
                 # collective, same order on every rank; on the RCCL path the side branch gets a
                 # communicator of its own (two concurrently running branches must not share one)
                 side = self.comm if self._hsync.ws is not None else self.comm.subgroup()
                 self._hsync_side = self.hd.SyncBN(side)
-            self.hess_concurrent = self._hsync_side is not None and self._hsync_side.capturable
-        if self.hess_concurrent:
+            if self._hsync_side is None or not self._hsync_side.capturable:
+                hessian = "sequential"
+        self.hessian = hessian
+        self.hess_concurrent = hessian == "concurrent"
+        if hessian in ("stacked", "concurrent"):
             self.Wp = torch.empty_like(self.W)
             self.Wm = torch.empty_like(self.W)
             self.Wp_views = layout.views(self.Wp)
@@ -181,8 +186,9 @@ class DartsSearch:
             self.Aw_p, _ = self._alpha_leaves(self.A, self.gAp)
             self.bn_plus = BNState(layout, dev)
             self.bn_zero = BNState(layout, dev)
+            self._one_side = torch.ones((), device=dev)  # the second pass's own unit upstream gradient
+        if hessian == "concurrent":
             self._side = torch.cuda.Stream(device=dev)
-            self._one_side = torch.ones((), device=dev)  # the side branch's own unit upstream gradient
         # fused optimizer kernels (csrc/hip/darts_optim.hip) on the HIP path:
         # virtual step, Hessian perturbations, Adam on alphas and clipped SGD are one launch each
         self.K = self.hd._K if self.hd is not None else None
@@ -194,6 +200,7 @@ class DartsSearch:
         self.rendezvous_in_graph = None
         self.static = None
         self._eval_graphs = {}  # (x shape, y shape, dtypes) -> (graph, static x, static y, [loss, top1, top5])
+        self.stack_stats = None  # launches issued / merged by the last stacked Hessian pair
 
     def _alpha_leaves(self, A, gA):
         rows, K = self.layout.n_alpha_rows, len(self.layout.prims)
@@ -260,7 +267,7 @@ class DartsSearch:
 
     def _seg_hessian(self, tx, ty):
         """+/- eps perturbations, FWD3/BWD3 and FWD4/BWD4 w.r.t. alphas only."""
-        if self.K is not None and self.hess_concurrent:
+        if self.K is not None and self.hessian in ("stacked", "concurrent"):
             K, args = self.K, (self.eps, self._parts)
             nparts = K.optim_sumsq(self.gWv, self._parts)
             tail = (self.gA, self.gAp, self.gAv, self.alpha_grad, self.lr, self.Wp, self.Wm, self.bn.buf,
@@ -273,6 +280,17 @@ class DartsSearch:
 
                     warnings.warn("DartsSearch.debug_skip_hessian_passes is set: the architecture gradient is wrong")
                     self._warned_skip = True
+                K.optim_hessian_split(2, self.W, self.gWv, *args, nparts, *tail)
+                return
+            if self.hessian == "stacked":
+                with self.hd.stacked_passes() as sp:
+                    with sp.pass_():
+                        loss, _ = self._loss(tx, ty, self.Wp_views, *self._arch(self.Aw_p), self.bn_plus)
+                        torch.autograd.backward(loss, grad_tensors=self._one_side, inputs=self.Aw_p)
+                    with sp.pass_():
+                        loss, _ = self._loss(tx, ty, self.Wm_views, *self._arch(self.Aw), self.bn)
+                        self._backward(loss, self.Aw)
+                self.stack_stats = sp.stats
                 K.optim_hessian_split(2, self.W, self.gWv, *args, nparts, *tail)
                 return
             main = torch.cuda.current_stream()

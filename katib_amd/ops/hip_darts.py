@@ -33,6 +33,7 @@ silently degrades to PyTorch ops.
 
 from __future__ import annotations
 
+import contextlib
 import importlib
 import weakref
 from collections import defaultdict
@@ -1452,6 +1453,108 @@ class _Network(torch.autograd.Function):
             _stem_bwd(st_stem, g[0], sinks, (key(conv), key(gamma), key(beta)), flags)
         sinks.finish(grads)
         return tuple(grads)
+
+
+# ------------------------------------------------------------------------- stacked passes
+# Two network passes of identical structure (the +eps / -eps finite-difference Hessian passes of the
+# architect step: same batch and shapes, their own weights, BN state and alpha-gradient leaves) are
+# RECORDED - every launch and SyncBN fold they would issue goes to a tape instead of the device - and
+# then replayed side by side: where both tapes hold the same edge-batched launch with identical
+# non-entry arguments, the two entry lists go out as ONE launch (capacities in darts_ops.h are sized
+# for two passes; by-value kernel arguments past 4 KB are fine on this stack); everything else is
+# issued pass by pass in tape order. Each pass keeps its own stream order and no cross-pass
+# dependency exists (disjoint buffers), so the result equals the two passes run one after the other.
+# Under SyncBN the twin folds become one fold + cross-rank sum: one rendezvous instead of two.
+# Reference: the architect's Hessian-vector product, examples/v1beta1/trial-images/darts-cnn-cifar10/
+# architect.py:98-135 (two forward/backward passes at w +- eps dw').
+_MERGE_CAP = {"dwpw_fwd": 16, "pw_fwd": 32, "pool_fwd": 16, "combine_bwd_reduce": 8, "pw_bwd": 32, "dw_bwd": 40,
+              "pool_bwd": 16, "dw_bwd_multi": 40, "dwpw_fwd_multi": 40, "pool_fwd_multi": 16,
+              "pool_bwd_multi": 16, "fold_f64": 128, "alpha_grad": 128, "__sync_fold__": 64}
+_QUERIES = {"selffold_ready", "max_blocks", "stamps_compiled", "REP", "ZBF16", "OPTIM_MAX_PARTS"}
+
+
+class _Recorder:
+    """Stands in for the extension module (or the SyncBN object) while a pass is recorded."""
+
+    def __init__(self, real, tape, sync=False):
+        self._real, self._tape, self._sync = real, tape, sync
+
+    def __getattr__(self, name):
+        attr = getattr(self._real, name)
+        if self._sync:
+            if name != "fold":
+                return attr
+            name = "__sync_fold__"
+        elif name in _QUERIES or not callable(attr):
+            return attr
+
+        def rec(*args, **kw):
+            self._tape.append((name, args, kw))
+            return None
+
+        return rec
+
+
+def _same(x, y) -> bool:
+    if torch.is_tensor(x) or torch.is_tensor(y):
+        return x is y
+    if isinstance(x, (list, tuple)) and isinstance(y, (list, tuple)):
+        return len(x) == len(y) and all(_same(a, b) for a, b in zip(x, y))
+    return x == y
+
+
+class stacked_passes:
+    """``with stacked_passes() as sp: with sp.pass_(): ...; with sp.pass_(): ...`` - the launches of
+    the two recorded passes are issued, merged where possible, when the outer block exits."""
+
+    def __init__(self):
+        self.tapes: List[list] = []
+        self.stats = {"launches": 0, "merged": 0}
+
+    def __enter__(self):
+        return self
+
+    @contextlib.contextmanager
+    def pass_(self):
+        global _K, _SYNC
+        tape: list = []
+        self.tapes.append(tape)
+        real_k, real_sync = _K, _SYNC
+        _K = _Recorder(real_k, tape)
+        if real_sync is not None:
+            _SYNC = _Recorder(real_sync, tape, sync=True)
+        try:
+            yield
+        finally:
+            _K, _SYNC = real_k, real_sync
+
+    def _call(self, name, args, kw):
+        self.stats["launches"] += 1
+        if name == "__sync_fold__":
+            _SYNC.fold(*args, **kw)
+        else:
+            getattr(_K, name)(*args, **kw)
+
+    def __exit__(self, et, ev, tb):
+        if et is not None:
+            return False
+        tapes = self.tapes
+        if len(tapes) != 2 or len(tapes[0]) != len(tapes[1]) or any(a[0] != b[0] for a, b in zip(*tapes)):
+            for t in tapes:  # not twins: replay one after the other
+                for name, args, kw in t:
+                    self._call(name, args, kw)
+            return False
+        for (name, aa, ka), (_, ab, kb) in zip(*tapes):
+            cap = _MERGE_CAP.get(name)
+            if (cap and aa and ab and isinstance(aa[0], list) and isinstance(ab[0], list)
+                    and len(aa[0]) + len(ab[0]) <= cap and len(aa) == len(ab) and _same(aa[1:], ab[1:])
+                    and _same(sorted(ka.items()), sorted(kb.items()))):
+                self.stats["merged"] += 1
+                self._call(name, (list(aa[0]) + list(ab[0]),) + tuple(aa[1:]), ka)
+            else:
+                self._call(name, aa, ka)
+                self._call(name, ab, kb)
+        return False
 
 
 def network_loss(spec: NetSpec, x, y, params: Sequence[torch.Tensor], an, ar, bn_of, training: bool,

@@ -611,3 +611,36 @@ def test_network_function_matches_per_cell_path(leaf_alphas):
     for name_, a, b in zip(["loss", "logits", "gW", "ga_n", "ga_r", "bn"], out[True], out[False]):
         _close(a, b, name_, rtol=5e-3, atol=1e-5)
     dops.set_backend("torch")
+
+
+@pytest.mark.parametrize("capture", [False, True])
+def test_stacked_hessian_passes_match_concurrent_and_sequential(capture):
+    """the +eps / -eps finite-difference passes recorded and issued as ONE pass of
+    edge-batched launches (hip_darts.stacked_passes) compute what the two concurrent graph branches
+    and the sequential in-place perturbation compute: weights, alphas and BN running statistics after
+    3 second-order steps; and most launches of the pair really merge."""
+    from katib_amd.models.darts import DartsLayout
+    from katib_amd.models.darts_search import DartsSearch
+    from katib_amd.ops import darts as dops
+
+    dev = torch.device("cuda", 0)
+    layout = DartsLayout(ALL, init_channels=4, num_layers=2, num_nodes=3, stem_multiplier=1)
+    gen = torch.Generator(device=dev).manual_seed(5)
+    batches = [(torch.randn(32, 3, 32, 32, device=dev, generator=gen), torch.randint(0, 10, (32,), device=dev, generator=gen),
+                torch.randn(32, 3, 32, 32, device=dev, generator=gen), torch.randint(0, 10, (32,), device=dev, generator=gen))
+               for _ in range(3)]
+    dops.set_backend("hip")
+    res = {}
+    for mode in ("stacked", "concurrent", "sequential"):
+        s = DartsSearch(layout, dev, capture=capture, hessian=mode)
+        assert s.hessian == mode
+        for b in batches:
+            s.step(*b)
+        torch.cuda.synchronize()
+        res[mode] = (s.W.clone(), s.A.clone(), s.bn.mean.clone(), s.bn.var.clone(), s.stack_stats)
+    dops.set_backend("torch")
+    st = res["stacked"][4]
+    assert st is not None and st["merged"] >= 40, st
+    for other in ("concurrent", "sequential"):
+        for name_, a, b in zip(["W", "alpha", "rm", "rv"], res["stacked"][:4], res[other][:4]):
+            _close(a, b, "%s vs %s: %s" % ("stacked", other, name_), rtol=1e-4, atol=1e-5)
