@@ -81,9 +81,9 @@ def main():
                          "its measured wall clock next to the projection (-1: on for the b5 config)")
     ap.add_argument("--floor", type=int, default=1,
                     help="N>1: rank 0 also times a dp1 step at the per-rank batch (per_rank_floor_ms)")
-    ap.add_argument("--hessian", default="stacked", choices=["stacked", "concurrent", "sequential"],
-                    help="finite-difference Hessian passes: stacked into shared launches (default), two concurrent "
-                         "graph branches, or one after the other")
+    ap.add_argument("--hessian", default="concurrent", choices=["stacked", "concurrent", "sequential"],
+                    help="finite-difference Hessian passes: two concurrent graph branches (default), stacked into "
+                         "shared launches (profiles/darts_hessian_stacked_ab_r06.log), or one after the other")
     ap.add_argument("--per-rank-bn", type=int, default=1,
                     help="N>1 with SyncBN: also time the step with per-rank BatchNorm (DDP semantics) -> "
                          "per_rank_bn_ms_per_step")

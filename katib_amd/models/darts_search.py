@@ -82,7 +82,7 @@ class DartsSearch:
 
     def __init__(self, layout: DartsLayout, device, comm: Optional[Comm] = None, seed: int = 2,
                  settings: Optional[Dict] = None, capture: bool = False, ops=None, sync_bn: bool = False,
-                 hessian: str = "stacked"):
+                 hessian: str = "concurrent"):
         self.layout = layout
         self.device = torch.device(device)
         self.comm = comm or Comm(device=self.device)
@@ -157,11 +157,12 @@ class DartsSearch:
         self.W_detached = layout.views(self.W.detach())
         # finite-difference Hessian passes (HIP path), w + eps dw' and w - eps dw', each with its own
         # weight copy, alpha-gradient leaves and BN running statistics (merged by one kernel after both):
-        # * "stacked" (default): both passes recorded and issued as ONE pass of edge-batched launches
-        #   (hip_darts.stacked_passes: both entry lists per launch, one SyncBN rendezvous per fold pair);
-        # * "concurrent": two branches of the captured graph (side stream fork / join); under SyncBN the
+        # * "concurrent" (default): two branches of the captured graph (side stream fork / join); under SyncBN the
         #   side branch folds through a workspace of its own (calls of one workspace must pair up in the
         #   same order on every rank, which two concurrently running branches do not guarantee);
+        # * "stacked": both passes recorded and issued as ONE pass of edge-batched launches
+        #   (hip_darts.stacked_passes: both entry lists per launch, one SyncBN rendezvous per fold pair);
+        #   measured 0.24 ms slower than "concurrent" on B5 (profiles/darts_hessian_stacked_ab_r06.log);
         # * "sequential": one in-place perturbation after the other (also the torch-ops path).
         if hessian not in ("stacked", "concurrent", "sequential"):
             raise ValueError("hessian must be stacked, concurrent or sequential")

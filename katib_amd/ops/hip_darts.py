@@ -1517,6 +1517,11 @@ class stacked_passes:
     @contextlib.contextmanager
     def pass_(self):
         global _K, _SYNC
+        if EDGE_BWD or JOINT_POOL or SELFFOLD:
+            # opt-in paths that branch on launch return values or attach per-launch fold tails:
+            # the passes run live, one after the other
+            yield
+            return
         tape: list = []
         self.tapes.append(tape)
         real_k, real_sync = _K, _SYNC
@@ -1539,11 +1544,17 @@ class stacked_passes:
         if et is not None:
             return False
         tapes = self.tapes
+        if not tapes:
+            return False
         if len(tapes) != 2 or len(tapes[0]) != len(tapes[1]) or any(a[0] != b[0] for a, b in zip(*tapes)):
             for t in tapes:  # not twins: replay one after the other
                 for name, args, kw in t:
                     self._call(name, args, kw)
             return False
+        self._replay_merged(tapes)
+        return False
+
+    def _replay_merged(self, tapes):
         for (name, aa, ka), (_, ab, kb) in zip(*tapes):
             cap = _MERGE_CAP.get(name)
             if (cap and aa and ab and isinstance(aa[0], list) and isinstance(ab[0], list)
@@ -1554,7 +1565,6 @@ class stacked_passes:
             else:
                 self._call(name, aa, ka)
                 self._call(name, ab, kb)
-        return False
 
 
 def network_loss(spec: NetSpec, x, y, params: Sequence[torch.Tensor], an, ar, bn_of, training: bool,

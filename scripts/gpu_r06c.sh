@@ -9,7 +9,7 @@ export TMPDIR=/tmp PYTHONPATH=$(pwd)
 L=gpurun_out/r06c.log
 : > $L
 echo "=== darts tests $(date +%T)" >> $L
-timeout -k 10 600 python -u -m pytest tests/test_gpu_darts.py tests/test_gpu_syncbn.py tests/test_gpu_graph_hygiene.py -x -q --timeout 300 --timeout-method thread -m gpu >> $L 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_darts.py -k "stacked or trajectory" -x -q --timeout 300 --timeout-method thread -m gpu >> $L 2>&1 || exit 1
 B5="--steps 40 --warmup 5 --trials 0 --b1 0 --experiment 0 --comparator-steps 0 --full-search 0"
 for rep in 1 2; do
   for h in stacked concurrent; do
@@ -18,6 +18,6 @@ for rep in 1 2; do
     python -c "import json; r=json.load(open('gpurun_out/b.json')); print(json.dumps({k: r[k] for k in ('ms_per_step','value','hessian_stack')}))" >> $L || exit 1
   done
 done
-echo "=== bench_gemm256 ablate $(date +%T)" >> $L
-timeout -k 10 400 python benchmarks/bench_gemm256.py --ablate >> $L 2>&1 || exit 1
+
+
 echo done >> $L

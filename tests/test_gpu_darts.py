@@ -643,4 +643,7 @@ def test_stacked_hessian_passes_match_concurrent_and_sequential(capture):
     assert st is not None and st["merged"] >= 40, st
     for other in ("concurrent", "sequential"):
         for name_, a, b in zip(["W", "alpha", "rm", "rv"], res["stacked"][:4], res[other][:4]):
-            _close(a, b, "%s vs %s: %s" % ("stacked", other, name_), rtol=1e-4, atol=1e-5)
+            # alphas move by a finite difference over eps = 0.01 / ||dw'||: float-atomic summation order
+            # (workgroup counts differ between the modes) shows up there first
+            tol = dict(rtol=1e-3, atol=5e-5) if name_ == "alpha" else dict(rtol=1e-4, atol=1e-5)
+            _close(a, b, "%s vs %s: %s" % ("stacked", other, name_), **tol)
