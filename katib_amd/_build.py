@@ -166,7 +166,6 @@ def build_hip(force: bool = False, verbose: bool = False, arch: str = "gfx950", 
         os.utime(cmd[-1], (t0, t0))
     link = [hipcc, "-shared", "-fPIC", f"--offload-arch={arch}"] + objs + [
         f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-        "-lhipblaslt",  # lt_epilogue.cpp: torch's own copy (torch/lib), not a second one from /opt/rocm
         f"-Wl,-rpath,{torch_lib}", "-o", out + ".tmp"]
     if verbose:
         print(" ".join(link), file=sys.stderr)

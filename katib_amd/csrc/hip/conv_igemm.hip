@@ -497,23 +497,16 @@ hipError_t launch_patch(const ConvGeom& g, const bf16* src, const bf16* wm, bf16
 }
 
 // 3x3 / s1 / p1 / d1 on 32x32 (4-row tiles), 16x16 (8-row tiles) or 8x8 (2 images per tile) planes
-// with 64-channel chunks on both sides; anything else keeps the im2col kernel. KATIB_CONV_PATCH=0
-// turns the path off (A/B); =1 limits it to the 16 / 32-wide planes; =3 adds 4x4 planes.
+// with 64-channel chunks on both sides; anything else keeps the im2col kernel. 4x4 planes (8 images
+// per tile) measured slower than the im2col kernel at ResNet-18's l4 (fwd 72 -> 102 us: 256 workgroups
+// of 9 serial tap stages for 512 channels).
 bool patch_ok(const ConvGeom& g, int Cin, int Cout) {
-  static const int mode = [] {
-    const char* e = getenv("KATIB_CONV_PATCH");
-    return e == nullptr ? 2 : atoi(e);
-  }();
-  if (mode == 0 || !(g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 && g.pw == 1 && g.dh == 1 &&
+  if (!(g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 && g.pw == 1 && g.dh == 1 &&
                      g.dw == 1 && g.OH == g.H && g.OW == g.W && Cin % 64 == 0 && Cout % 64 == 0))
     return false;
   if (g.W == 32 && g.H % 4 == 0) return true;
   if (g.W == 16 && g.H % 8 == 0) return true;
-  if (mode < 2) return false;
-  if (g.W == 8 && g.H == 8 && g.N % 2 == 0) return true;  // l3: fwd 44.7 -> 38.3, dgrad 48.8 -> 37.1 us
-  // 4x4 planes (8 images per tile) measured slower than the im2col kernel at ResNet-18's l4 (fwd 72 ->
-  // 102 us: 256 workgroups of 9 serial tap stages for 512 channels); opt-in with KATIB_CONV_PATCH=3
-  return mode >= 3 && g.W == 4 && g.H == 4 && g.N % 8 == 0;
+  return g.W == 8 && g.H == 8 && g.N % 2 == 0;  // l3: fwd 44.7 -> 38.3, dgrad 48.8 -> 37.1 us
 }
 
 template <bool FLIP>
@@ -561,10 +554,7 @@ hipError_t launch_fwd(const ConvGeom& g, const bf16* x, const bf16* w, bf16* y, 
 
 hipError_t launch_dgrad(const ConvGeom& g, const bf16* dy, const bf16* wt, bf16* dx, hipStream_t st, const bf16* add_d,
                         const bf16* add_y) {
-  static const bool phase_split = [] {
-    const char* e = getenv("KATIB_CONV_DGRAD_PHASES");
-    return e == nullptr || atoi(e) != 0;
-  }();
+  constexpr bool phase_split = true;
   if (patch_ok(g, g.K, g.C)) return dispatch_patch<true>(g, dy, wt, dx, g.K, g.C, st, add_d, add_y);
   // 1x1 strided (the shortcut): one class holds every tap, the unit-stride path is as fast (measured)
   if (phase_split && (g.sh > 1 || g.sw > 1) && g.dh == 1 && g.dw == 1 && g.R * g.S > 1) {
@@ -582,18 +572,10 @@ hipError_t launch_wgrad(const ConvGeom& g, const bf16* x, const bf16* dy, float*
   constexpr int BP = 64;
   // Split-K over pixels: every split adds its 128 x 128 fp32 tile into dw32 with atomics, so the
   // split count trades fill (workgroups) against atomic traffic (tiles x splits x 64 KB).
-  // KATIB_CONV_WGRAD_WG / _MIN_STAGES override the target workgroups / stages per workgroup.
   // Round-5 sweep on the ResNet-18 shapes (profiles/conv_graph_table_r05.log): 2048 WGs / >= 4
   // stages (the old policy) 1.64 ms for the nine layers' fwd+bwd, 512 / >= 16: 1.42 ms - the
   // 128 x 128 tiles of l2-l4 spent most of their time in atomics (l3 wgrad 110 -> 61 us).
-  static const int target_wg = [] {
-    const char* e = getenv("KATIB_CONV_WGRAD_WG");
-    return e ? atoi(e) : 512;
-  }();
-  static const int min_stages = [] {
-    const char* e = getenv("KATIB_CONV_WGRAD_MIN_STAGES");
-    return e ? atoi(e) : 16;
-  }();
+  constexpr int target_wg = 512, min_stages = 16;
   int splits = (target_wg + tiles - 1) / tiles;
   const int max_splits = (P + min_stages * BP - 1) / (min_stages * BP);  // >= min_stages stages per block
   splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);

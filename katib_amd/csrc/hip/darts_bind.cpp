@@ -106,7 +106,7 @@ GradSrc make_gs(const py::tuple& t, int C) {
 // ------------------------------------------------------------------------------------------------
 // Self-folding launches (darts_ops.h FoldTail): a per-device ring of zeroed arrival counters,
 // registered once from Python outside any graph capture (set_fold_counters); every launch that
-// produces replicated f64 sums takes the next counter. Off unless KATIB_HIP_SELFFOLD=1 (the
+// produces replicated f64 sums takes the next counter. Off unless set_selffold(true) (the
 // Python side then launches fold_f64 as before; selffold_ready() tells it which mode is live).
 // ------------------------------------------------------------------------------------------------
 struct CtrRing {
@@ -115,7 +115,7 @@ struct CtrRing {
   int cursor = 0;
 };
 CtrRing g_ring[64];
-bool g_selffold = getenv("KATIB_HIP_SELFFOLD") && atoi(getenv("KATIB_HIP_SELFFOLD")) != 0;  // measured slower
+bool g_selffold = false;  // self-folding launches (set_selffold): measured slower, tests only
 
 void set_selffold(bool on) { g_selffold = on; }
 
@@ -796,7 +796,6 @@ void register_dwconv(py::module& m);  // dwconv_bind.cpp
 void register_darts_optim(py::module& m);  // darts_optim_bind.cpp
 void register_darts_head(py::module& m);  // darts_head_bind.cpp
 void register_resnet(py::module& m);  // resnet_bind.cpp
-void register_lt_epilogue(py::module& m);  // lt_epilogue.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "katib_amd HIP kernels for gfx950 (DARTS edge ops, implicit-GEMM conv, transformer, xGMI all-reduce)";
@@ -826,14 +825,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fold_f64", &fold_f64);
   m.def("set_fold_counters", &set_fold_counters, "register the current device's self-fold counter ring (int32, zeroed)");
   m.def("selffold_ready", &selffold_ready, "launches on the current device fold their own f64 replicas");
-  m.def("set_selffold", &set_selffold, "turn self-folding launches on / off (default: KATIB_HIP_SELFFOLD)");
+  m.def("set_selffold", &set_selffold, "turn self-folding launches on / off (default off: measured slower)");
   m.attr("REP") = kRep;
   m.attr("ZBF16") = kZbf16;  // per-op intermediates stored as bf16 (the _hipkern_zbf16 variant)
   m.def("max_blocks", &max_blocks);
   register_xgmi(m);
   register_conv(m);
   register_transformer(m);
-  register_lt_epilogue(m);
   register_batchnorm(m);
   register_enas(m);
   register_dwconv(m);

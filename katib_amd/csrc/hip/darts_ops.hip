@@ -47,16 +47,12 @@ int max_blocks() {
 }
 void set_max_blocks(int n) { g_max_blocks = n; }
 
-// 4-pixels-per-thread output paths of the plane kernels, per channel group (KATIB_HIP_VEC_MASK,
-// read once): bit 0 dwpw_plane C = 4, bit 1 dwpw_plane C = 8, bit 2 dw_bwd_plane C = 4, bit 3
+// 4-pixels-per-thread output paths of the plane kernels, per channel group: bit 0 dwpw_plane C = 4, bit 1 dwpw_plane C = 8, bit 2 dw_bwd_plane C = 4, bit 3
 // dw_bwd_plane C = 8 (stride 1), bit 4 dw_bwd_plane stride-2 parity classes (any C). Default C = 4
 // only: at C = 8 the four-pixel register arrays cost more than the wider stores save, and the
 // stride-2 classes (a quarter of the multiply-adds) measured slower, B5 6.98 vs 6.80 ms
 // (profiles/darts_vec_ab_r04.log).
-int vec_mask() {
-  static const int m = getenv("KATIB_HIP_VEC_MASK") ? atoi(getenv("KATIB_HIP_VEC_MASK")) : 0x5;
-  return m;
-}
+int vec_mask() { return 0x5; }
 
 // phase-stamp arming (diagnostic build): the `call`-th launch of `kind` after stamps_arm()
 static int g_stamp_kind = 0, g_stamp_call = -1, g_stamp_seen = 0;

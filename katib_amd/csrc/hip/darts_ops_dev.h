@@ -70,7 +70,7 @@ __host__ __device__ constexpr int dwb_head_floats(int C) { return (2 * C * 25 + 
 __host__ __device__ constexpr int lds_pitch(int w) {
   return (((w + 3) & ~3) >> 2) & 1 ? ((w + 3) & ~3) : ((w + 3) & ~3) + 4;
 }
-// 4-pixels-per-thread output paths of the plane kernels (darts_ops.hip, KATIB_HIP_VEC_MASK)
+// 4-pixels-per-thread output paths of the plane kernels (darts_ops.hip vec_mask())
 int vec_mask();
 
 // s += p[r*rs], s2 += p[r*rs + off2] over r < rep replicas, 8 replicas (16 loads) in flight per

@@ -929,9 +929,9 @@ bool launch_edge_bwd(EdgeBwdBatch b, hipStream_t st) {
     for (int v = 0; v < 4; ++v)
       if (a.conv_mask & (1 << v)) bits |= (uintptr_t)a.dd[v];
     if (bits & 15) return false;
-    // bands: LDS per workgroup <= KATIB_HIP_EDGE_LDS_KB and >= KATIB_HIP_EDGE_WG workgroups per launch
-    static const int lds_kb = getenv("KATIB_HIP_EDGE_LDS_KB") ? atoi(getenv("KATIB_HIP_EDGE_LDS_KB")) : 48;
-    static const int min_wg = getenv("KATIB_HIP_EDGE_WG") ? atoi(getenv("KATIB_HIP_EDGE_WG")) : 1024;
+    // bands: LDS per workgroup <= lds_kb and >= min_wg workgroups per launch
+    constexpr int lds_kb = 48;
+    constexpr int min_wg = 1024;
     int nb = 1;
     while (nb < 32 && a.H % (2 * nb) == 0 &&
            (edge_bwd_floats(a, nb, CG) * 4 > (size_t)lds_kb * 1024 || N * nb * G * b.n < min_wg))
@@ -954,7 +954,7 @@ bool launch_edge_bwd(EdgeBwdBatch b, hipStream_t st) {
 void launch_pool_bwd_multi(const PoolBwdBatch& b, hipStream_t st) {
   int maxblk = 0;
   size_t lds = 0;
-  bool v4 = !getenv("KATIB_HIP_POOL_BWD_SCALAR");
+  bool v4 = true;
   auto al = [](const void* p, uintptr_t m) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & (m - 1)) == 0; };
   for (int i = 0; i < b.n; ++i) {
     const PoolBwdArgs& a = b.e[i];
@@ -994,7 +994,7 @@ static void launch_dw_bwd_plane_t(const DwBwdBatch& b, bool prebn, hipStream_t s
     nb *= 2;
   const size_t lds = sizeof(float) * dw_plane_floats(a, K, DIL, S, nb, accum, C);
   dim3 grid(a.N * nb * G, b.n);
-  static const int dbg = getenv("KATIB_HIP_DWB_DBG") ? atoi(getenv("KATIB_HIP_DWB_DBG")) : 0;  // timing probes
+  constexpr int dbg = 0;  // timing probes
   if (prebn) hipLaunchKernelGGL((dw_bwd_plane_kernel<K, DIL, S, true, C>), grid, dim3(256), lds, st, b, nb, dbg);
   else hipLaunchKernelGGL((dw_bwd_plane_kernel<K, DIL, S, false, C>), grid, dim3(256), lds, st, b, nb, dbg);
 }
@@ -1007,7 +1007,6 @@ static bool aligned16(const DwBwdBatch& b) {
 
 // plane path: narrow layers whose spatial sizes divide exactly by the stride
 static bool dw_plane_ok(const DwBwdBatch& b, int K, int DIL, int S) {
-  if (getenv("KATIB_HIP_DW_BWD_TILED")) return false;
   const DwBwdArgs& a = b.e[0];
   return (a.C == 4 || a.C == 8 || (a.C % 16 == 0 && a.C <= kMaxC)) && a.H == a.Ho * S && a.W == a.Wo * S &&
          a.pad == (K - 1) / 2 * DIL && a.Wo % 4 == 0 && aligned16(b);
@@ -1017,11 +1016,11 @@ template <int K, int DIL, int S>
 static void launch_dw_bwd_t(const DwBwdBatch& b, bool prebn, hipStream_t st) {
   const DwBwdArgs& a = b.e[0];
   if (dw_plane_ok(b, K, DIL, S)) {
-    // wide layers run in channel groups of KATIB_HIP_DWB_GROUP (4, 8 or 16) channels: 8 measured
+    // wide layers run in channel groups of grp (4, 8 or 16) channels: 8 measured
     // 48.2 vs 50.8 ms per darts-gpu.yaml step against 16 (half the LDS per band: fewer, taller bands),
     // and 4 beats 8 on the round-4 kernels (B5 6.37 vs 6.44 ms, default 41.98 vs 42.20 ms,
     // profiles/darts_dwb_group_ab_r04.log)
-    static const int grp = getenv("KATIB_HIP_DWB_GROUP") ? atoi(getenv("KATIB_HIP_DWB_GROUP")) : 4;
+    constexpr int grp = 4;
     if (a.C == 4 || grp == 4) return launch_dw_bwd_plane_t<K, DIL, S, 4>(b, prebn, st);
     if (a.C == 8 || grp == 8) return launch_dw_bwd_plane_t<K, DIL, S, 8>(b, prebn, st);
     return launch_dw_bwd_plane_t<K, DIL, S, 16>(b, prebn, st);
@@ -1040,7 +1039,7 @@ bool launch_dw_bwd_multi(DwBwdBatch b, hipStream_t st) {
   if (b.n < 1) return true;
   const DwBwdArgs& a0 = b.e[0];
   if (!(a0.C == 4 || a0.C == 8 || (a0.C % 16 == 0 && a0.C <= kMaxC)) || !aligned16(b)) return false;
-  static const int grp = getenv("KATIB_HIP_DWB_GROUP") ? atoi(getenv("KATIB_HIP_DWB_GROUP")) : 4;
+  constexpr int grp = 4;
   const int C = (a0.C == 4 || grp == 4) ? 4 : 8;  // channel groups as launch_dw_bwd_t
   if (a0.C % C) return false;
   int maxblk = 0;
@@ -1055,7 +1054,7 @@ bool launch_dw_bwd_multi(DwBwdBatch b, hipStream_t st) {
       return false;
     int nb = 1;
     const int G = a.C / C;
-    static const int min_wg = getenv("KATIB_HIP_DWB_MIN_WG") ? atoi(getenv("KATIB_HIP_DWB_MIN_WG")) : 1024;
+    constexpr int min_wg = 1024;
     while (nb < 8 && a.H % (2 * nb) == 0 &&
            (dw_plane_floats(a, K, DIL, S, nb, false, C) * 4 > 40 * 1024 || a.N * nb * G * b.n < min_wg))
       nb *= 2;

@@ -35,13 +35,13 @@ static bool try_dwpw_split_g(const DwPwFwdBatch& b, bool prebn, hipStream_t st, 
 
 // layers of 16..64 channels: depthwise on channel groups (dwpw_plane_kernel<..., PW = false>), then
 // the pointwise + BN statistics as an MFMA GEMM over d (pw_fwd_wave_kernel). At C = 16 this measured
-// faster than the fused plane kernel (50.7 vs 52.5 ms per darts-gpu.yaml step); KATIB_HIP_DWPW_SPLIT=0
+// faster than the fused plane kernel (50.7 vs 52.5 ms per darts-gpu.yaml step); the fused form
 // keeps the fused kernel there.
 template <int K, int DIL, int S>
 static bool try_dwpw_split(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
   const DwPwFwdArgs& a = b.e[0];
-  static const bool split16 = !getenv("KATIB_HIP_DWPW_SPLIT") || atoi(getenv("KATIB_HIP_DWPW_SPLIT")) > 0;
-  static const int grp = getenv("KATIB_HIP_DW_GROUP") ? atoi(getenv("KATIB_HIP_DW_GROUP")) : 8;
+  constexpr bool split16 = true;
+  constexpr int grp = 8;
   if (grp == 4) return try_dwpw_split_g<K, DIL, S, 4>(b, prebn, st, split16);
   if (grp == 8) return try_dwpw_split_g<K, DIL, S, 8>(b, prebn, st, split16);
   return try_dwpw_split_g<K, DIL, S, 16>(b, prebn, st, split16);
@@ -50,7 +50,7 @@ static bool try_dwpw_split(const DwPwFwdBatch& b, bool prebn, hipStream_t st) {
 template <int K, int DIL, int S, int CG>
 static bool try_dwpw_split_g(const DwPwFwdBatch& b, bool prebn, hipStream_t st, bool split16) {
   const DwPwFwdArgs& a = b.e[0];
-  if (getenv("KATIB_HIP_DWPW_TILED") || a.C % 16 != 0 || a.C > 64 || (a.C == 16 && !split16) ||
+  if (a.C % 16 != 0 || a.C > 64 || (a.C == 16 && !split16) ||
       (a.Ho * a.Wo) % 64 != 0 || a.W % 4 != 0)
     return false;
   for (int i = 0; i < b.n; ++i)
@@ -120,7 +120,7 @@ void launch_dwpw_fwd(const DwPwFwdBatch& b, int K, int dil, int S, bool prebn, h
 // per-entry band counts / variants of a dw-pw multi batch; false: the entries do not fit the plane kernels
 static bool dwpw_multi_prep(DwPwMultiBatch& b, bool& fused, int& maxblk, size_t& lds) {
   const int C = b.e[0].C, N = b.e[0].N;
-  static const bool split16 = !getenv("KATIB_HIP_DWPW_SPLIT") || atoi(getenv("KATIB_HIP_DWPW_SPLIT")) > 0;
+  constexpr bool split16 = true;
   fused = C == 4 || C == 8 || (C == 16 && !split16);
   const bool split = !fused && C % 16 == 0 && C <= 64;
   if (!fused && !split) return false;
@@ -199,10 +199,10 @@ bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st) {
 
 // workgroups per pool entry, and whether the LDS-staged 4-pixel path applies (lds: its plane bytes)
 static bool pool_fwd_prep(PoolFwdArgs* e, int n, int& maxblk, size_t& lds) {
-  // the LDS-staged 4-pixel path is opt-in (KATIB_HIP_POOL_FWD_V4=1): neutral on the B5 step and
+  // the LDS-staged 4-pixel path is off: neutral on the B5 step and
   // 42 -> 68 us per call on the darts-gpu.yaml step (a barrier round trip per staged plane),
   // profiles/darts_default_ab_r04.log
-  static const bool v4_on = getenv("KATIB_HIP_POOL_FWD_V4") != nullptr && atoi(getenv("KATIB_HIP_POOL_FWD_V4")) > 0;
+  constexpr bool v4_on = false;  // LDS-staged 4-pixel pool forward: measured slower (42 -> 68 us)
   bool v4 = v4_on;
   auto al = [](const void* p, uintptr_t m) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & (m - 1)) == 0; };
   maxblk = 0;
@@ -228,7 +228,7 @@ void launch_pool_fwd_multi(PoolFwdBatch b, hipStream_t st) {
 }
 
 bool launch_dwpw_pool_multi(DwPwMultiBatch b, const PoolFwdBatch& pb, hipStream_t st) {
-  static const bool off = getenv("KATIB_HIP_DWPW_POOL_SPLIT") != nullptr;
+  constexpr bool off = false;
   if (off || b.n < 1 || pb.n < 1 || b.tail.ctr || pb.tail.ctr || b.n + pb.n > 65535) return false;
   const int C = b.e[0].C;
   bool fused;
@@ -252,7 +252,7 @@ template <int CI, int CO>
 static bool try_pw_fwd_wave(const PwFwdBatch& b, hipStream_t st) {
   const PwFwdArgs& a = b.e[0];
   constexpr int BO = CO / 16;
-  if (a.Cin != CI || a.Cout != CO || (a.Ho * a.Wo) % 64 != 0 || getenv("KATIB_HIP_PW_FWD_TILED")) return false;
+  if (a.Cin != CI || a.Cout != CO || (a.Ho * a.Wo) % 64 != 0) return false;
   for (int e = 0; e < b.n; ++e) {  // 16-byte loads (flat input) and stores
     const PwFwdArgs& x = b.e[e];
     const bool flat = !x.relu || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);

@@ -501,26 +501,17 @@ static bool try_pw_bwd_px(const PwBwdBatch& b, hipStream_t st) {
   const PwBwdArgs& a = b.e[0];
   if (a.Cin != CI || a.Cout != CO) return false;
   const int total = a.N * a.Ho * a.Wo;
-  // the 4-pixel vector path measured slower at C = 8 (register pressure: 21.7 vs 17.6 us) and
-  // neutral at C = 4 on MI355X; it stays selectable for experiments (KATIB_HIP_PW_PX_V4=1)
-  bool v4 = CI * CO <= 64 && (a.Ho * a.Wo) % 4 == 0 && getenv("KATIB_HIP_PW_PX_V4");
-  for (int e = 0; e < b.n && v4; ++e) {
-    const PwBwdArgs& x = b.e[e];
-    const bool m1ok = x.mode == 0 || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);
-    const uintptr_t bits = (uintptr_t)x.gs.z | (uintptr_t)x.gs.g | (x.mode == 0 ? (uintptr_t)x.ain : (uintptr_t)x.x) |
-                           (uintptr_t)(x.mode == 0 ? x.dd : x.gx);
-    v4 = m1ok && (bits & 15) == 0 && x.co_off % 4 == 0;
-  }
-  const int per_edge = std::max(1, std::min(((v4 ? total / 4 : total) + 255) / 256, max_blocks() / std::max(b.n, 1)));
-  if (v4) hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO, true>), dim3(per_edge, b.n), dim3(256), 0, st, b);
-  else hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO, false>), dim3(per_edge, b.n), dim3(256), 0, st, b);
+  // one pixel per thread: the 4-pixel vector form (pw_bwd_px_kernel<..., true>) measured slower at C = 8
+  // (register pressure: 21.7 vs 17.6 us) and neutral at C = 4 on MI355X, so it is not launched
+  const int per_edge = std::max(1, std::min((total + 255) / 256, max_blocks() / std::max(b.n, 1)));
+  hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO, false>), dim3(per_edge, b.n), dim3(256), 0, st, b);
   return true;
 }
 
 template <int CI, int CO>
 static bool try_pw_bwd_wave(const PwBwdBatch& b, hipStream_t st) {
   const PwBwdArgs& a = b.e[0];
-  if (a.Cin != CI || a.Cout != CO || (a.Ho * a.Wo) % 64 != 0 || getenv("KATIB_HIP_PW_BWD_TILED")) return false;
+  if (a.Cin != CI || a.Cout != CO || (a.Ho * a.Wo) % 64 != 0) return false;
   for (int e = 0; e < b.n; ++e) {  // 16-byte operand loads
     const PwBwdArgs& x = b.e[e];
     const bool flat = x.mode == 0 || (x.S == 1 && x.off == 0 && x.H == x.Ho && x.W == x.Wo);

@@ -17,14 +17,14 @@
 //     (ping-pong), and the DMA of tile k+1 / k+2 stays in flight across the barriers: each wave waits
 //     for its own loads with a counted vmcnt once per K-tile (never __syncthreads, whose fence would
 //     drain the DMA).
-//   * Phase plan of K-tile t (buffer t & 1; the DMA runs TWO tiles ahead, into the buffer being read):
-//     P1 reads B columns 0-31 + A rows 0-63 (12 ds_read_b128); P2 DMA A(t+2) rows 0-63; P3 reads A rows
-//     64-127, DMA B(t+2) half 0, and the wait that retires tile t+1 (vmcnt 4: its DMA had >= 3 phases
-//     to land); P4 reads tile t+1's B columns 32-63 (their registers are free after P3), DMA B(t+2)
-//     half 1 + A(t+2) rows 64-127. 64 fragment VGPRs + 128 accumulators. A_g is read by group g alone;
-//     B_g by both groups, free for group 0's DMA only from P3 (group 1's P1 reads retire in the segment
-//     that ends P2). MN-major A (wgrad): its 1 KB blocks span all 128 columns, so all of A(t+2) waits
-//     for P4.
+//   * Phase plan of K-tile t (buffer t & 1): P1 reads all B fragments + A rows 0-63 (16 ds_read_b128),
+//     DMA A(t+1) half 1; P2 MFMAs only; P3 reads A rows 64-127 (into the same registers), DMA B(t+2)
+//     half 0; P4 DMA B(t+2) half 1 + A(t+2) half 0 and the wait that retires tile t+1 (vmcnt 6: three
+//     half-blocks of DMA stay in flight; A(t+1) had three phases to land). 64 fragment VGPRs + 128
+//     accumulators. A_g is read by group g alone (free once its P3 reads retired); B_g by both groups,
+//     free for group 0's DMA only from P3 (group 1's P1 reads retire in the segment that ends P2).
+//     Measured alternative (profiles/gemm256_r06.log): the DMA two tiles ahead with the next tile's B
+//     fragments read in P4 - 8192^3 equal, the MN-major GPT-2 shapes 10 % slower.
 //   * K-major half-tile image: 128 rows x 128 B, 16-byte chunk c of row r at slot c ^ ((r >> 1) & 7):
 //     every 16-lane phase of a ds_read_b128 fragment read then hits 16 distinct slots of the 256-byte
 //     bank row (conflict-free; the (r & 7) form of gemm_bf16.hip is 2-way). The swizzle is applied to
@@ -162,41 +162,24 @@ __global__ void __launch_bounds__(512) g256_kernel(const uint16_t* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // K-major A: part p = image rows [64 p, 64 p + 64) (blocks 8 p ..), so rows 0-63 of the next-but-one
-  // tile can land as soon as this tile's rows 0-63 are read (P1); MN-major A: any split (each 1 KB block
-  // holds 4 k rows of all 128 columns)
   auto stageA = [&](int kt, int part) {
     char* img = lds + (kt & 1) * BUF + g * HALF;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      stage_blk<A_MN>(A, lda, am0, kbeg + kt * BK, img, A_MN ? wq * 4 + part * 2 + i : part * 8 + wq * 2 + i, lane);
+    for (int i = 0; i < 2; ++i) stage_blk<A_MN>(A, lda, am0, kbeg + kt * BK, img, wq * 4 + part * 2 + i, lane);
   };
   auto stageB = [&](int kt, int part) {
     char* img = lds + (kt & 1) * BUF + 2 * HALF + g * HALF;
 #pragma unroll
     for (int i = 0; i < 2; ++i) stage_blk<B_MN>(B, ldb, bn0, kbeg + kt * BK, img, wq * 4 + part * 2 + i, lane);
   };
-  auto readB = [&](const char* ib, int j0, bf16x8 (&b)[2][4]) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = j0; j < j0 + 2; ++j) b[kk][j] = frag<B_MN>(ib, cb + j * 16, kk, lane);
-  };
   constexpr bool kDma = ABL != 1 && ABL != 3, kReads = ABL != 2 && ABL != 3;
-  // DMA issued after the last one of tile t+1 (P4 of tile t-1) when tile t+1 is waited for in P3 of tile t
-  constexpr int kAfter = A_MN ? 2 : 4;
   auto wait_next = [&](int kt) {
-    if (kt + 2 < nk) {
-      if constexpr (kAfter == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
-  // prologue: tiles 0 and 1 (16 DMA per thread); wait for tile 0 (tile 1's 8 may stay in flight), read
-  // tile 0's B fragments of columns 32-63 (P4 of the previous tile reads them in the loop), then group 1
-  // falls one barrier behind
+  // prologue: B(0), A(0), B(1), A(1) half 0; wait for tile 0 (the 6 DMA of tile 1 may stay in flight),
+  // then group 1 falls one barrier behind
   stageB(0, 0);
   stageB(0, 1);
   stageA(0, 0);
@@ -205,15 +188,13 @@ __global__ void __launch_bounds__(512) g256_kernel(const uint16_t* __restrict__ 
     stageB(1, 0);
     stageB(1, 1);
     stageA(1, 0);
-    stageA(1, 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   bar();
-  bf16x8 bq[2][4], a4[2][4];
-  readB(lds + 2 * HALF + (wq >> 1) * HALF, 2, bq);
   if (ABL != 4 && g == 1) bar();
+  bf16x8 bq[2][4], a4[2][4];
   if constexpr (!kReads) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -227,25 +208,27 @@ __global__ void __launch_bounds__(512) g256_kernel(const uint16_t* __restrict__ 
   for (int kt = 0; kt < nk; ++kt) {
     const char* ia = lds + (kt & 1) * BUF + g * HALF;
     const char* ib = lds + (kt & 1) * BUF + 2 * HALF + (wq >> 1) * HALF;
-    // P1: B columns 0-31 + A rows 0-63 of tile t; quadrant (rows 0-63, cols 0-31)
+    // P1: all B fragments + A rows 0-63; DMA A(t+1) half 1; quadrant (rows 0-63, cols 0-31)
     if constexpr (kReads) {
-      readB(ib, 0, bq);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bq[kk][j] = frag<B_MN>(ib, cb + j * 16, kk, lane);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < 4; ++i) a4[kk][i] = frag<A_MN>(ia, i * 16, kk, lane);
     }
+    if (kDma && kt + 1 < nk) stageA(kt + 1, 1);
     bar();
     quad(acc, a4, bq, 0, 0);
     bar();
-    // P2: DMA A(t+2) rows 0-63 (K-major A: read in P1); quadrant (rows 0-63, cols 32-63)
-    if (!A_MN && kDma && kt + 2 < nk) stageA(kt + 2, 0);
+    // P2: quadrant (rows 0-63, cols 32-63)
     bar();
     quad(acc, a4, bq, 0, 2);
     bar();
     // P3: A rows 64-127 (into the registers of rows 0-63); DMA B(t+2) half 0 (B of tile t was read in P1);
-    // the wait that retires tile t+1 (group 1 in its read segment, group 0 after its MFMAs: both before
-    // the barrier that precedes P4's reads of tile t+1); quadrant (rows 64-127, cols 32-63)
+    // quadrant (rows 64-127, cols 32-63)
     if constexpr (kReads) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -253,21 +236,21 @@ __global__ void __launch_bounds__(512) g256_kernel(const uint16_t* __restrict__ 
         for (int i = 0; i < 4; ++i) a4[kk][i] = frag<A_MN>(ia, 64 + i * 16, kk, lane);
     }
     if (kDma && kt + 2 < nk) stageB(kt + 2, 0);
-    if (ABL == 4 || g == 1) wait_next(kt);
     bar();
     quad(acc, a4, bq, 4, 2);
-    if (ABL != 4 && g == 0) wait_next(kt);
     bar();
-    // P4: B columns 32-63 of tile t+1 (their registers are free after P3); DMA B(t+2) half 1 and the rest
-    // of A(t+2); quadrant (rows 64-127, cols 0-31)
-    if (kReads && kt + 1 < nk) readB(lds + ((kt + 1) & 1) * BUF + 2 * HALF + (wq >> 1) * HALF, 2, bq);
+    // P4: DMA B(t+2) half 1 + A(t+2) half 0 (A_g of tile t was read in P1 / P3); the wait that retires
+    // tile t+1 (this wave's own DMA: the 6 issued after A(t+1) half 1 may stay in flight), group 1 in its
+    // read segment, group 0 after its MFMAs - both before the barrier that precedes tile t+1's reads;
+    // quadrant (rows 64-127, cols 0-31)
     if (kDma && kt + 2 < nk) {
       stageB(kt + 2, 1);
-      if constexpr (A_MN) stageA(kt + 2, 0);
-      stageA(kt + 2, 1);
+      stageA(kt + 2, 0);
     }
+    if (ABL == 4 || g == 1) wait_next(kt);
     bar();
     quad(acc, a4, bq, 4, 0);
+    if (ABL != 4 && g == 0) wait_next(kt);
     bar();
   }
   if (ABL != 4 && g == 0) bar();  // group 0 catches up: every wave's reads and MFMAs issued, the LDS is free

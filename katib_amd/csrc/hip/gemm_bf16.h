@@ -10,12 +10,6 @@ bool supported(int M, int N, int K);  // M, N multiples of 128, K of 64
 hipError_t launch_nt(const void* A, const void* W, const void* bias, void* C, void* G, int M, int N, int K,
                      hipStream_t st);
 
-// 256 x 256 tile variant (4 waves of 128 x 128, 4 LDS stages): M, N multiples of 256, K of 64
-bool supported_big(int M, int N, int K);
-// variant 0: plain K loop, 1: software-pipelined (fragments of tile k + 1 read under tile k's MFMAs)
-hipError_t launch_nt_big(const void* A, const void* W, const void* bias, void* C, void* G, int M, int N, int K,
-                         int variant, hipStream_t st);
-
 // Layout-native GEMM: C = op(A) op(B), op(A)[M][K] from A stored [M][K] (a_mn false) or [K][M]
 // (a_mn true), op(B)[K][N] from B stored [N][K] (b_mn false) or [K][N] (b_mn true); lda / ldb are
 // the stored row strides (elements). out_f32: C is an fp32 slab [splitk][M][N] (one slab per K

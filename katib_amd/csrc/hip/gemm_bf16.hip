@@ -19,7 +19,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
 
 #include "gemm_bf16.h"
 
@@ -70,16 +69,14 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ (row & 7)) << 4));
 }
 
-// STAGES LDS buffers; STAGES - 1 K-tiles in flight while one is consumed. STAGES == 2: one
-// barrier per K-tile with the DMA drained before it (2 workgroups per CU). STAGES >= 3 (1 per CU):
-// the DMA of the next STAGES - 2 tiles stays in flight across the raw s_barrier, each wave waiting
-// only for its own loads of the tile about to be read with a counted vmcnt (8 DMA instructions
-// per thread per tile), never __syncthreads() (its fence would wait vmcnt(0) and drain the pipe).
-template <int EPI, int STAGES>
+// Two LDS buffers, one barrier per K-tile with the DMA drained before it (2 workgroups per CU): measured
+// fastest of 2 / 3 / 4 stages on MI355X (profiles/gemm_bf16_r03.log: 3 / 4 stages at one workgroup per CU
+// 1.3-1.6x slower).
+template <int EPI>
 __global__ void __launch_bounds__(256) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
                                                       const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
                                                       uint16_t* __restrict__ G, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char lds[STAGES * 2 * TILE_BYTES];  // [stage][A|W][128][64] bf16
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * TILE_BYTES];  // [stage][A|W][128][64] bf16
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
   // XCD-aware tile renumbering (bijective): XCD x = b % 8 gets the x-th contiguous range
   const int NB = N / BN, nwg = NB * (M / BM), b = blockIdx.x;
@@ -95,12 +92,12 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const uint16_t* __restrict
 
   const int nk = K / BK;
   auto stage_tile = [&](int kt) {
-    char* d = lds + (kt % STAGES) * 2 * TILE_BYTES;
+    char* d = lds + (kt & 1) * 2 * TILE_BYTES;
     stage(A, K, m0, kt * BK, d, wave, lane);
     stage(W, K, n0, kt * BK, d + TILE_BYTES, wave, lane);
   };
   auto compute = [&](int kt) {
-    const char* la = lds + (kt % STAGES) * 2 * TILE_BYTES;
+    const char* la = lds + (kt & 1) * 2 * TILE_BYTES;
     const char* lw = la + TILE_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -116,33 +113,14 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const uint16_t* __restrict
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
     }
   };
-  if constexpr (STAGES == 2) {
-    stage_tile(0);
+  stage_tile(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) stage_tile(kt + 1);  // the other buffer: its readers passed the last barrier
+    compute(kt);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) stage_tile(kt + 1);  // the other buffer: its readers passed the last barrier
-      compute(kt);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else {
-#pragma unroll
-    for (int p = 0; p < STAGES - 1; ++p)
-      if (p < nk) stage_tile(p);
-    for (int kt = 0; kt < nk; ++kt) {
-      // this wave's loads of tile kt have landed: the younger tiles' 8 DMA each may stay in flight
-      const int younger = min(nk - 1 - kt, STAGES - 2);
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // every wave's tile-kt loads landed, and every wave finished reading tile kt - 1's buffer,
-      // which the next stage_tile refills
-      __builtin_amdgcn_s_barrier();
-      if (kt + STAGES - 1 < nk) stage_tile(kt + STAGES - 1);
-      compute(kt);
-    }
-    __builtin_amdgcn_s_barrier();  // all reads done before the epilogue reuses the LDS
   }
 
   // epilogue: wave tile 64 x 64 -> LDS (bf16, row-major, 128 B rows) -> 16-byte global stores
@@ -377,336 +355,6 @@ __global__ void __launch_bounds__(256) gemm_lt_kernel(const uint16_t* __restrict
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// 256 x 128 tile, 8 waves (4 along M x 2 along N, 64 x 64 each), three LDS stages (144 KB, one
-// workgroup per CU): the DMA of K-tile t + 2 is issued right after the barrier that opens tile t
-// and stays in flight across the next barrier - each wave waits only for its OWN 6 loads of the
-// tile about to be read (counted vmcnt, never 0 in the loop) before a raw s_barrier (no
-// __syncthreads: its fence would drain the DMA). Two waves per SIMD keep the matrix pipe fed while
-// the other pair waits on LDS. Operand tiles are 1 KB DMA blocks of 16 KB sub-images (K-contiguous
-// [128 rows][64 k] or MN-contiguous [64 k][128 mn], the same swizzled images as above).
-// ------------------------------------------------------------------------------------------------
-constexpr int BM2 = 256, BN2 = 128, SUB = 16384, STAGE2 = 3 * SUB;  // per stage: A 2 sub-images + B 1
-
-// DMA block `blk` (0..15) of a 16 KB sub-image whose first mn row / column is mn0
-template <bool MN>
-__device__ __forceinline__ void stage_blk(const uint16_t* __restrict__ src, int ld, int mn0, int k0, char* img,
-                                          int blk, int lane) {
-  if constexpr (MN) {
-    const int row = blk * 4 + (lane >> 4);
-    const int chunk = (lane & 15) ^ mn_swz(row);
-    __builtin_amdgcn_global_load_lds(src + (size_t)(k0 + row) * ld + mn0 + chunk * 8, (lds_ptr)(img + blk * 1024),
-                                     16, 0, 0);
-  } else {
-    const int row = blk * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ (row & 7);
-    __builtin_amdgcn_global_load_lds(src + (size_t)(mn0 + row) * ld + k0 + chunk * 8, (lds_ptr)(img + blk * 1024),
-                                     16, 0, 0);
-  }
-}
-
-template <bool A_MN, bool B_MN, bool OUT_F32>
-__global__ void __launch_bounds__(512) gemm_lt2_kernel(const uint16_t* __restrict__ A, int lda,
-                                                       const uint16_t* __restrict__ B, int ldb,
-                                                       const uint16_t* __restrict__ bias, void* __restrict__ Cv,
-                                                       int M, int N, int kslice) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];  // [3 stages][A0 | A1 | B] 16 KB each
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
-  const int NB = N / BN2, nwg = NB * (M / BM2), b = blockIdx.x;
-  const int q = nwg / 8, r = nwg % 8, xcd = b % 8, loc = b / 8;
-  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-  const int m0 = (t / NB) * BM2, n0 = (t % NB) * BN2;
-  const int kbeg = blockIdx.y * kslice;
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = kslice / BK;
-  // 48 DMA blocks per stage, 6 per wave: A sub-image (wave >> 2) blocks (wave & 3) * 4 .. + 3, B blocks
-  // (wave * 2, wave * 2 + 1)
-  auto stage_tile = [&](int kt) {
-    char* d = lds + (kt % 3) * STAGE2;
-    const int k0 = kbeg + kt * BK, ai = wave >> 2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      stage_blk<A_MN>(A, lda, m0 + ai * 128, k0, d + ai * SUB, (wave & 3) * 4 + i, lane);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) stage_blk<B_MN>(B, ldb, n0, k0, d + 2 * SUB, wave * 2 + i, lane);
-  };
-  auto compute = [&](int kt) {
-    const char* la = lds + (kt % 3) * STAGE2 + (wr >> 1) * SUB;  // this wave's 128-row A sub-image
-    const char* lb = lds + (kt % 3) * STAGE2 + 2 * SUB;
-    const int ar = (wr & 1) * 64;
-    bf16x8 a[2][4], w[2][4];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[kk][i] = A_MN ? frag_mn(la, ar + i * 16, kk, lane) : frag(la, ar + i * 16 + (lane & 15), chunk);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        w[kk][j] = B_MN ? frag_mn(lb, wc * 64 + j * 16, kk, lane) : frag(lb, wc * 64 + j * 16 + (lane & 15), chunk);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], w[kk][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  stage_tile(0);
-  if (nk > 1) stage_tile(1);
-  for (int kt = 0; kt < nk; ++kt) {
-    // this wave's 6 loads of tile kt have landed (tile kt + 1's 6 may stay in flight), every wave
-    // is past compute(kt - 1), whose buffer the next stage_tile refills
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 2 < nk) stage_tile(kt + 2);
-    compute(kt);
-  }
-  __builtin_amdgcn_s_barrier();  // every wave's reads done before the epilogue reuses the LDS
-
-  const int orow = m0 + wr * 64, ocol = n0 + wc * 64;
-  if constexpr (OUT_F32) {
-    float* C = static_cast<float*>(Cv) + (size_t)blockIdx.y * M * N;
-    float* tile = reinterpret_cast<float*>(lds + wave * 16384);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) tile[(i * 16 + (lane >> 4) * 4 + e) * 64 + j * 16 + (lane & 15)] = acc[i][j][e];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int row = it * 4 + (lane >> 4), ch = lane & 15;
-      *reinterpret_cast<float4*>(C + (size_t)(orow + row) * N + ocol + ch * 4) =
-          *reinterpret_cast<const float4*>(tile + row * 64 + ch * 4);
-    }
-  } else {
-    uint16_t* C = static_cast<uint16_t*>(Cv);
-    char* tile_u = lds + wave * 8192;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = j * 16 + (lane & 15);
-      const float bv = bias ? bf2f(bias[ocol + col]) : 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          *reinterpret_cast<uint16_t*>(tile_u + (i * 16 + (lane >> 4) * 4 + e) * 128 + col * 2) = f2bf(acc[i][j][e] + bv);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int row = it * 8 + (lane >> 3), ch = lane & 7;
-      *reinterpret_cast<uint4*>(C + (size_t)(orow + row) * N + ocol + ch * 8) =
-          *reinterpret_cast<const uint4*>(tile_u + row * 128 + ch * 16);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// 256 x 256 output tile, 4 waves of 128 x 128 (8 x 8 v_mfma_f32_16x16x32_bf16 accumulators = 256
-// AGPRs per lane, one wave per SIMD), K-step 32, four LDS stages (32 KB each, three K-tiles in flight).
-// Why: a 64 x 64 wave tile reads (64 + 64) x 32 x 2 B of fragments per 64 x 64 x 32 MFMA block - at
-// 128 B/clk of LDS per CU that is exactly the matrix cores' 4096 FLOP/clk, so the 128^2 kernels above
-// are LDS-bound at ~60-70 % of peak; a 128 x 128 wave tile halves the fragment bytes per FLOP.
-// LDS image: 64-byte rows (32 bf16 of k), 16-byte chunk c of row r stored at slot c ^ ((r >> 2) & 3)
-// (the 8 lanes of a ds_read_b128 phase, rows r..r+7 of one chunk, hit 8 distinct 16-byte bank groups).
-// MEASURED SLOWER than both the 128^2 kernel and hipBLASLt (profiles/gemm_big_tile_r05.log: 490-730
-// TF/s vs 750-960 and 850-1260): with one wave per SIMD the compiler waits lgkmcnt(0) for all 16
-// fragment reads of a K-tile before the first MFMA (4 waves x 16 KB burst = ~512 LDS cycles against
-// 1024 MFMA cycles), and the software-pipelined variant (PIPE 1) spills accumulator renames into
-// v_accvgpr moves. Kept selectable (gemm_nt(..., big=0|1)) for that record; not used by the model.
-// Epilogue: accumulators -> bf16 pairs (adjacent columns swapped across lane pairs with one DPP
-// exchange, 32-bit LDS writes) into a per-wave 128 x 128 tile with 272-byte rows (16-byte pad: the
-// 4 row groups of a write land 4 banks apart), then 16-byte row-segment global stores.
-// ------------------------------------------------------------------------------------------------
-constexpr int BM3 = 256, BK3 = 32, ST3 = 4, SUB3 = BM3 * BK3 * 2;  // SUB3: one operand's K-tile (16 KB)
-constexpr int ROW3 = 272, WTILE3 = 128 * ROW3;                        // epilogue tile row / wave tile bytes
-constexpr int LDS3 = (ST3 * 2 * SUB3 > 4 * WTILE3) ? ST3 * 2 * SUB3 : 4 * WTILE3;
-
-__device__ __forceinline__ void stage3(const uint16_t* __restrict__ src, int ld, int row0, int k0, char* img, int wave,
-                                       int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = wave * 4 + i;             // 1 KB block = 16 rows of 64 B
-    const int row = blk * 16 + (lane >> 2);
-    const int chunk = (lane & 3) ^ ((row >> 2) & 3);
-    __builtin_amdgcn_global_load_lds(src + (size_t)(row0 + row) * ld + k0 + chunk * 8, (lds_ptr)(img + blk * 1024),
-                                     16, 0, 0);
-  }
-}
-
-__device__ __forceinline__ bf16x8 frag3(const char* img, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4));
-}
-
-template <int EPI, int PIPE>
-__global__ void __launch_bounds__(256) gemm_nt_big_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
-                                                          const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
-                                                          uint16_t* __restrict__ G, int M, int N, int K) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];  // [stage][A | W][256 rows][64 B]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
-  const int NB = N / BM3, nwg = NB * (M / BM3), b = blockIdx.x;
-  const int q = nwg / 8, r = nwg % 8, xcd = b % 8, loc = b / 8;
-  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-  const int m0 = (t / NB) * BM3, n0 = (t % NB) * BM3;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK3;
-  if constexpr (PIPE == 0) {
-    // plain form: wait for tile kt, barrier, refill the buffer of tile kt - 1, fragments, 64 MFMAs
-    auto stage_tile = [&](int kt) {
-      char* d = lds + (kt % ST3) * 2 * SUB3;
-      stage3(A, K, m0, kt * BK3, d, wave, lane);
-      stage3(W, K, n0, kt * BK3, d + SUB3, wave, lane);
-    };
-#pragma unroll
-    for (int p = 0; p < ST3 - 1; ++p)
-      if (p < nk) stage_tile(p);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int younger = min(nk - 1 - kt, ST3 - 2);
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (kt + ST3 - 1 < nk) stage_tile(kt + ST3 - 1);
-      const char* la = lds + (kt % ST3) * 2 * SUB3;
-      const char* lb = la + SUB3;
-      const int chunk = lane >> 4;
-      bf16x8 a[8], w[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        a[i] = frag3(la, wr * 128 + i * 16 + (lane & 15), chunk);
-        w[i] = frag3(lb, wc * 128 + i * 16 + (lane & 15), chunk);
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  } else {
-  // Software pipeline, branch-free body (so the scheduler can interleave it): step kt waits for tile
-  // kt + 1 (its own 8 DMA; tiles kt + 2, kt + 3 stay in flight), refills tile kt's buffer with tile
-  // kt + 4 (clamped to the last tile past the end: a harmless re-load into a dead buffer), reads tile
-  // kt + 1's fragments into the other register set while tile kt's 64 MFMAs issue (1 ds_read per 4
-  // MFMAs, the 8 DMA spread over the first half). The lgkmcnt(0) before the barrier makes every wave's
-  // tile-kt fragments resident before any wave's DMA overwrites that buffer.
-  auto stage_tile = [&](int kt) {
-    const int kc = min(kt, nk - 1);
-    char* d = lds + (kt % ST3) * 2 * SUB3;
-    stage3(A, K, m0, kc * BK3, d, wave, lane);
-    stage3(W, K, n0, kc * BK3, d + SUB3, wave, lane);
-  };
-  auto read_frags = [&](int kt, bf16x8 (&fa)[8], bf16x8 (&fw)[8]) {
-    const char* la = lds + (kt % ST3) * 2 * SUB3;
-    const char* lb = la + SUB3;
-    const int chunk = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      fa[i] = frag3(la, wr * 128 + i * 16 + (lane & 15), chunk);
-      fw[i] = frag3(lb, wc * 128 + i * 16 + (lane & 15), chunk);
-    }
-  };
-  auto step = [&](int kt, bf16x8 (&ca)[8], bf16x8 (&cw)[8], bf16x8 (&na)[8], bf16x8 (&nw)[8]) {
-    asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    stage_tile(kt + ST3);
-    read_frags(kt + 1, na, nw);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i], cw[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 ds_read
-      if (g < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 DMA (VMEM read)
-    }
-  };
-#pragma unroll
-  for (int p = 0; p < ST3; ++p) stage_tile(p);
-  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // own loads of tile 0
-  __builtin_amdgcn_s_barrier();
-  bf16x8 a0[8], w0[8], a1[8], w1[8];
-  read_frags(0, a0, w0);
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(kt, a0, w0, a1, w1);
-    step(kt + 1, a1, w1, a0, w0);
-  }
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the clamped tail DMA writes LDS too
-  __builtin_amdgcn_s_barrier();  // all fragment reads done before the epilogue reuses the LDS
-
-  char* tile = lds + wave * WTILE3;
-  const bool odd = lane & 1;
-  const int orow = m0 + wr * 128, ocol = n0 + wc * 128;
-#pragma unroll
-  for (int pass = 0; pass < (EPI == 1 ? 2 : 1); ++pass) {
-    uint16_t* out = pass ? G : C;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int col = j * 16 + (lane & 15);
-      const float bv = bias ? bf2f(bias[ocol + col]) : 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float u = bf2f(f2bf(acc[i][j][e] + bv));
-          v[e] = pass ? gelu_tanh(u) : u;
-        }
-        // lane pair (c, c+1): the even lane writes rows 0-1, the odd lane rows 2-3, as column pairs
-        const float s0 = odd ? v[0] : v[2], s1 = odd ? v[1] : v[3];
-        const float r0 = __shfl_xor(s0, 1, 64), r1 = __shfl_xor(s1, 1, 64);
-        const int row = i * 16 + (lane >> 4) * 4 + (odd ? 2 : 0);
-        const int c2 = col & ~1;
-        const uint32_t w0 = odd ? ((uint32_t)f2bf(r0) | ((uint32_t)f2bf(v[2]) << 16))
-                                : ((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(r0) << 16));
-        const uint32_t w1 = odd ? ((uint32_t)f2bf(r1) | ((uint32_t)f2bf(v[3]) << 16))
-                                : ((uint32_t)f2bf(v[1]) | ((uint32_t)f2bf(r1) << 16));
-        *reinterpret_cast<uint32_t*>(tile + row * ROW3 + c2 * 2) = w0;
-        *reinterpret_cast<uint32_t*>(tile + (row + 1) * ROW3 + c2 * 2) = w1;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // wave-private tile: LDS writes before reads
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 8
-    for (int it = 0; it < 32; ++it) {
-      const int row = it * 4 + (lane >> 4), ch = lane & 15;
-      *reinterpret_cast<uint4*>(out + (size_t)(orow + row) * N + ocol + ch * 8) =
-          *reinterpret_cast<const uint4*>(tile + row * ROW3 + ch * 16);
-    }
-    if (EPI == 1 && pass == 0) {  // the G pass rewrites the tile: every lane's reads first
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  }
-}
-
 }  // namespace
 
 hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, bool b_mn, const void* bias, void* C,
@@ -720,37 +368,6 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
   const uint16_t* b = static_cast<const uint16_t*>(B);
   const uint16_t* bb = static_cast<const uint16_t*>(bias);
   const int ks = K / splitk;
-  // tile: 128 (128 x 128, 2 stages, 2 workgroups per CU; default) or KATIB_HIP_GEMM_TILE=256
-  // (256 x 128, 3 stages, 8 waves, 1 per CU): measured 15-25 % slower on every GPT-2 backward shape
-  // (profiles/gemm_fwd_bwd_table_r05.log), kept selectable
-  static const int tile = getenv("KATIB_HIP_GEMM_TILE") ? atoi(getenv("KATIB_HIP_GEMM_TILE")) : 128;
-  if (tile == 256 && M % BM2 == 0 && !gu && !colpart) {
-    static bool attr = false;
-    if (!attr) {  // > 64 KB of dynamic LDS must be opted into per kernel
-      const void* ks_[] = {(const void*)gemm_lt2_kernel<false, false, false>, (const void*)gemm_lt2_kernel<false, true, false>,
-                           (const void*)gemm_lt2_kernel<true, false, false>, (const void*)gemm_lt2_kernel<true, true, false>,
-                           (const void*)gemm_lt2_kernel<false, false, true>, (const void*)gemm_lt2_kernel<false, true, true>,
-                           (const void*)gemm_lt2_kernel<true, false, true>, (const void*)gemm_lt2_kernel<true, true, true>};
-      for (const void* f : ks_) hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * STAGE2);
-      attr = true;
-    }
-    const dim3 grid2((M / BM2) * (N / BN2), splitk);
-#define LT2_LAUNCH(AM, BMN, F32) \
-  hipLaunchKernelGGL((gemm_lt2_kernel<AM, BMN, F32>), grid2, dim3(512), 3 * STAGE2, st, a, lda, b, ldb, bb, C, M, N, ks)
-    if (out_f32) {
-      if (a_mn && b_mn) LT2_LAUNCH(true, true, true);
-      else if (a_mn) LT2_LAUNCH(true, false, true);
-      else if (b_mn) LT2_LAUNCH(false, true, true);
-      else LT2_LAUNCH(false, false, true);
-    } else {
-      if (a_mn && b_mn) LT2_LAUNCH(true, true, false);
-      else if (a_mn) LT2_LAUNCH(true, false, false);
-      else if (b_mn) LT2_LAUNCH(false, true, false);
-      else LT2_LAUNCH(false, false, false);
-    }
-#undef LT2_LAUNCH
-    return hipGetLastError();
-  }
   const dim3 grid((M / BM) * (N / BN), splitk);
 #define LT_LAUNCH(AM, BMN, F32) \
   hipLaunchKernelGGL((gemm_lt_kernel<AM, BMN, F32>), grid, dim3(256), 0, st, a, lda, b, ldb, bb, C, M, N, ks, gu, \
@@ -772,59 +389,17 @@ hipError_t launch_lt(const void* A, int lda, bool a_mn, const void* B, int ldb, 
 
 bool supported(int M, int N, int K) { return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0; }
 
-bool supported_big(int M, int N, int K) {
-  return M > 0 && N > 0 && K > 0 && M % BM3 == 0 && N % BM3 == 0 && K % (2 * BK3) == 0;
-}
-
-hipError_t launch_nt_big(const void* A, const void* W, const void* bias, void* C, void* G, int M, int N, int K,
-                         int variant, hipStream_t st) {
-  if (!supported_big(M, N, K)) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {  // > 64 KB of dynamic LDS is opted into per kernel
-    const void* ks_[] = {(const void*)gemm_nt_big_kernel<0, 0>, (const void*)gemm_nt_big_kernel<1, 0>,
-                         (const void*)gemm_nt_big_kernel<0, 1>, (const void*)gemm_nt_big_kernel<1, 1>};
-    for (const void* f : ks_) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS3);
-    attr = true;
-  }
-  const dim3 grid((M / BM3) * (N / BM3));
-  const uint16_t* a = static_cast<const uint16_t*>(A);
-  const uint16_t* w = static_cast<const uint16_t*>(W);
-  const uint16_t* bb = static_cast<const uint16_t*>(bias);
-  uint16_t* c = static_cast<uint16_t*>(C);
-  uint16_t* g = static_cast<uint16_t*>(G);
-  if (variant == 1) {
-    if (g) hipLaunchKernelGGL((gemm_nt_big_kernel<1, 1>), grid, dim3(256), LDS3, st, a, w, bb, c, g, M, N, K);
-    else hipLaunchKernelGGL((gemm_nt_big_kernel<0, 1>), grid, dim3(256), LDS3, st, a, w, bb, c, nullptr, M, N, K);
-  } else {
-    if (g) hipLaunchKernelGGL((gemm_nt_big_kernel<1, 0>), grid, dim3(256), LDS3, st, a, w, bb, c, g, M, N, K);
-    else hipLaunchKernelGGL((gemm_nt_big_kernel<0, 0>), grid, dim3(256), LDS3, st, a, w, bb, c, nullptr, M, N, K);
-  }
-  return hipGetLastError();
-}
-
 hipError_t launch_nt(const void* A, const void* W, const void* bias, void* C, void* G, int M, int N, int K,
                      hipStream_t st) {
   if (!supported(M, N, K)) return hipErrorInvalidValue;
   const dim3 grid((M / BM) * (N / BN));
-  // 2 stages at 2 workgroups per CU measured fastest on MI355X (GPT-2 projections: 3 / 4 stages at one
-  // workgroup per CU are 1.3-1.6x slower, profiles/gemm_bf16_r03.log)
-  static const int stages = getenv("KATIB_HIP_GEMM_STAGES") ? atoi(getenv("KATIB_HIP_GEMM_STAGES")) : 2;
   const uint16_t* a = static_cast<const uint16_t*>(A);
   const uint16_t* w = static_cast<const uint16_t*>(W);
   const uint16_t* bb = static_cast<const uint16_t*>(bias);
   uint16_t* c = static_cast<uint16_t*>(C);
   uint16_t* g = static_cast<uint16_t*>(G);
-#define GEMM_LAUNCH(S)                                                                              \
-  if (g) hipLaunchKernelGGL((gemm_nt_kernel<1, S>), grid, dim3(256), 0, st, a, w, bb, c, g, M, N, K); \
-  else hipLaunchKernelGGL((gemm_nt_kernel<0, S>), grid, dim3(256), 0, st, a, w, bb, c, nullptr, M, N, K);
-  if (stages == 2) {
-    GEMM_LAUNCH(2)
-  } else if (stages == 4) {
-    GEMM_LAUNCH(4)
-  } else {
-    GEMM_LAUNCH(3)
-  }
-#undef GEMM_LAUNCH
+  if (g) hipLaunchKernelGGL((gemm_nt_kernel<1>), grid, dim3(256), 0, st, a, w, bb, c, g, M, N, K);
+  else hipLaunchKernelGGL((gemm_nt_kernel<0>), grid, dim3(256), 0, st, a, w, bb, c, nullptr, M, N, K);
   return hipGetLastError();
 }
 

@@ -1119,15 +1119,8 @@ hipError_t ln_fwd(const float* x32, const bf16* r, float* xo, const bf16* gamma,
 }
 
 // (one workgroup per CU: the partial rows stay few for ln_reduce_k; each wave keeps two rows in flight,
-// see ln_bwd_k). KATIB_LN_BWD_BLOCKS overrides (A/B).
-int ln_bwd_blocks(int M) {
-  static const int cap = [] {
-    const char* e = getenv("KATIB_LN_BWD_BLOCKS");
-    const int v = e ? atoi(e) : kLnBwdBlocks;
-    return v > 0 ? v : kLnBwdBlocks;
-  }();
-  return (M + 3) / 4 < cap ? (M + 3) / 4 : cap;
-}
+// see ln_bwd_k).
+int ln_bwd_blocks(int M) { return (M + 3) / 4 < kLnBwdBlocks ? (M + 3) / 4 : kLnBwdBlocks; }
 
 hipError_t ln_bwd(const bf16* dy, const float* xin, const float* mean, const float* rstd, const bf16* gamma,
                   const float* dres, float* dx, bf16* dr, float* part_g, float* part_b, int M, int D,

@@ -252,9 +252,8 @@ void attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& dout, const Tens
 }
 
 // C[M][N] = A[M][K] . W[N][K]^T (+ bias[N]); G given: C = pre-activation, G = gelu_tanh(C)
-// big: -1 the 128 x 128 kernel, 0 / 1 the 256 x 256 kernel (plain / software-pipelined K loop)
 void gemm_nt(const Tensor& A, const Tensor& W, const c10::optional<Tensor>& bias, const Tensor& C,
-             const c10::optional<Tensor>& G, int64_t big) {
+             const c10::optional<Tensor>& G) {
   TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && C.dim() == 2, "gemm_nt: 2-D operands");
   const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
   TORCH_CHECK(W.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_nt: shapes");
@@ -272,13 +271,6 @@ void gemm_nt(const Tensor& A, const Tensor& W, const c10::optional<Tensor>& bias
   if (G.has_value() && G->defined()) {
     chk(*G, at::kBFloat16, M * N, "G");
     gp = G->data_ptr();
-  }
-  if (big >= 0) {
-    TORCH_CHECK(katib_hip::gemm::supported_big((int)M, (int)N, (int)K), "gemm_nt: 256-tile needs M, N % 256, K % 64");
-    ok(katib_hip::gemm::launch_nt_big(A.data_ptr(), W.data_ptr(), bp_, C.data_ptr(), gp, (int)M, (int)N, (int)K,
-                                      (int)big, stream()),
-       "gemm_nt (256 tile)");
-    return;
   }
   ok(katib_hip::gemm::launch_nt(A.data_ptr(), W.data_ptr(), bp_, C.data_ptr(), gp, (int)M, (int)N, (int)K, stream()),
      "gemm_nt");
@@ -381,10 +373,7 @@ void register_transformer(py::module& m) {
         py::arg("A"), py::arg("a_mn"), py::arg("B"), py::arg("b_mn"), py::arg("bias"), py::arg("C"),
         py::arg("splitk") = 1, py::arg("gelu_u") = py::none(), py::arg("colpart") = py::none());
   m.def("gemm_nt", &gemm_nt, "bf16 C = A W^T (+ bias) (+ GELU) on MFMA (gemm_bf16.hip)", py::arg("A"), py::arg("W"),
-        py::arg("bias"), py::arg("C"), py::arg("G"), py::arg("big") = -1);
-  m.def("gemm_nt_big_supported", [](int64_t M, int64_t N, int64_t K) {
-    return katib_hip::gemm::supported_big((int)M, (int)N, (int)K);
-  });
+        py::arg("bias"), py::arg("C"), py::arg("G"));
   m.def("gemm_nt_supported", [](int64_t M, int64_t N, int64_t K) {
     return M < (1 << 30) && N < (1 << 30) && K < (1 << 30) && katib_hip::gemm::supported((int)M, (int)N, (int)K);
   });

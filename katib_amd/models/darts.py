@@ -242,8 +242,9 @@ class DartsNetwork:
         # (parallel/syncbn.py; the HIP cells use ops/hip_darts.py SyncBN under DartsSearch)
         self.sync = None
         # HIP path: the whole network as one Function (hip_darts.network_loss) instead of per-cell
-        # Functions under autograd (KATIB_DARTS_NET_FUNCTION=0: the per-cell path, A/B switch)
-        self.net_function = __import__("os").environ.get("KATIB_DARTS_NET_FUNCTION", "1") != "0"
+        # Functions under autograd (attribute False: the per-cell path, kept for its A/B test;
+        # profiles/darts_netfn_ab_r04.log)
+        self.net_function = True
 
     def _batch_norm(self, x, rm, rv, w, b, training):
         if training and self.sync is not None and self.sync.distributed:

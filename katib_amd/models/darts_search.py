@@ -40,7 +40,7 @@ from .darts import BNState, DartsLayout, DartsNetwork, accuracy
 # the running statistics, so k batches of n give the same losses and correct counts as one of k*n;
 # at B5 sizes the forward is launch / latency bound: per 128-image batch 0.54 ms at k = 1, 0.31 at 4,
 # 0.27 at 8, profiles/darts_eval_group_ab_r04.log; 0.252 at 16 and 32, darts_eval_group_ab_r05.log)
-EVAL_GROUP = int(__import__("os").environ.get("KATIB_DARTS_EVAL_GROUP", "16"))
+EVAL_GROUP = 16
 
 
 def eval_groups(batches, group: int = 0):

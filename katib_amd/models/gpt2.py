@@ -36,8 +36,7 @@ import torch
 import torch.nn.functional as F
 
 # attn-proj / fc2 bias gradients summed by the LayerNorm backward that writes their output gradient
-# (KATIB_GPT2_LN_BIAS=0: a separate column-sum pass per bias, as before; A/B switch)
-_LN_BIAS = __import__("os").environ.get("KATIB_GPT2_LN_BIAS", "1") != "0"
+_LN_BIAS = True  # (module attribute; False: a separate column-sum pass per bias, as before)
 
 from ..utils.tracing import gpu_range
 

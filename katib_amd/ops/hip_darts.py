@@ -54,21 +54,21 @@ REP = int(_K.REP)
 # _hipkern_zbf16 build variant (KATIB_AMD_HIPKERN), fp32 otherwise; node states, gradients, BN
 # statistics and weights stay fp32 either way
 ZDT = torch.bfloat16 if bool(getattr(_K, "ZBF16", False)) else torch.float32
-# FOLD=1 (default): a fold_f64 launch sums the REP replicas of each cross-workgroup reduction
-# before its consumers (which then read rep=1); FOLD=0 (KATIB_HIP_FOLD=0): consumers sum the
-# replicas themselves and the fold launches disappear. Measured on MI355X (B5 step): 13.3 ms
+# FOLD (module attribute, tests only): a fold_f64 launch sums the REP replicas of each cross-workgroup
+# reduction before its consumers (which then read rep=1); False: consumers sum the replicas themselves
+# and the fold launches disappear. Measured on MI355X (B5 step): 13.3 ms
 # with the folds, 17.1 ms without - every consumer workgroup re-reading 32 replicas costs more
 # than ~180 small fold launches.
-FOLD = __import__("os").environ.get("KATIB_HIP_FOLD", "1") != "0"
+FOLD = True
 _R = 1 if FOLD else REP
 # Self-folding producers (darts_ops.h FoldTail): with a counter ring registered for the device,
 # every launch that adds into f64 replicas folds them in its last workgroup, and the fold_f64
 # launches between producers and consumers disappear. Needs FOLD (consumers read replica 0).
-# Off by default (KATIB_HIP_SELFFOLD=1 turns it on): measured on MI355X, one arrival counter
+# Off (set_selffold(True): tests and experiments): measured on MI355X, one arrival counter
 # made every producer ~15-25 us slower (2000 same-address atomics serialise memory-side: B5
 # step 12.1 ms), 32 sharded counters still lose to the fold launches (8.22 vs 8.05 ms),
 # profiles/darts_selffold_edge_ab_r03.log.
-SELFFOLD = __import__("os").environ.get("KATIB_HIP_SELFFOLD", "0") != "0"
+SELFFOLD = False
 _CTR: Dict[int, torch.Tensor] = {}
 
 
@@ -107,15 +107,15 @@ _SYNC = None
 
 def _check_sync_fold_mode():
     """SyncBN sums the BN reductions over the ranks inside the fold (``_fold`` / ``SyncBN.fold``)
-    and ``_bn`` then divides by count * world. Without fold launches (KATIB_HIP_FOLD=0) or with
-    self-folding producers (KATIB_HIP_SELFFOLD=1) that fold never runs, and every rank would
+    and ``_bn`` then divides by count * world. Without fold launches (FOLD False) or with
+    self-folding producers (SELFFOLD True) that fold never runs, and every rank would
     normalise its LOCAL sums by the global count - mean and variance off by a factor of world,
     silently. Refuse those combinations."""
     if not FOLD:
-        raise RuntimeError("SyncBN needs the fold launches (KATIB_HIP_FOLD=1): the cross-rank BN sum "
+        raise RuntimeError("SyncBN needs the fold launches (hip_darts.FOLD): the cross-rank BN sum "
                            "happens inside them")
     if SELFFOLD:
-        raise RuntimeError("SyncBN is incompatible with self-folding producers (KATIB_HIP_SELFFOLD=1): "
+        raise RuntimeError("SyncBN is incompatible with self-folding producers (hip_darts.SELFFOLD): "
                            "their replicas would never be summed over the ranks")
 
 
@@ -307,13 +307,13 @@ def _launch(name: str, calls: List, *args):
         fn(calls[i:i + cap], *args)
 
 
-MULTI = __import__("os").environ.get("KATIB_HIP_MULTI", "1") != "0"  # mixed-variant launches (A/B switch)
+MULTI = True  # mixed-variant launches (module attribute: the per-variant path stays for A/B tests)
 # Deferred folds: the consumers right after a node's first reduction (the separable second stage's
 # input BN in the forward, the second-stage / dilated pointwise backward after combine_bwd_reduce)
 # sum the 32 replicas themselves in their prologue (workgroup-cooperative, one round trip:
 # darts_ops.hip coop_pair_sums), so those fold launches merge into the node's next fold
-# (KATIB_HIP_DEFER_FOLD=0: fold before every consumer, as before)
-DEFER_FOLD = __import__("os").environ.get("KATIB_HIP_DEFER_FOLD", "1") != "0"
+# (False: fold before every consumer, as before; profiles/darts_defer_fold_ab_r03.log)
+DEFER_FOLD = True
 
 
 def _unfolded(bn):
@@ -322,20 +322,20 @@ def _unfolded(bn):
 
 
 # a node's stage-1 separable + dilated depthwise backward in one mixed-variant launch, each part in
-# its own buffer, summed into gx by the pool-backward launch (A/B switch KATIB_HIP_DWB_MULTI)
-DWB_MULTI = __import__("os").environ.get("KATIB_HIP_DWB_MULTI", "1") != "0"
+# its own buffer, summed into gx by the pool-backward launch (profiles/darts_dwb_multi_ab_r03.log)
+DWB_MULTI = True
 # fused per-edge input gradient (edge_bwd_kernel) instead of per-family dw_bwd / pool_bwd launches.
 # Off by default: measured SLOWER on MI355X (B5 step 9.22 vs 8.05 ms; its 4 conv slots run
 # serially inside each workgroup, and fewer / larger bands only narrow the gap: 8.74 ms at 64 KB
-# bands), profiles/darts_selffold_edge_ab_r03.log. KATIB_HIP_EDGE_BWD=1 turns it on.
-EDGE_BWD = __import__("os").environ.get("KATIB_HIP_EDGE_BWD", "0") != "0"
+# bands), profiles/darts_selffold_edge_ab_r03.log. Kept for its numerics test (module attribute).
+EDGE_BWD = False
 
 
 # A node's pools launched beside its stage-1 dw-pw entries (one launch instead of two per node).
-# Opt-in (KATIB_HIP_JOINT_POOL=1): measured a wash on the B5 step (6.98 vs 6.96 ms,
+# Off (module attribute, tests): measured a wash on the B5 step (6.98 vs 6.96 ms,
 # profiles/darts_vec_ab_r04.log) - the pool workgroups (highest blockIdx.y) dispatch after the dw-pw
 # bands anyway, so only the ~1.6 us launch boundary goes.
-JOINT_POOL = __import__("os").environ.get("KATIB_HIP_JOINT_POOL", "0") != "0"
+JOINT_POOL = False
 
 
 def _dwpw_multi(entries):

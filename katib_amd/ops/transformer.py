@@ -45,19 +45,15 @@ def _kern():
         raise ImportError("katib_amd._hipkern is not built (run __graft_entry__.build()): %s" % e)
 
 
-# one-pass training cross-entropy (KATIB_XENT_FUSED=0: the two-pass xent_fwd + xent_bwd; A/B switch)
-_XENT_FUSED = os.environ.get("KATIB_XENT_FUSED", "1") != "0"
-# hipBLASLt BGRADB epilogue: weight + bias gradient in one GEMM for GPT-2's fc1 / qkv layers
-# (csrc/hip/lt_epilogue.cpp). Opt-in (KATIB_LT_EPILOGUE=1): gfx950's only BGRADB solutions are
-# unsplit 256x128 MI32x32 tiles, 197 / 115 us against 65-72 us for the split-K wgrad + a 14.5 us
-# colsum, 782k -> 743k tokens/s (profiles/lt_epilogue_r05.log).
-_LT_EPILOGUE = os.environ.get("KATIB_LT_EPILOGUE", "0") == "1"
-# GELU backward folded into the fc2 dgrad epilogue (HipOps.dgrad_gelu; =0: hipBLASLt dgrad + gelu_bwd)
-_GELU_DGRAD = os.environ.get("KATIB_GELU_DGRAD", "1") != "0"
-# ... and the fc1 bias gradient's column sums from the same epilogue + one row-sum launch. Opt-in
-# (KATIB_GELU_DGRAD_BIAS=1): measured neutral, 806.3k vs 807.1k tokens/s against the colsum pass over du
-# (profiles/gpt2_gelu_dgrad_bias_ab_r05.log) - the epilogue's shuffles cost what the 100 MB re-read saved
-_GELU_DGRAD_BIAS = os.environ.get("KATIB_GELU_DGRAD_BIAS", "0") == "1"
+# Kernel choices of the GPT-2 step are fixed by measurement, not switched by the environment:
+# * one-pass training cross-entropy (xent_fused_k): 783k -> 793k tokens/s against xent_fwd + xent_bwd
+#   (profiles/gpt2_xent_fused_ab_r05.log);
+# * the fc2 input gradient with the GELU backward in its epilogue (gemm_lt gelu_u): +1.3 % tokens/s
+#   against hipBLASLt dgrad + gelu_bwd (profiles/gpt2_gelu_dgrad_ab_r05.log);
+# * measured and removed: hipBLASLt's BGRADB weight + bias gradient epilogue (782k -> 743k tokens/s,
+#   profiles/lt_epilogue_r05.log) and the fc1 bias gradient from the dgrad epilogue (neutral,
+#   profiles/gpt2_gelu_dgrad_bias_ab_r05.log).
+
 
 class TorchOps:
     name = "torch"
@@ -198,7 +194,7 @@ class HipOps:
 
     name = "hip"
 
-    def __init__(self, eps: float = 1e-5):
+    def __init__(self, eps: float = 1e-5, gemm: str = "auto", gemm_bwd: str = "auto"):
         self.k = _kern()
         self.eps = eps
         self._bmm_f32 = True
@@ -206,8 +202,10 @@ class HipOps:
         # epilogue) for the shapes where it measured faster than hipBLASLt on MI355X, hipBLASLt
         # (torch.addmm) for the rest (profiles/gemm_bf16_r03.log: at M = 8192 the 128x128-tile kernel
         # wins the d x d projection 1.23-1.37x and loses qkv 0.87x, fc + GELU 0.96x, fc2 0.80x, the LM
-        # head 0.61x). KATIB_HIP_GEMM=all: every supported shape (tests), =0: hipBLASLt only.
-        self.gemm = os.environ.get("KATIB_HIP_GEMM", "auto")
+        # head 0.61x). gemm="all": every supported shape (tests), "0": hipBLASLt only; gemm_bwd likewise
+        # for the backward GEMMs.
+        self.gemm = gemm
+        self.gemm_bwd = gemm_bwd
 
     # (N, K) classes where gemm_bf16 beat hipBLASLt in the measured table
     GEMM_WINS = {(768, 768), (256, 256), (512, 512), (1024, 1024)}
@@ -226,10 +224,6 @@ class HipOps:
         c = torch.empty((x.shape[0], w.shape[0]), device=x.device, dtype=torch.bfloat16)
         self.k.gemm_nt(x, w, b, c, None)
         return c
-
-    def _lt_epi_ok(self, *ts):
-        return _LT_EPILOGUE and all(t is not None and t.dtype == torch.bfloat16 and t.is_contiguous()
-                                    and t.data_ptr() % 16 == 0 for t in ts)
 
     def linear_gelu(self, x, w, b):
         if not self._gemm_ok(x, w):
@@ -271,23 +265,15 @@ class HipOps:
         return du
 
     def dgrad_gelu(self, dy, w, u, db=None):
-        """(dy @ w) * gelu_tanh'(u) in one launch: the NN dgrad kernel (gemm_lt) with the GELU backward
-        in its epilogue (reads u where it writes the gradient) - against hipBLASLt's dgrad + the
-        gelu_bwd pass, which writes the gradient, then re-reads it with u and writes it again.
-        ``db`` (the fc1 bias gradient): per-64-row column sums from the same epilogue + one row-sum
-        launch, instead of a colsum pass re-reading the gradient. KATIB_GELU_DGRAD=0: the
-        two-launch form."""
+        """(dy @ w) * gelu_tanh'(u) in one launch: the NN dgrad kernel (gemm_lt) with the GELU backward in
+        its epilogue (reads u where it writes the gradient) - against hipBLASLt's dgrad + the gelu_bwd
+        pass, which writes the gradient, then re-reads it with u and writes it again. ``db`` (the fc1
+        bias gradient): one colsum pass over the result."""
         M, N = dy.shape
         K = w.shape[1]
-        if (_GELU_DGRAD and self._bwd_mode() != "0" and self._lt_ok(dy, w, u) and u.shape == (M, K)
+        if (self._bwd_mode() != "0" and self._lt_ok(dy, w, u) and u.shape == (M, K)
                 and M % 128 == 0 and K % 128 == 0 and N % 64 == 0):
             out = torch.empty((M, K), device=dy.device, dtype=torch.bfloat16)
-            if (_GELU_DGRAD_BIAS and db is not None and db.is_contiguous() and db.numel() == K
-                    and db.dtype == torch.bfloat16 and db.data_ptr() % 16 == 0):
-                part = torch.empty((M // 64, K), device=dy.device, dtype=torch.float32)
-                self.k.gemm_lt(dy, False, w, True, None, out, 1, u, part)
-                self.k.reduce_rows(part, db)
-                return out
             self.k.gemm_lt(dy, False, w, True, None, out, 1, u)
             if db is not None:
                 self.colsum(out, db)
@@ -298,11 +284,7 @@ class HipOps:
         return du
 
     def wgrad_bgrad(self, dy, x, dw, db):
-        """dw = dy^T x and db = column sums of dy: one hipBLASLt GEMM with the BGRADB epilogue where
-        it has a solution (csrc/hip/lt_epilogue.cpp), else wgrad + colsum."""
-        if self._lt_epi_ok(dy, x, dw, db) and dy.dim() == 2 and self._bwd_mode() != "all":
-            if self.k.lt_wgrad_bgrad(dy, x, dw, db):
-                return
+        """dw = dy^T x and db = column sums of dy (a linear layer's weight + bias gradients)."""
         self.wgrad(dy, x, dw)
         self.colsum(dy, db)
 
@@ -336,7 +318,7 @@ class HipOps:
         N = logits.shape[0]
         loss = torch.empty(N, device=logits.device, dtype=torch.float32)
         lse = torch.empty_like(loss)
-        if not (_XENT_FUSED and self.k.xent_fused(logits, tgt, loss, lse, gscale, 1.0 / N, V)):
+        if not self.k.xent_fused(logits, tgt, loss, lse, gscale, 1.0 / N, V):
             self.k.xent_fwd(logits, tgt, loss, lse, V)
             self.k.xent_bwd(logits, tgt, lse, gscale, 1.0 / N, V)
         return loss, lse, logits
@@ -359,13 +341,13 @@ class HipOps:
     # tokens = the PBT member's batch). Against the best hipBLASLt form (split-K batched fp32 +
     # row sum for wgrad, the strided mm for dgrad) the 128^2 two-stage tile (~600-800 TF/s) wins
     # only the qkv wgrad (1.07x); hipBLASLt's 192x256 / 256x256 tiles reach ~1 PF/s on the rest.
-    # The d x d dgrad wins at 8k tokens (1.19x). KATIB_HIP_GEMM_BWD=0: hipBLASLt for all, =all:
-    # gemm_lt wherever supported (tests).
+    # The d x d dgrad wins at 8k tokens (1.19x). gemm_bwd="0": hipBLASLt for all, "all": gemm_lt
+    # wherever supported (tests).
     WGRAD_SPLIT = {(2304, 768): 4}  # (out, in) -> split-K
     DGRAD_WINS = {(768, 768)}  # (out, in) classes of W where the NN kernel won (at <= 8k tokens)
 
     def _bwd_mode(self):
-        return os.environ.get("KATIB_HIP_GEMM_BWD", "auto")
+        return self.gemm_bwd
 
     def _lt_ok(self, *ts):
         return all(t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous() for t in ts)

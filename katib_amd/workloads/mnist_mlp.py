@@ -60,7 +60,7 @@ def parse_args(argv):
     p.add_argument("--num-layers", type=int, default=0,
                    help="hidden layers of width --hidden (0: the 784-h-h/2-10 net of the fused HIP path)")
     p.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "ftrl"])
-    p.add_argument("--unroll", type=int, default=int(__import__("os").environ.get("KATIB_MLP_UNROLL", "1")),
+    p.add_argument("--unroll", type=int, default=1,
                    help="train steps per captured HIP graph replay (the batch index comes from a device-side "
                         "step counter into the epoch's permutation, so one replay runs that many SGD steps); "
                         "1 (default) = one replay + one index copy per step. Measured on the B1 trials (3 per "

@@ -102,27 +102,6 @@ def test_dgrad_gelu_epilogue(ops, M):
     assert _rel(db, dbr) < 2e-2
 
 
-@pytest.mark.parametrize("M,N,K", [(2048, 3072, 768), (16384, 3072, 768), (16384, 2304, 768)])
-def test_lt_wgrad_bgrad(ops, M, N, K):
-    """hipBLASLt BGRADB (weight + bias gradient in one GEMM) vs the fp32 products."""
-    hip, ref = ops
-    g = _gen(5)
-    dy = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
-    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-    dw = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
-    db = torch.empty(N, device=DEV, dtype=torch.bfloat16)
-    assert hip.k.lt_wgrad_bgrad(dy, x, dw, db), "hipBLASLt has no BGRADB solution"
-    assert _rel(dw, dy.float().t() @ x.float()) < 1e-2
-    assert _rel(db, dy.float().sum(0)) < 1e-2
-    # the ops-level entry point (BGRADB opt-in, else wgrad + colsum) and the torch contract agree
-    dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
-    hip.wgrad_bgrad(dy, x, dw2, db2)
-    assert _rel(dw2, dw) < 1e-2 and _rel(db2, db) < 1e-2
-    dw3, db3 = torch.empty_like(dw), torch.empty_like(db)
-    ref.wgrad_bgrad(dy, x, dw3, db3)
-    assert _rel(dw, dw3) < 1e-2 and _rel(db, db3) < 1e-2
-
-
 @pytest.mark.parametrize("V,Vp", [(1000, 1024), (50257, 50304), (512, 512)])
 def test_cross_entropy(ops, V, Vp):
     hip, ref = ops

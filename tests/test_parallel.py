@@ -123,9 +123,9 @@ def test_syncbn_rejects_fold_modes_without_cross_rank_sum(monkeypatch):
 
     sync = h.SyncBN(FakeComm())  # default modes: accepted
     monkeypatch.setattr(h, "FOLD", False)
-    with pytest.raises(RuntimeError, match="KATIB_HIP_FOLD"):
+    with pytest.raises(RuntimeError, match="hip_darts.FOLD"):
         h.SyncBN(FakeComm())
-    with pytest.raises(RuntimeError, match="KATIB_HIP_FOLD"):
+    with pytest.raises(RuntimeError, match="hip_darts.FOLD"):
         with h.sync_scope(sync):
             pass
     monkeypatch.setattr(h, "FOLD", True)
