@@ -17,6 +17,8 @@ constexpr int kSigEpoch = kMaxBlocks * kMaxRanks;
 constexpr int kSigErr = kSigEpoch + kMaxBlocks;
 constexpr int kSigWords = kSigErr + 64;
 
+constexpr int kSmallFold = 4096;  // fold_sync: totals up to this many doubles run on one workgroup
+
 struct AllReduceArgs {
   const float* in;
   float* out;

@@ -129,14 +129,23 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(AllReduceArgs a) {
 }
 
 // fold + cross-rank sum of f64 segments (SyncBN), same hand-off protocol as oneshot_kernel
+// Small payloads (every SyncBN fold of the B5 supernet: a few hundred doubles) run on block 0 alone: one
+// flag per peer instead of one per (block, peer) - the handshake, not the bytes, is the cost there
+// (2 / 4 ranks: 4.1 / 5.0 us per rendezvous on 1 workgroup vs 5.9 / 8.7 on 16, profiles/rendezvous_r06.log).
+// The other blocks return at once (the decision is the same on every rank: same segments), so their
+// epochs do not move; block 0 stages small calls in a region of its own at the top of each half, which
+// no multi-block call touches (those are limited to cap / 2 - kSmallFold doubles), so block 0's parity
+// alternation protects both regions exactly as in the uniform case.
 __global__ __launch_bounds__(kThreads) void fold_sync_kernel(AllReduceArgs a, FoldF64Args f, uint64_t mask) {
-  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  const bool small = f.total <= kSmallFold;
+  if (small && blockIdx.x > 0) return;
+  const int b = blockIdx.x, nb = small ? 1 : gridDim.x, tid = threadIdx.x;
   uint32_t* mysig = a.sig[a.rank];
   __shared__ uint32_t s_e;
   if (tid == 0) s_e = ld_sys(mysig + kSigEpoch + b) + 1u;
   __syncthreads();
   const uint32_t e = s_e;
-  const int64_t half = (int64_t)(e & 1u) * (a.cap / 2);  // in doubles
+  const int64_t half = (int64_t)(e & 1u) * (a.cap / 2) + (small ? a.cap / 2 - kSmallFold : 0);  // in doubles
   const int per = (f.total + nb - 1) / nb;
   const int lo = min(f.total, b * per), hi = min(f.total, lo + per);
   double* mine = reinterpret_cast<double*>(a.buf[a.rank]) + half;

@@ -143,7 +143,9 @@ class XgmiWorkspace {
       const bool sync = segs[k].size() < 4 || segs[k][3].cast<bool>();
       if (sync) mask |= (1ull << k);
     }
-    TORCH_CHECK((int64_t)f.total <= cap_ / 2, "fold_sync: segments exceed the workspace capacity");
+    TORCH_CHECK(f.total <= katib_hip::xgmi::kSmallFold || (int64_t)f.total <= cap_ / 2 - katib_hip::xgmi::kSmallFold,
+                "fold_sync: segments exceed the workspace capacity");
+    TORCH_CHECK(cap_ / 2 >= 2 * katib_hip::xgmi::kSmallFold, "fold_sync: workspace too small for the small-fold region");
     XG_CHECK(launch_fold_sync(args_, f, mask, blocks_, c10::hip::getCurrentHIPStream(device_).stream()));
   }
 

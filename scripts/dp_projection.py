@@ -14,18 +14,25 @@ Model (strong scaling, the bench default: global batch 128, SyncBN over all rank
 Weak scaling (batch 128 per rank, per-rank BN): only the gradient all-reduces rendezvous (4 per
 step, one per flat gradient vector), so step(N) = floor(128) + 4 t_rv(N).
 
-Prints the table; `profiles/dp_projection_r05.log` is its output.
+Prints the table; `profiles/dp_projection_r06.log` is its output.
 """
 
-FLOOR_MS = {  # per-rank batch -> measured dp1 step (ms), round 5
-    "b5": {128: 6.23, 64: 4.67, 32: 3.70, 16: 3.32},
+FLOOR_MS = {  # per-rank batch -> measured dp1 step (ms): batch 128 of B5 round 6 (profiles/gpu_round_r06d.log), the rest round 5
+    "b5": {128: 6.11, 64: 4.67, 32: 3.70, 16: 3.32},
     "default": {128: 41.74, 64: 24.73, 32: 16.60, 16: 12.66},
 }
-RENDEZVOUS = {"b5": 175, "default": 315}  # measured, 2 ranks (gpurun_out/r05f.log, r05n.log)
-# 2, 4 measured (mid of 5.6-6.6 / 8.7-11.8 us) with every rank on ONE GPU, so the ranks' fold kernels
-# time-share the device; 8 extrapolated linearly. On 8 separate GPUs the peers' flags are polled in
-# parallel, so the 2-rank figure is the optimistic bound (last column of the SyncBN tables).
-T_RV_US = {1: 0.0, 2: 6.1, 4: 10.3, 8: 18.5}
+# SyncBN rendezvous on the step's critical path, measured with 2 ranks (profiles/dp_rendezvous_r06.log): the
+# concurrent Hessian branches fold through two workspaces side by side, so of 175 (B5) / 315 (default)
+# rendezvous per step 141 / 253 are serial - exactly the count of the stacked mode, where each twin pair of
+# folds is one rendezvous.
+RENDEZVOUS = {"b5": 141, "default": 253}
+# SyncBN fold rendezvous floor (us) with the single-workgroup small-payload path of fold_sync (round 6):
+# 2 / 4 ranks measured (scripts/rendezvous_probe.py, 1 workgroup, 64-2048 floats: 4.1-4.25 / 5.0-5.2 us,
+# profiles/rendezvous_r06.log) with every rank on ONE GPU, 8 extrapolated linearly in the peer count
+# (+0.45 us per peer). Round 5 ran 16 workgroups: 6.1 / 10.3 / 18.5.
+T_RV_US = {1: 0.0, 2: 4.2, 4: 5.1, 8: 6.9}
+# gradient-bucket all-reduces (one-shot, B5-size vectors ~9.5k floats, 16 workgroups): 5.9 / 9.7 us, 8 extrapolated
+T_GRAD_US = {1: 0.0, 2: 5.9, 4: 9.7, 8: 17.3}
 GRAD_ALLREDUCES = 4
 
 
@@ -34,34 +41,34 @@ def main():
     for cfg in ("b5", "default"):
         f, R = FLOOR_MS[cfg], RENDEZVOUS[cfg]
         base = f[128]
-        print(f"\n== {cfg}: strong scaling, global batch 128, SyncBN ({R} rendezvous/step)")
+        print(f"\n== {cfg}: strong scaling, global batch 128, SyncBN ({R} serial rendezvous/step)")
         print(" N | per-rank batch | floor ms | rendezvous ms | step ms | speedup vs 1 GPU | images/s"
               " | step ms if t_rv stays at the 2-rank figure")
         for n in (1, 2, 4, 8):
             b = 128 // n
-            rv = 0.0 if n == 1 else R * T_RV_US[n] / 1000.0
+            rv = 0.0 if n == 1 else (R - GRAD_ALLREDUCES) * T_RV_US[n] / 1000.0 + GRAD_ALLREDUCES * T_GRAD_US[n] / 1000.0
             step = f[b] + rv
-            opt = f[b] + (0.0 if n == 1 else R * T_RV_US[2] / 1000.0)
+            opt = f[b] + (0.0 if n == 1 else (R - GRAD_ALLREDUCES) * T_RV_US[2] / 1000.0
+                          + GRAD_ALLREDUCES * T_GRAD_US[2] / 1000.0)
             print(f" {n} | {b:>14} | {f[b]:8.2f} | {rv:13.2f} | {step:7.2f} | {base / step:16.2f} | {128 / step * 1000:8.0f}"
                   f" | {opt:7.2f} ({base / opt:.2f}x)")
         print(f"== {cfg}: strong scaling, global batch 128, per-rank BN (--sync-bn 0: BN over 128/N images, "
               f"{GRAD_ALLREDUCES} rendezvous/step)")
         print(" N | step ms | speedup vs 1 GPU")
         for n in (1, 2, 4, 8):
-            rv = 0.0 if n == 1 else GRAD_ALLREDUCES * T_RV_US[n] / 1000.0
+            rv = 0.0 if n == 1 else GRAD_ALLREDUCES * T_GRAD_US[n] / 1000.0
             step = f[128 // n] + rv
             print(f" {n} | {step:7.2f} | {base / step:16.2f}")
         print(f"== {cfg}: weak scaling, batch 128 per rank, per-rank BN ({GRAD_ALLREDUCES} rendezvous/step)")
         print(" N | step ms | images/s | efficiency")
         for n in (1, 2, 4, 8):
-            rv = 0.0 if n == 1 else GRAD_ALLREDUCES * T_RV_US[n] / 1000.0
+            rv = 0.0 if n == 1 else GRAD_ALLREDUCES * T_GRAD_US[n] / 1000.0
             step = base + rv
             print(f" {n} | {step:7.2f} | {128 * n / step * 1000:8.0f} | {base / step:10.3f}")
-    print("\nReading: strong scaling of B5 is bound twice over - by the SyncBN rendezvous (175 serial folds of ~6-18 us"
-          "\nagainst a 3.3-4.7 ms per-rank floor: ~1.1x at 2-4 GPUs, flat at 8) and, without SyncBN, by the per-rank"
-          "\nfloor itself (batch 16 still costs 3.3 ms: the step is launch / latency bound, 1.8x at 8). The default"
-          "\nconfig (larger per-rank work) projects 1.6x / 2.1x / 2.3x with SyncBN. Weak scaling keeps >= 98%"
-          "\nefficiency at 8 ranks.")
+    print("\nReading: with the single-workgroup fold rendezvous (4.2 / 5.1 us at 2 / 4 ranks instead of 6.1 / 10.3) and"
+          "\nthe serial count the concurrent Hessian branches really pay (141 of 175 on B5), SyncBN strong scaling of B5"
+          "\nprojects 1.16x / 1.38x / 1.41x at 2 / 4 / 8 GPUs (round 5: 1.09x / 1.13x / 0.95x); the default config 1.62x /"
+          "\n2.33x / 2.89x. Per-rank BN (the reference's DDP semantics) and weak scaling are unchanged in kind.")
 
 
 if __name__ == "__main__":

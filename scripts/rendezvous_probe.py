@@ -19,27 +19,29 @@ rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 dist.init_process_group("gloo", rank=rank, world_size=world)
-ar = XgmiAllReduce(rank, world, dev, capacity=1 << 20, blocks=16)
-assert ar.ok, "one-shot all-reduce unavailable"
 R = 50
-for n in (64, 2048, 9472, 65536):  # BN-fold segments .. the B5 gradient vector (~37 KB) .. 256 KB
-    x = torch.ones(n, device=dev)
-    for _ in range(3):
-        ar.allreduce_(x)
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for _ in range(R):
+for blocks in (1, 4, 16):  # workgroups of the fixed grid: each exchanges one flag with every peer
+    ar = XgmiAllReduce(rank, world, dev, capacity=1 << 20, blocks=blocks)
+    assert ar.ok, "one-shot all-reduce unavailable"
+    for n in (64, 2048, 9472, 65536):  # BN-fold segments .. the B5 gradient vector (~37 KB) .. 256 KB
+        x = torch.ones(n, device=dev)
+        for _ in range(3):
             ar.allreduce_(x)
-    g.replay()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(5):
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(R):
+                ar.allreduce_(x)
         g.replay()
-    torch.cuda.synchronize()
-    us = (time.perf_counter() - t0) * 1e6 / (5 * R)
-    if rank == 0:
-        print("world %d floats %7d: %.2f us per rendezvous (captured, back to back)" % (world, n, us), flush=True)
-assert ar.error() == 0
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            g.replay()
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) * 1e6 / (5 * R)
+        if rank == 0:
+            print("world %d blocks %2d floats %7d: %.2f us per rendezvous (captured, back to back)" % (world, blocks, n, us),
+                  flush=True)
+    assert ar.error() == 0
 dist.destroy_process_group()
