@@ -340,6 +340,7 @@ def main():
             "xgmi_self_test": comm.xgmi_status if comm.distributed else None,
             "syncbn_path": search._hsync.path if getattr(search, "_hsync", None) is not None else None,
             "rendezvous_per_step": search.rendezvous_per_step if comm.distributed else 0,
+            "rendezvous_serial_per_step": search.rendezvous_serial_per_step if comm.distributed else 0,
             "rendezvous_in_graph": search.rendezvous_in_graph if comm.distributed else None,
             "hessian_stack": search.stack_stats,
             "batchnorm": ("global batch (sync-bn)" if sync_bn else

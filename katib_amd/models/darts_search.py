@@ -198,6 +198,7 @@ class DartsSearch:
         self._one = None
         self.graphs = None
         self.rendezvous_per_step = None  # cross-rank rendezvous per step (set by the first step)
+        self.rendezvous_serial_per_step = None  # ... of them on the critical path (not on a concurrent branch)
         self.rendezvous_in_graph = None
         self.static = None
         self._eval_graphs = {}  # (x shape, y shape, dtypes) -> (graph, static x, static y, [loss, top1, top5])
@@ -435,6 +436,12 @@ class DartsSearch:
                 n += sy.comm.calls
         return n
 
+    def _side_folds(self) -> int:
+        sy = self._hsync_side
+        if sy is None:
+            return 0
+        return sy.folds if sy.ws is not None else sy.comm.calls
+
     def _build_graphs(self):
         segs = self._segments()
         # merge segments with no host-side collective in between: all of them at world size 1
@@ -462,6 +469,7 @@ class DartsSearch:
         torch.cuda.current_stream().wait_stream(s)
         graphs = []
         n0 = self._rendezvous()
+        side0 = self._side_folds()
         for fns, colls in groups:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g), self._scope():
@@ -472,6 +480,8 @@ class DartsSearch:
         # inside the graphs (captured once, replayed every step) + the host-side ones per replay
         self.rendezvous_per_step = self._rendezvous() - n0 + (
             sum(len(c) for _, c in graphs) if self.comm.distributed else 0)
+        # the concurrent Hessian branch's folds run beside the main branch's: not on the critical path
+        self.rendezvous_serial_per_step = self.rendezvous_per_step - (self._side_folds() - side0)
         self.rendezvous_in_graph = not any(c for _, c in graphs)
 
     def _state_tensors(self):
@@ -518,9 +528,10 @@ class DartsSearch:
                 for t in colls:
                     self.comm.allreduce_mean_(t)
         else:
-            n0 = self._rendezvous()
+            n0, side0 = self._rendezvous(), self._side_folds()
             self._run_eager()
             self.rendezvous_per_step = self._rendezvous() - n0
+            self.rendezvous_serial_per_step = self.rendezvous_per_step - (self._side_folds() - side0)
             self.rendezvous_in_graph = False
         return self.loss_out
 

@@ -63,6 +63,8 @@ def test_bench_two_ranks_strong_scaling():
     # physical devices behind the ranks (both ranks on this one host's CPU: 1)
     assert r["per_rank_bn_ms_per_step"] > 0 and r["per_rank_bn_search_wall_s"] > 0
     assert r["distinct_devices"] == 1
+    # CPU: torch ops, sequential Hessian passes -> every rendezvous is on the critical path
+    assert r["rendezvous_serial_per_step"] == r["rendezvous_per_step"] > 4
 
 
 def test_bench_two_ranks_weak_scaling_label():
