@@ -27,12 +27,19 @@ def main():
                          num_nodes=3, stem_multiplier=1)
     B, W, r = 64, comm.world_size, comm.rank
     g = torch.Generator().manual_seed(11)
+    # a learnable task (class-dependent channel means) and a larger alpha lr, as in the 30-step trajectory
+    # test: the architecture then moves by gradient signal, so its genotype is decided by the search and
+    # not by rounding noise (pure-noise batches left the alphas at ~7e-3 from init, where a near-tie
+    # between two edges could flip on summation order alone)
+    proto = torch.randn(10, 3, 1, 1, generator=g)
     data = []
     for _ in range(steps):
-        tx, vx = torch.randn(B, 3, 32, 32, generator=g), torch.randn(B, 3, 32, 32, generator=g)
         ty, vy = torch.randint(0, 10, (B,), generator=g), torch.randint(0, 10, (B,), generator=g)
+        tx = proto[ty] + 0.5 * torch.randn(B, 3, 32, 32, generator=g)
+        vx = proto[vy] + 0.5 * torch.randn(B, 3, 32, 32, generator=g)
         data.append([t.to(dev) for t in (tx, ty, vx, vy)])
-    dp = DartsSearch(layout, dev, comm, seed=3, capture=True, sync_bn=sync)
+    settings = {"alpha_lr": 3e-2}
+    dp = DartsSearch(layout, dev, comm, seed=3, capture=True, sync_bn=sync, settings=settings)
     sl = slice(r * B // W, (r + 1) * B // W)
     W1 = None
     verbose = os.environ.get("SYNCBN_VERBOSE") == "1"
@@ -50,7 +57,7 @@ def main():
            "loss": float(dp.loss_out), "capture": dp.capture, "allreduce": "xgmi" if comm.xgmi else comm.backend}
     comm.barrier()
     if r == 0:
-        single = DartsSearch(layout, dev, Comm(device=dev), seed=3, capture=True)
+        single = DartsSearch(layout, dev, Comm(device=dev), seed=3, capture=True, settings=settings)
         A0 = single.A.clone()
         dW1 = None
         for i, (tx, ty, vx, vy) in enumerate(data):
@@ -60,7 +67,7 @@ def main():
         torch.cuda.synchronize()
         # run-to-run noise of the single-process search itself (float atomics: summation order
         # varies between runs; Adam turns near-zero alpha gradients' rounding into O(lr) steps)
-        again = DartsSearch(layout, dev, Comm(device=dev), seed=3, capture=True)
+        again = DartsSearch(layout, dev, Comm(device=dev), seed=3, capture=True, settings=settings)
         for tx, ty, vx, vy in data:
             again.step(tx, ty, vx, vy)
         torch.cuda.synchronize()

@@ -1,7 +1,7 @@
 """SyncBN on the HIP DARTS path: a 2-rank strong-scaling step with half the
 batch per rank and global-batch BN (fused fold + cross-rank sum launch, captured with the rest of
 the step) follows the single-process batch-64 search - genotype equal and alpha drift within 5 %
-of the alphas' displacement after 30 steps - while per-rank BN does not. The ranks share the box's
+of the alphas' displacement after 30 steps of a learnable task - while per-rank BN does not. The ranks share the box's
 GPU through IPC (the same protocol as peers over xGMI)."""
 import json
 import os
@@ -38,11 +38,10 @@ def test_gpu_syncbn_two_ranks_match_single_process():
     res = _run(True)
     print(res)
     assert res["capture"] and res["allreduce"] == "xgmi", res
-    # the genotype of 30-step alphas (displacement ~7e-3) can flip on rounding alone: require it
-    # equal unless two single-process runs of the same search disagree as well, or the alphas
-    # themselves agree to within 5 % of their displacement (then the flip is a near-tie between two
-    # edges: seen once in round 5 with dA 2.2e-4 against a 3.6e-4 bound, single-process pair equal)
-    assert res["geno_equal"] or not res["geno_ss_equal"] or res["dA"] <= 0.05 * res["A_disp"], res
+    # the search moves the alphas by gradient signal (learnable task, alpha lr 3e-2: displacement well above
+    # the rounding-driven spread), so the genotype must match exactly (no escape clause)
+    assert res["A_disp"] > 1e-2, res
+    assert res["geno_equal"] and res["geno_ss_equal"], res
     # alpha drift within 5 % of the alphas' displacement, or within 3x the single-process search's
     # own run-to-run spread (float-atomic summation order)
     assert res["dA"] <= max(0.05 * res["A_disp"], 3 * res["dA_ss"]), res
@@ -52,3 +51,5 @@ def test_gpu_syncbn_two_ranks_match_single_process():
     per_rank = _run(False)
     print(per_rank)
     assert per_rank["dW1"] > 10 * max(res["dW1"], 1e-7), (per_rank, res)
+    # and the architecture it finds drifts far more than SyncBN's (r06: dA 0.16 vs 5.3e-4)
+    assert per_rank["dA"] > 10 * res["dA"], (per_rank, res)
