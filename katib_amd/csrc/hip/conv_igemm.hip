@@ -45,6 +45,21 @@ constexpr int kBK = 64;       // reduction depth per LDS stage
 constexpr int kPad = 8;       // bf16 row padding (16 B)
 constexpr int kThreads = 256;  // 4 waves as 2 x 2
 
+// Division by a runtime divisor d as a multiply-high (Granlund-Montgomery round-up form):
+// n / d = (umulhi(n, m) + n) >> s, exact for n < 2^31 (host-side make_fastdiv). The wgrad gather
+// decomposes every staged pixel index into (image, row, column): two integer divisions per
+// 16-byte load were ~70 VALU instructions each (profiles/conv_wgrad_r06.log).
+struct FastDiv {
+  unsigned m, s;
+};
+FastDiv make_fastdiv(unsigned d) {
+  unsigned s = 0;
+  while ((1ull << s) < d) ++s;
+  const unsigned long long m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return FastDiv{(unsigned)m, s};
+}
+__device__ __forceinline__ unsigned fdiv(unsigned n, FastDiv f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
 __device__ inline int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -250,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void igemm_kernel(ConvGeom g, const bf16*
 template <int BMW, int BNW>
 __global__ __launch_bounds__(kThreads) void wgrad_kernel(ConvGeom g, const bf16* __restrict__ x,
                                                          const bf16* __restrict__ dy, float* __restrict__ dw, int P,
-                                                         int Kd, int chunk) {
+                                                         int Kd, int chunk, FastDiv fd_hw, FastDiv fd_ow) {
   constexpr int BP = 64;  // pixels per LDS stage (2 MFMA k-steps)
   constexpr int WM = BMW / 2, WN = BNW / 2, RM = WM / 16, RN = WN / 16;
   constexpr int LDA = BMW + kPad, LDB = BNW + kPad;
@@ -286,8 +301,9 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(ConvGeom g, const bf16*
     b_col[i] = col;
     const int rs = col / g.C;
     b_c[i] = col - rs * g.C;
-    b_r[i] = rs / g.S;
-    b_s[i] = rs - b_r[i] * g.S;
+    const int r = rs / g.S;
+    b_r[i] = r * g.dh - g.ph;  // input row / column offsets of the tap: ih = oh * sh + b_r
+    b_s[i] = (rs - r * g.S) * g.dw - g.pw;
   }
   u32x4 ra[AC], rb[BC];
   const u32x4 zero = {0u, 0u, 0u, 0u};
@@ -295,19 +311,22 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(ConvGeom g, const bf16*
 #pragma unroll
     for (int i = 0; i < AC; ++i) {
       const int p = p0 + a_prow[i];
-      ra[i] = (p < p_end && a_col[i] < K) ? *reinterpret_cast<const u32x4*>(dy + (int64_t)p * K + a_col[i]) : zero;
+      // unconditional load from a clamped offset, zero selected afterwards: straight-line code
+      // instead of one exec-masked branch per load
+      const bool ok = p < p_end && a_col[i] < K;
+      const u32x4 t = *reinterpret_cast<const u32x4*>(dy + (ok ? p * K + a_col[i] : 0));
+      ra[i] = ok ? t : zero;
     }
 #pragma unroll
     for (int i = 0; i < BC; ++i) {
       const int p = p0 + b_prow[i];
-      u32x4 v = zero;
-      if (p < p_end && b_col[i] < Kd) {
-        const int n = p / hw, rem = p - n * hw, oh = rem / g.OW, ow = rem - oh * g.OW;
-        const int ih = oh * g.sh - g.ph + b_r[i] * g.dh, iw = ow * g.sw - g.pw + b_s[i] * g.dw;
-        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-          v = *reinterpret_cast<const u32x4*>(x + ((int64_t)(n * g.H + ih) * g.W + iw) * g.C + b_c[i]);
-      }
-      rb[i] = v;
+      // 32-bit offsets: the binding bounds N*H*W*C and N*OH*OW*K below 2^31
+      const int n = (int)fdiv((unsigned)p, fd_hw), rem = p - n * hw, oh = (int)fdiv((unsigned)rem, fd_ow),
+                ow = rem - oh * g.OW;
+      const int ih = oh * g.sh + b_r[i], iw = ow * g.sw + b_s[i];
+      const bool ok = p < p_end && b_col[i] < Kd && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const u32x4 t = *reinterpret_cast<const u32x4*>(x + (ok ? ((n * g.H + ih) * g.W + iw) * g.C + b_c[i] : 0));
+      rb[i] = ok ? t : zero;
     }
   };
   auto sstore = [&](int buf) {
@@ -575,6 +594,9 @@ hipError_t launch_wgrad(const ConvGeom& g, const bf16* x, const bf16* dy, float*
   // Round-5 sweep on the ResNet-18 shapes (profiles/conv_graph_table_r05.log): 2048 WGs / >= 4
   // stages (the old policy) 1.64 ms for the nine layers' fwd+bwd, 512 / >= 16: 1.42 ms - the
   // 128 x 128 tiles of l2-l4 spent most of their time in atomics (l3 wgrad 110 -> 61 us).
+  // Round 6 (profiles/conv_wgrad_r06.log): split-K slabs + a reduce launch instead of the atomics,
+  // and operand loads issued two stages ahead, both measured slower; the gather's divisions went
+  // to FastDiv (nine layers 500 -> 476 us).
   constexpr int target_wg = 512, min_stages = 16;
   int splits = (target_wg + tiles - 1) / tiles;
   const int max_splits = (P + min_stages * BP - 1) / (min_stages * BP);  // >= min_stages stages per block
@@ -584,14 +606,15 @@ hipError_t launch_wgrad(const ConvGeom& g, const bf16* x, const bf16* dy, float*
   chunk = (chunk + BP - 1) / BP * BP;
   splits = (P + chunk - 1) / chunk;
   dim3 grid(tiles, splits);
+  const FastDiv fh = make_fastdiv((unsigned)(g.OH * g.OW)), fo = make_fastdiv((unsigned)g.OW);
   if (wideM && wideN)
-    hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk);
+    hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk, fh, fo);
   else if (wideM)
-    hipLaunchKernelGGL((wgrad_kernel<128, 64>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk);
+    hipLaunchKernelGGL((wgrad_kernel<128, 64>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk, fh, fo);
   else if (wideN)
-    hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk);
+    hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk, fh, fo);
   else
-    hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk);
+    hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(kThreads), 0, st, g, x, dy, dw32, P, Kd, chunk, fh, fo);
   return hipGetLastError();
 }
 

@@ -90,6 +90,25 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
   float* sMean = smem;                                 // [ne][kMaxOps][C]
   float* sInv = sMean + ne * kMaxOps * C;              // [ne][kMaxOps][C]
   float* sW = sInv + ne * kMaxOps * C;                 // [ne][kMaxOps + 1]
+  // V4: the first element's operands are loaded BEFORE the coefficient prologue - they do not
+  // depend on it, so their memory round trip overlaps the statistic loads instead of following
+  // the barrier (two serial round trips per block -> one)
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int EM = CombineFwdBatch::kCap;
+  const size_t total4 = total / 4;
+  f4 zv[EM][kMaxOps], xv[EM];
+  auto load4 = [&](size_t i4) {
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      const CombineFwdArgs& a = bt.e[e < ne ? e : 0];
+#pragma unroll
+      for (int k = 0; k < kMaxOps; ++k)
+        if (e < ne && k < a.nops) zv[e][k] = zld4(a.z[k] + 4 * i4);
+      if (e < ne && a.xid) xv[e] = reinterpret_cast<const f4*>(a.xid)[i4];
+    }
+  };
+  size_t i4 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (V4 && i4 < total4) load4(i4);
   // every (edge, op, channel) coefficient in one pass: one round of statistic loads per block
   if (ne == 1 && a0.nops == 1 && !a0.bn[0].eval && a0.bn[0].rep > 1) {
     // a preprocess BN whose statistics arrive unfolded (their fold joins the cell's first node's)
@@ -137,22 +156,12 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
   if (V4) {
     // 4 consecutive elements per thread (HW % 4 == 0: one channel), 16-byte loads/stores;
     // the host picks this path only when every operand pointer is 16-byte aligned
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    const size_t total4 = total / 4;
-    constexpr int EM = CombineFwdBatch::kCap;
-    for (size_t i4 = (size_t)blockIdx.x * 256 + threadIdx.x; i4 < total4; i4 += (size_t)gridDim.x * 256) {
+    // every operand load of an element is issued first (up to EM * (kMaxOps + 1) in flight), then
+    // accumulated in the scalar path's order: a runtime-bounded load-then-add loop waited on each
+    // load in turn. The first element's loads went out before the prologue.
+    for (bool first = true; i4 < total4; i4 += (size_t)gridDim.x * 256, first = false) {
       const int c = (int)((i4 * 4 / HW) % C);
-      // issue every operand load first (up to EM * (kMaxOps + 1) in flight), then accumulate in
-      // the scalar path's order: a runtime-bounded load-then-add loop waited on each load in turn
-      f4 zv[EM][kMaxOps], xv[EM];
-#pragma unroll
-      for (int e = 0; e < EM; ++e) {
-        const CombineFwdArgs& a = bt.e[e < ne ? e : 0];
-#pragma unroll
-        for (int k = 0; k < kMaxOps; ++k)
-          if (e < ne && k < a.nops) zv[e][k] = zld4(a.z[k] + 4 * i4);
-        if (e < ne && a.xid) xv[e] = reinterpret_cast<const f4*>(a.xid)[i4];
-      }
+      if (!first) load4(i4);
       f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int e = 0; e < EM; ++e) {
