@@ -347,7 +347,8 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
     sRed[tid] = 0.f;
     sRed[C + tid] = 0.f;
   }
-  __syncthreads();
+  // only the input-BN staging reads the prologue's LDS (sMean / sInv) before the staging barrier
+  if (PREBN) __syncthreads();
   KSTAMP(1);
   // staging with 16-byte loads (the band's rows are contiguous per channel; W, Wo % 4 == 0):
   // many wide loads in flight per wave, which the one-row-per-wave scalar loop lacked

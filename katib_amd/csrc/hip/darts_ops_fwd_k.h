@@ -171,7 +171,9 @@ __device__ __forceinline__ void dwpw_plane_body(const DwPwFwdArgs& a, const int 
     sStat[tid] = 0.f;
     sStat[C + tid] = 0.f;
   }
-  __syncthreads();
+  // only the input-BN staging reads the prologue's LDS (sMean / sInv) before the staging barrier:
+  // without an input BN the weight loads and the staging loads share one round trip
+  if (PREBN) __syncthreads();
   KSTAMP(1);
   const size_t xin = ((size_t)n * a.C + c0) * H * W;
   if (VEC) {
