@@ -424,50 +424,59 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
     // 32 banks: 4-way conflicts)
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int NQ = (4 + 2 * PAD + 3) / 4;
-    for (int p = 4 * tid; p < ((dbg & 1) ? 0 : NP); p += 1024) {
+    // work item = (channel, pixel quad), channel-major: with the channel loop inside the thread
+    // only NP / 4 threads had work (64 of 256 for an 8-row band of a 32-wide plane), each walking
+    // C channels with nothing to hide its LDS latency behind; now every thread takes one item and a
+    // wave holds one channel whenever NP / 4 is a multiple of 64 (uniform weight reads)
+    const int NQ4 = NP / 4;
+    for (int j = tid; j < ((dbg & 1) ? 0 : C * NQ4); j += 256) {
+      const int c = j / NQ4, p = (j - c * NQ4) * 4;
       const int r = p / W, ix = p - r * W, iy = iy0 + r;
       int srow[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) srow[k] = (iy + PAD - k * DIL - oyA) * ODW + ix;
+      KEEP_WEIGHT_READS_LOCAL();
+      const float* wk = sWt + c * KK;
+      const float* dd = sDD + c * ODR * ODW;
+      f4 ga = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        KEEP_WEIGHT_READS_LOCAL();
-        const float* wk = sWt + c * KK;  // LDS broadcast reads
-        const float* dd = sDD + c * ODR * ODW;
-        f4 ga = {0.f, 0.f, 0.f, 0.f};
+      for (int ky = 0; ky < K; ++ky) {
+        float v[4 * NQ];  // v[m] = dd column ix + m
 #pragma unroll
-        for (int ky = 0; ky < K; ++ky) {
-          float v[4 * NQ];  // v[m] = dd column ix + m
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) {
-            const float4 t = *reinterpret_cast<const float4*>(dd + srow[ky] + 4 * q);
-            v[4 * q] = t.x;
-            v[4 * q + 1] = t.y;
-            v[4 * q + 2] = t.z;
-            v[4 * q + 3] = t.w;
-          }
-#pragma unroll
-          for (int kx = 0; kx < K; ++kx) {
-            const float w = wk[ky * K + kx];
-            const int o = 2 * PAD - kx * DIL;  // pixel ix + t meets dd column ix + t + o
-            ga.x += w * v[o];
-            ga.y += w * v[o + 1];
-            ga.z += w * v[o + 2];
-            ga.w += w * v[o + 3];
-          }
+        for (int q = 0; q < NQ; ++q) {
+          const float4 t = *reinterpret_cast<const float4*>(dd + srow[ky] + 4 * q);
+          v[4 * q] = t.x;
+          v[4 * q + 1] = t.y;
+          v[4 * q + 2] = t.z;
+          v[4 * q + 3] = t.w;
         }
-        const int li = (c * nrow + r) * W + ix;
-        const f4 act = *reinterpret_cast<const f4*>(sIn + li);
-        const f4 g = {act.x > 0.f ? ga.x : 0.f, act.y > 0.f ? ga.y : 0.f, act.z > 0.f ? ga.z : 0.f,
-                      act.w > 0.f ? ga.w : 0.f};
-        f4* dst = reinterpret_cast<f4*>(gn + ((size_t)c * H + iy) * W + ix);
-        if (PREBN) {
-          *dst = g;
-          st1[c] += (g.x + g.y) + (g.z + g.w);
-          st2[c] += (g.x * act.x + g.y * act.y) + (g.z * act.z + g.w * act.w);
-        } else {
-          *dst = accum ? *reinterpret_cast<const f4*>(sOld + li) + g : g;
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const float w = wk[ky * K + kx];
+          const int o = 2 * PAD - kx * DIL;  // pixel ix + t meets dd column ix + t + o
+          ga.x += w * v[o];
+          ga.y += w * v[o + 1];
+          ga.z += w * v[o + 2];
+          ga.w += w * v[o + 3];
         }
+      }
+      const int li = (c * nrow + r) * W + ix;
+      const f4 act = *reinterpret_cast<const f4*>(sIn + li);
+      const f4 g = {act.x > 0.f ? ga.x : 0.f, act.y > 0.f ? ga.y : 0.f, act.z > 0.f ? ga.z : 0.f,
+                    act.w > 0.f ? ga.w : 0.f};
+      f4* dst = reinterpret_cast<f4*>(gn + ((size_t)c * H + iy) * W + ix);
+      if (PREBN) {
+        *dst = g;
+        const float t1 = (g.x + g.y) + (g.z + g.w);
+        const float t2 = (g.x * act.x + g.y * act.y) + (g.z * act.z + g.w * act.w);
+#pragma unroll
+        for (int cc = 0; cc < C; ++cc)  // select into the register arrays (no dynamic index)
+          if (cc == c) {
+            st1[cc] += t1;
+            st2[cc] += t2;
+          }
+      } else {
+        *dst = accum ? *reinterpret_cast<const f4*>(sOld + li) + g : g;
       }
     }
   }
@@ -572,15 +581,21 @@ __device__ __forceinline__ void dw_bwd_plane_body(const DwBwdArgs& a, const int 
     // stride 1: job = (channel, ky, own row). A 4-pixel quad of the input row (one 16-byte LDS
     // read) and the 4 + 2*PAD dd values it meets across all K column taps (registers) feed
     // 4*K multiply-adds: ~1.5 per LDS read against 0.5 for a pixel-by-pixel walk per tap
-    const int JB = C * K * nrow;
-    for (int j = tid; j < JB; j += 256) {
-      const int c = j / (K * nrow), rem = j - c * K * nrow, ky = rem / nrow, r = rem - ky * nrow;
+    // job = (row part, channel, ky, row); when the C * K * nrow jobs leave threads idle, each row
+    // is split into XP column parts (XP | W / 4), a partial sum each
+    const int JB = C * K * nrow, W4 = W / 4;
+    int XP = 1;
+    while (XP * 2 * JB <= 256 && W4 % (XP * 2) == 0) XP *= 2;
+    const int XW = W / XP;
+    for (int j = tid; j < JB * XP; j += 256) {
+      const int xp = j / JB, jj = j - xp * JB;
+      const int c = jj / (K * nrow), rem = jj - c * K * nrow, ky = rem / nrow, r = rem - ky * nrow;
       const float* ddr = sDD + (c * ODR + iy0 + r + PAD - ky * DIL - oyA) * ODW + PO;
       const float* inr = sIn + c * NP + r * W;
       float acc[K];
 #pragma unroll
       for (int kx = 0; kx < K; ++kx) acc[kx] = 0.f;
-      for (int ix = 0; ix < W; ix += 4) {
+      for (int ix = xp * XW; ix < (xp + 1) * XW; ix += 4) {
         const float4 v = *reinterpret_cast<const float4*>(inr + ix);
         // dseg[m] = dd[ix - PAD + m]: dd column ix - PAD + PO + m = ix + m (PO = PAD at stride 1),
         // whole aligned quads from ix (ds_read_b128; ODW = lds_pitch)
