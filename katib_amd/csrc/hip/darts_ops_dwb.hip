@@ -170,13 +170,56 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
   // the plane's BN coefficients: four threads each sum one pair over the replicas
   __shared__ float sCo[8];
   KSTAMP(0);
-  if (threadIdx.x < 8) sCo[threadIdx.x] = (threadIdx.x & 1) ? 1.f : 0.f;
-  __syncthreads();
-  if (threadIdx.x == 0 && a.ga.z) bn_coeffs(a.ga.bn, c, sCo[0], sCo[1]);
-  if (threadIdx.x == 128 && a.gm.z) bn_coeffs(a.gm.bn, c, sCo[4], sCo[5]);
-  // BN-backward means: the reductions may arrive unfolded (workgroup-cooperative replica sums)
-  if (a.ga.z) gs_means_coop(a.ga, c, 1, sCo + 2, sCo + 3);
-  if (a.gm.z) gs_means_coop(a.gm, c, 1, sCo + 6, sCo + 7);
+  // all four replica pair-sums in ONE memory round trip: wave 0's 16-lane groups take the avg
+  // pool's BN statistics, the max pool's, and the two BN-backward sums (S1, S2) each - folded
+  // (rep 1) or not (rep kRep: two loads per lane). One thread per BN walking kRep replicas in
+  // rounds of 8 was four dependent round trips (~2.8 us of a ~10 us workgroup, phase stamps r06)
+  if (threadIdx.x < 64) {
+    const int grp = threadIdx.x >> 4, j = threadIdx.x & 15;
+    const GradSrc& gs = grp & 1 ? a.gm : a.ga;
+    const bool on = gs.z != nullptr, stats = grp < 2;
+    const BNRef& b = gs.bn;
+    double s = 0.0, s2 = 0.0;
+    if (on && stats && !b.eval) {
+      for (int r = j; r < b.rep; r += 16) {
+        s += b.sums[(size_t)r * b.rstride + c];
+        s2 += b.sums[(size_t)r * b.rstride + b.C + c];
+      }
+    } else if (on && !stats && !gs.eval) {
+      const int rep = gs.rep, rs = gs.rep == 1 ? 0 : gs.rstride;
+      const size_t off2 = gs.S2 - gs.S1;
+      for (int r = j; r < rep; r += 16) {
+        s += gs.S1[(size_t)r * rs + c];
+        s2 += gs.S1[(size_t)r * rs + off2 + c];
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if (j == 0) {
+      float* o = sCo + 4 * (grp & 1) + (stats ? 0 : 2);
+      if (!on) {
+        o[0] = 0.f;
+        o[1] = stats ? 1.f : 0.f;
+      } else if (stats) {
+        if (b.eval) {
+          o[0] = b.rmean[c];
+          o[1] = rsqrtf(b.rvar[c] + b.eps);
+        } else {  // as bn_moments / bn_coeffs
+          const double m = s * (double)b.inv_count;
+          double v = s2 * (double)b.inv_count - m * m;
+          if (v < 0) v = 0;
+          o[0] = (float)m;
+          o[1] = rsqrtf((float)v + b.eps);
+        }
+      } else {  // as gs_means
+        o[0] = gs.eval ? 0.f : (float)(s * (double)gs.bn.inv_count);
+        o[1] = gs.eval ? 0.f : (float)(s2 * (double)gs.bn.inv_count);
+      }
+    }
+  }
   __syncthreads();
   KSTAMP(1);
   const float ma = sCo[0], ia = sCo[1], a1 = a.ga.z ? sCo[2] : 0.f, a2 = a.ga.z ? sCo[3] : 0.f;
