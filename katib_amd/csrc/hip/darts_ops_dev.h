@@ -189,6 +189,62 @@ __device__ __forceinline__ void gs_means_coop(const GradSrc& gs, int c0, int n, 
   coop_pair_sums(gs.S1 + c0, gs.S2 + c0, gs.rep, gs.rstride, n, (double)gs.bn.inv_count, m1, m2, false, 0.f);
 }
 
+// A backward kernel's BN coefficients (mean, 1 / std) AND BN-backward means (m1, m2) of channels
+// [c0, c0 + n) in ONE memory round trip: 16-lane groups, the first n on the statistics, the next n
+// on the BN-backward sums, each folded (rep 1) or not (kRep replicas: a few loads per lane). The
+// per-channel bn_coeffs threads followed by a cooperative gs_means_coop were two dependent trips
+// (plus kRep / 8 more when the statistics arrived unfolded). Every thread calls; the caller
+// barriers before reading. Needs 32 n <= blockDim.x (falls back to the two-step form otherwise).
+__device__ __forceinline__ void bn_gs_coop(const GradSrc& gs, int c0, int n, float* mean, float* inv, float* m1,
+                                           float* m2) {
+  const BNRef& b = gs.bn;
+  if (32 * n > (int)blockDim.x) {
+    for (int c = threadIdx.x; c < n; c += blockDim.x) bn_coeffs(b, c0 + c, mean[c], inv[c]);
+    gs_means_coop(gs, c0, n, m1, m2);
+    return;
+  }
+  const int grp = threadIdx.x >> 4, j = threadIdx.x & 15;
+  const bool stats = grp < n, act = grp < 2 * n;
+  const int ch = c0 + (stats ? grp : grp - n);
+  double s = 0.0, s2 = 0.0;
+  if (act && stats && !b.eval) {
+    for (int r = j; r < b.rep; r += 16) {
+      s += b.sums[(size_t)r * b.rstride + ch];
+      s2 += b.sums[(size_t)r * b.rstride + b.C + ch];
+    }
+  } else if (act && !stats && !gs.eval) {
+    const int rs = gs.rep == 1 ? 0 : gs.rstride;
+    const size_t off2 = gs.S2 - gs.S1;
+    for (int r = j; r < gs.rep; r += 16) {
+      s += gs.S1[(size_t)r * rs + ch];
+      s2 += gs.S1[(size_t)r * rs + off2 + ch];
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if (act && j == 0) {
+    const int k = ch - c0;
+    if (stats) {
+      if (b.eval) {
+        mean[k] = b.rmean[ch];
+        inv[k] = rsqrtf(b.rvar[ch] + b.eps);
+      } else {  // as bn_moments / bn_coeffs
+        const double m = s * (double)b.inv_count;
+        double v = s2 * (double)b.inv_count - m * m;
+        if (v < 0) v = 0;
+        mean[k] = (float)m;
+        inv[k] = rsqrtf((float)v + b.eps);
+      }
+    } else {  // as gs_means
+      m1[k] = gs.eval ? 0.f : (float)(s * (double)b.inv_count);
+      m2[k] = gs.eval ? 0.f : (float)(s2 * (double)b.inv_count);
+    }
+  }
+}
+
 __device__ __forceinline__ int rep_slot() { return blockIdx.x % kRep; }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -26,9 +26,9 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdBatch bt) {
   float* sM2 = sM1 + Cout;
   float* sW = sM2 + Cout;        // [1]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (int c = tid; c < Cout; c += 256) bn_coeffs(a.gs.bn, a.co_off + c, sMean[c], sInv[c]);
-  gs_means_coop(a.gs, a.co_off, Cout, sM1, sM2);
-  if (tid == 0) sW[0] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
+  const float wv = (tid == 0 && a.gs.w) ? a.gs.w[a.gs.widx] : 1.f;  // issued with the coefficient loads
+  bn_gs_coop(a.gs, a.co_off, Cout, sMean, sInv, sM1, sM2);
+  if (tid == 0) sW[0] = wv;
   __syncthreads();
   const float wk = sW[0];
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -192,9 +192,9 @@ __global__ void __launch_bounds__(256) pw_bwd_px_kernel(PwBwdBatch bt) {
   __shared__ float sC[4 * CO + 1];
   __shared__ float sGW[CI * CO];
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int c = tid; c < CO; c += 256) bn_coeffs(a.gs.bn, a.co_off + c, sC[c], sC[CO + c]);
-  gs_means_coop(a.gs, a.co_off, CO, sC + 2 * CO, sC + 3 * CO);  // the BN-backward sums may arrive unfolded
-  if (tid == 0) sC[4 * CO] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
+  const float wv = (tid == 0 && a.gs.w) ? a.gs.w[a.gs.widx] : 1.f;  // issued with the coefficient loads
+  bn_gs_coop(a.gs, a.co_off, CO, sC, sC + CO, sC + 2 * CO, sC + 3 * CO);  // BN-backward sums may arrive unfolded
+  if (tid == 0) sC[4 * CO] = wv;
   for (int i = tid; i < CI * CO; i += 256) sGW[i] = 0.f;
   __syncthreads();
   float mean[CO], inv[CO], m1[CO], m2[CO];
@@ -353,9 +353,9 @@ __global__ void __launch_bounds__(256) pw_bwd_wave_kernel(PwBwdBatch bt) {
   __shared__ float sC[4 * CO + 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int c16 = lane & 15, q = lane >> 4;
-  for (int c = tid; c < CO; c += 256) bn_coeffs(a.gs.bn, a.co_off + c, sC[c], sC[CO + c]);
-  gs_means_coop(a.gs, a.co_off, CO, sC + 2 * CO, sC + 3 * CO);
-  if (tid == 0) sC[4 * CO] = a.gs.w ? a.gs.w[a.gs.widx] : 1.f;
+  const float wv = (tid == 0 && a.gs.w) ? a.gs.w[a.gs.widx] : 1.f;  // issued with the coefficient loads
+  bn_gs_coop(a.gs, a.co_off, CO, sC, sC + CO, sC + 2 * CO, sC + 3 * CO);
+  if (tid == 0) sC[4 * CO] = wv;
   __syncthreads();
   const float wk = sC[4 * CO];
   float mean[BO], inv[BO], m1[BO], m2[BO];
