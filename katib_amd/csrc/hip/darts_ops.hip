@@ -80,6 +80,40 @@ bool stamps_compiled() {
 // ------------------------------------------------------------------------------------------------
 // combine_fwd: out = sum_k w[k] * BN_k(z_k) + wid * x  (elementwise), running stats in block 0
 // ------------------------------------------------------------------------------------------------
+// Split form of bn_coeffs for prologues that overlap the statistic loads with operand loads:
+// bn_raw issues the loads (a folded or eval BN: two loads; unfolded: the replica walk), bn_finish
+// turns them into (mean, 1 / std) after the caller has issued its other loads - s_waitcnt vmcnt is
+// in order, so loads issued AFTER the statistic loads do not delay them.
+struct BnRaw {
+  double s, s2;
+  float rm, rv;
+};
+__device__ __forceinline__ BnRaw bn_raw(const BNRef& b, int c) {
+  BnRaw r{0.0, 0.0, 0.f, 1.f};
+  if (b.eval) {
+    r.rm = b.rmean[c];
+    r.rv = b.rvar[c];
+  } else if (b.rep == 1) {
+    r.s = b.sums[c];
+    r.s2 = b.sums[b.C + c];
+  } else {
+    sum_replicas(b.sums + c, b.rep, b.rstride, b.C, r.s, r.s2);
+  }
+  return r;
+}
+__device__ __forceinline__ void bn_finish(const BNRef& b, const BnRaw& r, float& mean, float& invstd) {
+  if (b.eval) {
+    mean = r.rm;
+    invstd = rsqrtf(r.rv + b.eps);
+  } else {  // as bn_moments / bn_coeffs
+    const double m = r.s * (double)b.inv_count;
+    double v = r.s2 * (double)b.inv_count - m * m;
+    if (v < 0) v = 0;
+    mean = (float)m;
+    invstd = rsqrtf((float)v + b.eps);
+  }
+}
+
 template <bool V4>
 __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
   // All edges of a node in one pass: out = sum_e [ sum_k w_e[k] * BN_ek(z_ek) + w_e[id] * x_e ].
@@ -90,9 +124,8 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
   float* sMean = smem;                                 // [ne][kMaxOps][C]
   float* sInv = sMean + ne * kMaxOps * C;              // [ne][kMaxOps][C]
   float* sW = sInv + ne * kMaxOps * C;                 // [ne][kMaxOps + 1]
-  // V4: the first element's operands are loaded BEFORE the coefficient prologue - they do not
-  // depend on it, so their memory round trip overlaps the statistic loads instead of following
-  // the barrier (two serial round trips per block -> one)
+  // V4: the statistic loads go out first, then the first element's operands (which do not depend
+  // on them), then the coefficient math: the two memory round trips of a block overlap
   typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int EM = CombineFwdBatch::kCap;
   const size_t total4 = total / 4;
@@ -108,9 +141,35 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
     }
   };
   size_t i4 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int NE = ne * kMaxOps * C;
+  const bool coop = ne == 1 && a0.nops == 1 && !a0.bn[0].eval && a0.bn[0].rep > 1;
+  const bool split = !coop && NE <= 256;  // one (edge, op, channel) coefficient per thread
+  BnRaw raw{0.0, 0.0, 0.f, 1.f};
+  bool has_raw = false;
+  if (split && (int)threadIdx.x < NE) {
+    const int i = threadIdx.x, e = i / (kMaxOps * C), k = (i / C) % kMaxOps, c = i % C;
+    const CombineFwdArgs& a = bt.e[e];
+    if (k < a.nops) {
+      raw = bn_raw(a.bn[k], c);
+      has_raw = true;
+    }
+  }
+  // the softmax weights of every (edge, op) and identity, issued with the statistics
+  float wv = 0.f;
+  if ((int)threadIdx.x < ne * (kMaxOps + 1)) {
+    const int e = threadIdx.x / (kMaxOps + 1), k = threadIdx.x % (kMaxOps + 1);
+    const CombineFwdArgs& a = bt.e[e];
+    if (k < a.nops) wv = a.w ? a.w[a.widx[k]] : 1.f;
+    else if (k == kMaxOps) wv = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
+  }
   if (V4 && i4 < total4) load4(i4);
   // every (edge, op, channel) coefficient in one pass: one round of statistic loads per block
-  if (ne == 1 && a0.nops == 1 && !a0.bn[0].eval && a0.bn[0].rep > 1) {
+  if (split) {
+    if (has_raw) {
+      const int i = threadIdx.x, e = i / (kMaxOps * C), k = (i / C) % kMaxOps;
+      bn_finish(bt.e[e].bn[k], raw, sMean[i], sInv[i]);
+    }
+  } else if (coop) {
     // a preprocess BN whose statistics arrive unfolded (their fold joins the cell's first node's)
     bn_coeffs_coop(a0.bn[0], 0, C, sMean, sInv);
   } else {
@@ -120,12 +179,7 @@ __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
       if (k < a.nops) bn_coeffs(a.bn[k], c, sMean[i], sInv[i]);
     }
   }
-  for (int i = threadIdx.x; i < ne * (kMaxOps + 1); i += 256) {
-    const int e = i / (kMaxOps + 1), k = i % (kMaxOps + 1);
-    const CombineFwdArgs& a = bt.e[e];
-    if (k < a.nops) sW[i] = a.w ? a.w[a.widx[k]] : 1.f;
-    else if (k == kMaxOps) sW[i] = (a.w && a.id_idx >= 0) ? a.w[a.id_idx] : 0.f;
-  }
+  if ((int)threadIdx.x < ne * (kMaxOps + 1)) sW[threadIdx.x] = wv;  // ne * (kMaxOps + 1) <= 36 < 256
   __syncthreads();
   // running-statistic updates spread over the grid's threads (one (edge, op, channel) each), not
   // looped by block 0: its fp64 moments then delayed that one block's elementwise work - the tail
