@@ -80,40 +80,6 @@ bool stamps_compiled() {
 // ------------------------------------------------------------------------------------------------
 // combine_fwd: out = sum_k w[k] * BN_k(z_k) + wid * x  (elementwise), running stats in block 0
 // ------------------------------------------------------------------------------------------------
-// Split form of bn_coeffs for prologues that overlap the statistic loads with operand loads:
-// bn_raw issues the loads (a folded or eval BN: two loads; unfolded: the replica walk), bn_finish
-// turns them into (mean, 1 / std) after the caller has issued its other loads - s_waitcnt vmcnt is
-// in order, so loads issued AFTER the statistic loads do not delay them.
-struct BnRaw {
-  double s, s2;
-  float rm, rv;
-};
-__device__ __forceinline__ BnRaw bn_raw(const BNRef& b, int c) {
-  BnRaw r{0.0, 0.0, 0.f, 1.f};
-  if (b.eval) {
-    r.rm = b.rmean[c];
-    r.rv = b.rvar[c];
-  } else if (b.rep == 1) {
-    r.s = b.sums[c];
-    r.s2 = b.sums[b.C + c];
-  } else {
-    sum_replicas(b.sums + c, b.rep, b.rstride, b.C, r.s, r.s2);
-  }
-  return r;
-}
-__device__ __forceinline__ void bn_finish(const BNRef& b, const BnRaw& r, float& mean, float& invstd) {
-  if (b.eval) {
-    mean = r.rm;
-    invstd = rsqrtf(r.rv + b.eps);
-  } else {  // as bn_moments / bn_coeffs
-    const double m = r.s * (double)b.inv_count;
-    double v = r.s2 * (double)b.inv_count - m * m;
-    if (v < 0) v = 0;
-    mean = (float)m;
-    invstd = rsqrtf((float)v + b.eps);
-  }
-}
-
 template <bool V4>
 __global__ void __launch_bounds__(256) combine_fwd_kernel(CombineFwdBatch bt) {
   // All edges of a node in one pass: out = sum_e [ sum_k w_e[k] * BN_ek(z_ek) + w_e[id] * x_e ].
