@@ -364,11 +364,14 @@ __global__ void __launch_bounds__(256) fold_rows_kernel(FoldArgs a) {
 // Replica fold for the f64 reductions (BN statistics, BN-backward sums, d alpha): run between a
 // producer and its consumers so that every consumer reads ONE value per channel (rep = 1).
 __global__ void __launch_bounds__(256) fold_f64_kernel(FoldF64Args a) {
-  for (int g = blockIdx.x * 256 + threadIdx.x; g < a.total; g += gridDim.x * 256) {
-    int seg = 0, i = g;
-    while (seg < a.nseg - 1 && i >= a.n[seg]) i -= a.n[seg++];
-    double* p = a.p[seg] + i;
-    const int rs = a.rstride[seg];
+  // one grid row per segment: its pointer / length / stride are wave-uniform kernarg reads. A flat
+  // element index walked the segment table per thread (a dependent, divergent load per segment
+  // passed) before its first replica load could issue
+  const int seg = blockIdx.y;
+  const int n = a.n[seg], rs = a.rstride[seg];
+  double* base = a.p[seg];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    double* p = base + i;
     double v[kRep];
 #pragma unroll
     for (int r = 0; r < kRep; ++r) v[r] = p[(size_t)r * rs];  // all loads in flight together
@@ -382,8 +385,11 @@ __global__ void __launch_bounds__(256) fold_f64_kernel(FoldF64Args a) {
 }
 
 void launch_fold_f64(const FoldF64Args& a, hipStream_t st) {
-  int blocks = std::max(1, std::min((a.total + 255) / 256, 1024));
-  hipLaunchKernelGGL(fold_f64_kernel, dim3(blocks), dim3(256), 0, st, a);
+  if (a.nseg < 1) return;
+  int maxn = 1;
+  for (int s = 0; s < a.nseg; ++s) maxn = std::max(maxn, a.n[s]);
+  const int bx = std::max(1, std::min((maxn + 255) / 256, std::max(1, 1024 / a.nseg)));
+  hipLaunchKernelGGL(fold_f64_kernel, dim3(bx, a.nseg), dim3(256), 0, st, a);
 }
 
 void launch_fold_rows(const FoldArgs& a, hipStream_t st) {
