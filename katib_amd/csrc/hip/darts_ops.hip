@@ -336,7 +336,9 @@ void launch_combine_bwd_reduce(const CombineBwdBatch& b, hipStream_t st) {
     for (int k = 0; k < x.nops; ++k) bits |= (uintptr_t)x.z[k];
     v4 &= (bits & 15) == 0;
   }
-  const dim3 grid(a.C * channel_groups(a.N, a.C, b.n), b.n);
+  // half the persistent-grid budget: two images per workgroup at B5 sizes, so each thread keeps two
+  // elements' operands in flight and the coefficient prologue / reduction tail are paid half as often
+  const dim3 grid(a.C * channel_groups(a.N, a.C, 2 * b.n), b.n);
   if (v4) hipLaunchKernelGGL(combine_bwd_reduce_kernel<true>, grid, dim3(256), 0, st, b);
   else hipLaunchKernelGGL(combine_bwd_reduce_kernel<false>, grid, dim3(256), 0, st, b);
 }
