@@ -1113,7 +1113,7 @@ bool launch_dw_bwd_multi(DwBwdBatch b, hipStream_t st) {
       return false;
     int nb = 1;
     const int G = a.C / C;
-    constexpr int min_wg = 1024;
+    constexpr int min_wg = 512;
     while (nb < 8 && a.H % (2 * nb) == 0 &&
            (dw_plane_floats(a, K, DIL, S, nb, false, C) * 4 > 40 * 1024 || a.N * nb * G * b.n < min_wg))
       nb *= 2;
