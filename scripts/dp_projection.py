@@ -17,9 +17,9 @@ step, one per flat gradient vector), so step(N) = floor(128) + 4 t_rv(N).
 Prints the table; `profiles/dp_projection_r06.log` is its output.
 """
 
-FLOOR_MS = {  # per-rank batch -> measured dp1 step (ms): batch 128 of B5 round 6 (profiles/gpu_round_r06d.log), the rest round 5
-    "b5": {128: 6.11, 64: 4.67, 32: 3.70, 16: 3.32},
-    "default": {128: 41.74, 64: 24.73, 32: 16.60, 16: 12.66},
+FLOOR_MS = {  # per-rank batch -> measured dp1 step (ms), round 6 final kernels (profiles/dp_floors_r06.log)
+    "b5": {128: 5.73, 64: 4.24, 32: 3.41, 16: 3.00},
+    "default": {128: 39.54, 64: 23.28, 32: 15.66, 16: 12.14},
 }
 # SyncBN rendezvous on the step's critical path, measured with 2 ranks (profiles/dp_rendezvous_r06.log): the
 # concurrent Hessian branches fold through two workspaces side by side, so of 175 (B5) / 315 (default)
@@ -66,9 +66,9 @@ def main():
             step = base + rv
             print(f" {n} | {step:7.2f} | {128 * n / step * 1000:8.0f} | {base / step:10.3f}")
     print("\nReading: with the single-workgroup fold rendezvous (4.2 / 5.1 us at 2 / 4 ranks instead of 6.1 / 10.3) and"
-          "\nthe serial count the concurrent Hessian branches really pay (141 of 175 on B5), SyncBN strong scaling of B5"
-          "\nprojects 1.16x / 1.38x / 1.41x at 2 / 4 / 8 GPUs (round 5: 1.09x / 1.13x / 0.95x); the default config 1.62x /"
-          "\n2.33x / 2.89x. Per-rank BN (the reference's DDP semantics) and weak scaling are unchanged in kind.")
+          "\nthe serial count the concurrent Hessian branches really pay (141 of 175 on B5), the round-6 floors"
+          "\n(B5 5.73 ms, default 39.5 ms at batch 128) give the table above; per-rank BN (the reference's DDP"
+          "\nsemantics) and weak scaling are unchanged in kind.")
 
 
 if __name__ == "__main__":
