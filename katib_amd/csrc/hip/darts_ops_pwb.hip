@@ -503,7 +503,7 @@ static bool try_pw_bwd_px(const PwBwdBatch& b, hipStream_t st) {
   const int total = a.N * a.Ho * a.Wo;
   // one pixel per thread: the 4-pixel vector form (pw_bwd_px_kernel<..., true>) measured slower at C = 8
   // (register pressure: 21.7 vs 17.6 us) and neutral at C = 4 on MI355X, so it is not launched
-  const int per_edge = std::max(1, std::min((total + 255) / 256, max_blocks() / std::max(b.n, 1)));
+  const int per_edge = std::max(1, std::min((total + 255) / 256, max_blocks() / std::max(2 * b.n, 1)));
   hipLaunchKernelGGL((pw_bwd_px_kernel<CI, CO, false>), dim3(per_edge, b.n), dim3(256), 0, st, b);
   return true;
 }
