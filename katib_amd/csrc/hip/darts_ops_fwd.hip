@@ -134,7 +134,7 @@ static bool dwpw_multi_prep(DwPwMultiBatch& b, bool& fused, int& maxblk, size_t&
     const int K = (code & 4) ? 5 : 3, DIL = (code & 2) ? 2 : 1, S = (code & 1) ? 2 : 1;
     const bool aligned = ((((uintptr_t)a.x) | (uintptr_t)a.d | (uintptr_t)a.z) & 15) == 0;
     if (split && (!aligned || (a.Ho * a.Wo) % 64 != 0 || a.W % 4 != 0)) return false;
-    int nb = std::max(1, std::min(a.Ho / 4, 1024 / std::max(N * b.n * G, 1)));
+    int nb = std::max(1, std::min(a.Ho / 4, 512 / std::max(N * b.n * G, 1)));
     auto band_bytes = [&](int v) {
       const int BR = (a.Ho + v - 1) / v;
       return ((size_t)plane_head_floats(CG) + (size_t)CG * ((BR - 1) * S + (K - 1) * DIL + 1) * lds_pitch(a.W + 2 * a.pad)) * sizeof(float);
