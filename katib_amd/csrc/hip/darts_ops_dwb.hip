@@ -267,6 +267,93 @@ __device__ __forceinline__ void pool_bwd_body(const PoolBwdArgs& a, const int bx
       for (int j = 0; j < 4; ++j)
         if (j < a.nextra) g += *reinterpret_cast<const f4*>(a.extra[j] + pb + q4);
       const int iy = q4 / W, ix0 = q4 - iy * W;  // 4 pixels of one row (W % 4 == 0)
+      if constexpr (S == 1) {
+        // stride 1: the quad's 3 x 6 window of outputs (rows iy - 1 .. iy + 1, columns ix0 - 1 ..
+        // ix0 + 4; Ho = H, Wo = W) read once - a 16-byte / 4-byte LDS read for the middle four
+        // columns and two scalars per row and array - instead of 9 neighbours x 3 arrays per pixel
+        // (27 reads per row instead of 108 per quad); out-of-range neighbours read as ga = gm = 0 and
+        // tap 255, and the sums run in the per-pixel loop's order
+        float wa[3][6], wm[3][6];
+        unsigned char wt[3][6];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const int oy = iy - 1 + r;
+          const bool rok = oy >= 0 && oy < Ho;
+          const int o = (rok ? oy : 0) * Wo + ix0;
+          const f4 ga4 = *reinterpret_cast<const f4*>(sGa + o), gm4 = *reinterpret_cast<const f4*>(sGm + o);
+          const unsigned t4 = *reinterpret_cast<const unsigned*>(sArg + o);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            wa[r][k + 1] = rok ? ga4[k] : 0.f;
+            wm[r][k + 1] = rok ? gm4[k] : 0.f;
+            wt[r][k + 1] = rok ? (unsigned char)(t4 >> (8 * k)) : 255;
+          }
+          const bool lok = rok && ix0 > 0, hok = rok && ix0 + 4 < Wo;
+          wa[r][0] = lok ? sGa[o - 1] : 0.f;
+          wm[r][0] = lok ? sGm[o - 1] : 0.f;
+          wt[r][0] = lok ? sArg[o - 1] : 255;
+          wa[r][5] = hok ? sGa[o + 4] : 0.f;
+          wm[r][5] = hok ? sGm[o + 4] : 0.f;
+          wt[r][5] = hok ? sArg[o + 4] : 255;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float v = 0.f;
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int cx = 0; cx < 3; ++cx) {  // output (iy - 1 + r, ix0 + t - 1 + cx): tap (2 - r) * 3 + (2 - cx)
+              v += wa[r][t + cx];
+              if (wt[r][t + cx] == (2 - r) * 3 + (2 - cx)) v += wm[r][t + cx];
+            }
+          g[t] += v;
+        }
+        f4* dst = reinterpret_cast<f4*>(a.gx + pb + q4);
+        *dst = a.overwrite ? g : *dst + g;
+        continue;
+      }
+      if constexpr (S == 2) {
+        // stride 2: the quad (ix0 = 4k) meets output columns 2k .. 2k + 2 and output rows m = iy / 2
+        // and, for odd iy, m + 1 - a 2 x 3 window read once (an 8-byte pair + a scalar per row and
+        // array); pixel t reads columns t / 2 .. (t + 1) / 2. Out-of-range outputs read as 0 / tap 255
+        float wa[2][3], wm[2][3];
+        unsigned char wt[2][3];
+        const int m = iy >> 1, k2 = ix0 >> 1;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int oy = m + r;
+          const bool rok = oy < Ho && (r == 0 || (iy & 1));
+          const int o = (rok ? oy : m) * Wo + k2;
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          const f2 ga2 = *reinterpret_cast<const f2*>(sGa + o), gm2 = *reinterpret_cast<const f2*>(sGm + o);
+          const unsigned short t2 = *reinterpret_cast<const unsigned short*>(sArg + o);
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            wa[r][c] = rok ? ga2[c] : 0.f;
+            wm[r][c] = rok ? gm2[c] : 0.f;
+            wt[r][c] = rok ? (unsigned char)(t2 >> (8 * c)) : 255;
+          }
+          const bool hok = rok && k2 + 2 < Wo;
+          wa[r][2] = hok ? sGa[o + 2] : 0.f;
+          wm[r][2] = hok ? sGm[o + 2] : 0.f;
+          wt[r][2] = hok ? sArg[o + 2] : 255;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float v = 0.f;
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = t / 2; c <= (t + 1) / 2; ++c) {  // output (m + r, 2k + c)
+              v += wa[r][c];
+              if (wt[r][c] == (iy - 2 * (m + r) + 1) * 3 + (t - 2 * c + 1)) v += wm[r][c];
+            }
+          g[t] += v;
+        }
+        f4* dst = reinterpret_cast<f4*>(a.gx + pb + q4);
+        *dst = a.overwrite ? g : *dst + g;
+        continue;
+      }
       const int oy_lo = iy - 1 < 0 ? 0 : (iy - 1 + S - 1) / S, oy_hi = min((iy + 1) / S, Ho - 1);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
