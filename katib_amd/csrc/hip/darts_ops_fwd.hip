@@ -199,11 +199,10 @@ bool launch_dwpw_multi(DwPwMultiBatch b, hipStream_t st) {
 
 // workgroups per pool entry, and whether the LDS-staged 4-pixel path applies (lds: its plane bytes)
 static bool pool_fwd_prep(PoolFwdArgs* e, int n, int& maxblk, size_t& lds) {
-  // the LDS-staged 4-pixel path is off: neutral on the B5 step and
-  // 42 -> 68 us per call on the darts-gpu.yaml step (a barrier round trip per staged plane),
-  // profiles/darts_default_ab_r04.log
-  constexpr bool v4_on = false;  // LDS-staged 4-pixel pool forward: measured slower (42 -> 68 us)
-  bool v4 = v4_on;
+  // 4 outputs per thread from a register window loaded straight from global memory (round 6; the
+  // round-4 LDS-staged form was slower: a barrier round trip per staged plane, 42 -> 68 us per call
+  // on the darts-gpu.yaml step, profiles/darts_default_ab_r04.log)
+  bool v4 = true;
   auto al = [](const void* p, uintptr_t m) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & (m - 1)) == 0; };
   maxblk = 0;
   lds = 0;
@@ -211,11 +210,9 @@ static bool pool_fwd_prep(PoolFwdArgs* e, int n, int& maxblk, size_t& lds) {
     PoolFwdArgs& a = e[i];
     a.nblk = a.C * channel_groups(a.N, a.C, n);
     maxblk = std::max(maxblk, a.nblk);
-    lds = std::max(lds, sizeof(float) * a.H * a.W);
-    v4 = v4 && a.W % 4 == 0 && a.Wo % 4 == 0 && al(a.x, 16) && al(a.zavg, 4 * sizeof(zt)) && al(a.zmax, 4 * sizeof(zt)) &&
-         al(a.amax, 4) && sizeof(float) * a.H * a.W <= 32768;
+    v4 = v4 && a.W % 4 == 0 && a.Wo % 4 == 0 && (a.S == 1 || a.W == 2 * a.Wo) && al(a.x, 16) &&
+         al(a.zavg, 4 * sizeof(zt)) && al(a.zmax, 4 * sizeof(zt)) && al(a.amax, 4);
   }
-  if (!v4) lds = 0;
   return v4;
 }
 
