@@ -18,8 +18,8 @@ Prints the table; `profiles/dp_projection_r06.log` is its output.
 """
 
 FLOOR_MS = {  # per-rank batch -> measured dp1 step (ms), round 6 final kernels (profiles/dp_floors_r06.log)
-    "b5": {128: 5.54, 64: 4.11, 32: 3.34, 16: 2.99},
-    "default": {128: 39.48, 64: 23.22, 32: 15.65, 16: 12.16},
+    "b5": {128: 5.33, 64: 3.92, 32: 3.17, 16: 2.87},
+    "default": {128: 38.29, 64: 22.47, 32: 15.21, 16: 11.86},
 }
 # SyncBN rendezvous on the step's critical path, measured with 2 ranks (profiles/dp_rendezvous_r06.log): the
 # concurrent Hessian branches fold through two workspaces side by side, so of 175 (B5) / 315 (default)
@@ -67,7 +67,7 @@ def main():
             print(f" {n} | {step:7.2f} | {128 * n / step * 1000:8.0f} | {base / step:10.3f}")
     print("\nReading: with the single-workgroup fold rendezvous (4.2 / 5.1 us at 2 / 4 ranks instead of 6.1 / 10.3) and"
           "\nthe serial count the concurrent Hessian branches really pay (141 of 175 on B5), the round-6 floors"
-          "\n(B5 5.54 ms, default 39.5 ms at batch 128) give the table above; per-rank BN (the reference's DDP"
+          "\n(B5 5.33 ms, default 38.3 ms at batch 128) give the table above; per-rank BN (the reference's DDP"
           "\nsemantics) and weak scaling are unchanged in kind.")
 
 
